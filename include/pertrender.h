@@ -1,0 +1,174 @@
+/*
+ * pertrender.h — C ABI of the MI355X-native perturbed differentiable renderer
+ * (libpertrender.so, built for gfx950 by pertrenderer_amd/build_native.py).
+ *
+ * Drop-in boundary for the hot path of quentinll/pertrenderer (reference
+ * checkout: randomras/ *.py).  All buffers are device pointers owned by the
+ * caller (PyTorch's caching allocator); the library allocates nothing
+ * persistent.  Every entry point enqueues on the given HIP stream
+ * (hipStream_t passed as void*) and returns 0 on success or a negative
+ * PR_ERR_* code; pr_last_error() returns a thread-local message.
+ *
+ * Layouts are PyTorch3D's: Fragments are (N,H,W,K) row-major, K fastest;
+ * pix_to_face is int64, everything else float32; colours (N,H,W,K,3);
+ * images (N,H,W,4).  P = N*H*W pixels.
+ *
+ * Reference interfaces each entry point replaces (the reference is pure
+ * Python; these are the calls whose tensor work moves here):
+ *   pr_blend_fwd / pr_blend_bwd
+ *       random_rasterizer.py:34-56   smooth_rgb_blend with
+ *       smoothrast.py:136-147        GaussianRast.rasterize  -> randomHeaviside (:12-59)
+ *       smoothagg.py:185-205         GaussianAgg.aggregate   -> randomArgmax   (:10-73)
+ *       smoothagg.py:292-337         log_corrected / prod_corrected
+ *     flags select the fused shader path (RAST|COLOR) or the standalone
+ *     GaussianAgg.aggregate (flags = 0: prob in, weights (N,H,W,K+1) out).
+ *   pr_heaviside_fwd / pr_heaviside_bwd
+ *       smoothrast.py:144-147 GaussianRast.rasterize standalone (randomHeaviside).
+ *   pr_rast_fwd / pr_rast_bwd
+ *       PyTorch3D 0.4.0 rasterize_meshes / its backward, as called by
+ *       MeshRasterizer at experiments/eval.py:165-168 (requirements.txt:7).
+ *   pr_interp_fwd / pr_interp_bwd
+ *       PyTorch3D interpolate_face_attributes used by Meshes.sample_textures
+ *       for TexturesVertex (random_rasterizer.py:170, experiments/eval.py:251).
+ */
+#ifndef PERTRENDER_H_
+#define PERTRENDER_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PR_ABI_VERSION 1
+
+/* error codes */
+#define PR_OK 0
+#define PR_ERR_ARG -1     /* bad shape / null pointer / unsupported value */
+#define PR_ERR_HIP -2     /* HIP launch or runtime error */
+#define PR_ERR_WORKSPACE -3
+
+/* noise sources */
+#define PR_NOISE_PHILOX 0   /* in-kernel Philox4x32-10 keyed by (seed, pixel, slot, sample) */
+#define PR_NOISE_INJECTED 1 /* caller-provided N(0,1) tensors (reference-parity mode) */
+
+/* pr_blend flags */
+#define PR_BLEND_RAST 1  /* probabilities from dists via the perturbed Heaviside (else `prob` input) */
+#define PR_BLEND_COLOR 2 /* colour mix + alpha -> image (else weights (N,H,W,K+1) out) */
+
+typedef struct PRBlendParams {
+  int32_t N, H, W, K;        /* fragment shape */
+  int32_t Sr, Sa;            /* rast / agg Monte-Carlo samples of this call (shard) */
+  int32_t sample_offset_r;   /* global index of this shard's first rast sample (Philox) */
+  int32_t sample_offset_a;   /* global index of this shard's first agg sample (Philox) */
+  float sigma, gamma, alpha, eps;
+  float background[3];
+  int32_t noise_mode;        /* PR_NOISE_* */
+  uint64_t seed_r, seed_a;   /* Philox keys */
+  const float* noise_r;      /* injected: (Sr,N,H,W,K)   */
+  const float* noise_a;      /* injected: (Sa,N,H,W,K+1) */
+  const float* znear;        /* (N,) camera near plane per batch element */
+  const float* zfar;         /* (N,) */
+  int32_t flags;             /* PR_BLEND_* */
+} PRBlendParams;
+
+typedef struct PRBlendFwdArgs {
+  PRBlendParams p;
+  const int64_t* pix_to_face; /* (N,H,W,K); mask = p2f >= 0.  Either this or `mask`. */
+  const uint8_t* mask;        /* (N,H,W,K) bool, used when pix_to_face is NULL */
+  const float* dists;         /* RAST: (N,H,W,K) signed squared distances */
+  const float* prob;          /* !RAST: (N,H,W,K) probabilities */
+  const float* zbuf;          /* (N,H,W,K) */
+  const float* colors;        /* COLOR: (N,H,W,K,3) */
+  float* image;               /* COLOR out: (N,H,W,4) */
+  float* weights;             /* !COLOR out: (N,H,W,K+1) */
+  uint8_t* winners;           /* out: (P,Sa) per-sample argmax index, saved for backward */
+} PRBlendFwdArgs;
+
+typedef struct PRBlendBwdArgs {
+  PRBlendParams p;
+  const int64_t* pix_to_face;
+  const uint8_t* mask;
+  const float* dists;
+  const float* prob;
+  const float* zbuf;
+  const float* colors;
+  const uint8_t* winners;     /* from pr_blend_fwd */
+  const float* grad_image;    /* COLOR: (N,H,W,4) */
+  const float* grad_weights;  /* !COLOR: (N,H,W,K+1) */
+  float* grad_dists;          /* RAST out (N,H,W,K) */
+  float* grad_prob;           /* !RAST out (N,H,W,K) */
+  float* grad_zbuf;           /* out (N,H,W,K) */
+  float* grad_colors;         /* COLOR out (N,H,W,K,3) */
+  float* grad_scalars;        /* out (3,): d sigma, d gamma, d alpha */
+  void* workspace;            /* >= pr_blend_bwd_workspace_size(args) bytes */
+  size_t workspace_bytes;
+} PRBlendBwdArgs;
+
+typedef struct PRHeavisideArgs {
+  int32_t N, H, W, K, Sr, sample_offset_r, noise_mode;
+  float sigma;
+  uint64_t seed_r;
+  const float* noise_r;       /* injected (Sr,N,H,W,K) */
+  const float* dists;         /* (N,H,W,K); the op is applied to D = -dists */
+  float* prob;                /* fwd out (N,H,W,K) */
+  const float* grad_prob;     /* bwd in */
+  float* grad_dists;          /* bwd out */
+  float* grad_sigma;          /* bwd out (1,) */
+  void* workspace;
+  size_t workspace_bytes;
+} PRHeavisideArgs;
+
+typedef struct PRRastArgs {
+  const float* face_verts;          /* (F,3,3): x,y in NDC, z in view space */
+  const int64_t* mesh_first_face;   /* (N,) first packed face of each mesh */
+  const int64_t* mesh_num_faces;    /* (N,) */
+  int64_t F;
+  int32_t N, H, W, K;
+  float blur_radius;                /* squared-distance threshold, as PyTorch3D */
+  int32_t perspective_correct, clip_barycentric_coords, cull_backfaces;
+  /* forward outputs */
+  int64_t* pix_to_face; float* zbuf; float* bary; float* dists;
+  /* backward */
+  const float* grad_zbuf; const float* grad_bary; const float* grad_dists; /* nullable */
+  float* grad_face_verts;           /* (F,3,3), overwritten */
+  void* workspace;
+  size_t workspace_bytes;
+} PRRastArgs;
+
+typedef struct PRInterpArgs {
+  const int64_t* pix_to_face;  /* (P*K) */
+  const float* bary;           /* (P*K,3) */
+  const float* face_attr;      /* (F,3,D) */
+  int64_t PK, F;
+  int32_t D;
+  float* out;                  /* fwd (P*K,D) */
+  const float* grad_out;       /* bwd in (P*K,D) */
+  float* grad_bary;            /* bwd out (P*K,3), nullable */
+  float* grad_face_attr;       /* bwd out (F,3,D), overwritten, nullable */
+} PRInterpArgs;
+
+int pr_abi_version(void);
+const char* pr_last_error(void);
+
+int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream);
+size_t pr_blend_bwd_workspace_size(const PRBlendBwdArgs* args);
+int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream);
+
+int pr_heaviside_fwd(const PRHeavisideArgs* args, void* stream);
+size_t pr_heaviside_bwd_workspace_size(const PRHeavisideArgs* args);
+int pr_heaviside_bwd(const PRHeavisideArgs* args, void* stream);
+
+size_t pr_rast_fwd_workspace_size(const PRRastArgs* args);
+int pr_rast_fwd(const PRRastArgs* args, void* stream);
+size_t pr_rast_bwd_workspace_size(const PRRastArgs* args);
+int pr_rast_bwd(const PRRastArgs* args, void* stream);
+
+int pr_interp_fwd(const PRInterpArgs* args, void* stream);
+int pr_interp_bwd(const PRInterpArgs* args, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PERTRENDER_H_ */

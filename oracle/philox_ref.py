@@ -1,0 +1,78 @@
+"""numpy Philox4x32-10 and the noise streams of the kernels' Philox mode  —  TEST INFRASTRUCTURE ONLY.
+
+Restates Salmon, Moraes, Dror & Shaw, "Parallel random numbers: as easy as 1, 2, 3"
+(SC'11), Philox4x32 with R=10 rounds, as used by pertrenderer_amd/csrc/pr_common.h,
+and the counter layout the kernels use:
+  rast:  counter (pixel, slot, sample // 4, 0x52415354), key = seed_r
+  agg:   counter (pixel, slot, sample // 4, 0x41474752), key = seed_a
+Known-answer vectors from Random123's kat_vectors pin the generator itself.
+"""
+import numpy as np
+
+M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+W0, W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+TAG_RAST, TAG_AGG = 0x52415354, 0x41474752
+_MASK = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(ctr, key):
+    """ctr: (...,4) uint32, key: (...,2) uint32 -> (...,4) uint32."""
+    c = [np.asarray(ctr[..., i], np.uint32) for i in range(4)]
+    k0 = np.asarray(key[..., 0], np.uint32).copy()
+    k1 = np.asarray(key[..., 1], np.uint32).copy()
+    with np.errstate(over="ignore"):
+        for _ in range(10):
+            p0 = M0 * c[0].astype(np.uint64)
+            p1 = M1 * c[2].astype(np.uint64)
+            hi0, lo0 = (p0 >> np.uint64(32)).astype(np.uint32), (p0 & _MASK).astype(np.uint32)
+            hi1, lo1 = (p1 >> np.uint64(32)).astype(np.uint32), (p1 & _MASK).astype(np.uint32)
+            c = [hi1 ^ c[1] ^ k0, lo1, hi0 ^ c[3] ^ k1, lo0]
+            k0 = k0 + W0
+            k1 = k1 + W1
+    return np.stack(c, axis=-1)
+
+
+def u01(r):
+    """(r >> 8 | 1) * 2^-24, exactly as the kernels."""
+    return (((np.asarray(r, np.uint32) >> np.uint32(8)) | np.uint32(1)).astype(np.float32)
+            * np.float32(5.9604644775390625e-08))
+
+
+def block(seed, pixel, slot, group, tag):
+    pixel, slot, group = np.broadcast_arrays(np.asarray(pixel, np.uint32), np.asarray(slot, np.uint32),
+                                             np.asarray(group, np.uint32))
+    ctr = np.stack([pixel, slot, group, np.full(pixel.shape, tag, np.uint32)], axis=-1)
+    key = np.array([seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF], np.uint32)
+    return philox4x32_10(ctr, np.broadcast_to(key, ctr.shape[:-1] + (2,)))
+
+
+def rast_uniforms(seed, P, K, S, offset=0):
+    """(S, P, K) uniforms of the rast stream (samples offset..offset+S-1)."""
+    s = np.arange(offset, offset + S)
+    pix = np.arange(P)[None, :, None]
+    slot = np.arange(K)[None, None, :]
+    words = block(seed, pix, slot, (s // 4)[:, None, None], TAG_RAST)       # (S,P,K,4)
+    r = np.take_along_axis(words, (s % 4)[:, None, None, None].repeat(P, 1).repeat(K, 2), axis=-1)[..., 0]
+    return u01(r)
+
+
+def agg_normals(seed, P, KP1, S, offset=0):
+    """(S, P, K+1) Box-Muller normals of the agg stream (float64 math; the kernels use
+    the hardware log2/sqrt/sin/cos, so values agree to a few ulp)."""
+    s = np.arange(offset, offset + S)
+    groups = np.unique(s // 4)
+    pix = np.arange(P)[:, None]
+    slot = np.arange(KP1)[None, :]
+    out = np.empty((S, P, KP1), np.float64)
+    for g in groups:
+        w = block(seed, pix, slot, g, TAG_AGG)                               # (P,K+1,4)
+        u = u01(w).astype(np.float64)
+        r0 = np.sqrt(-2.0 * np.log(u[..., 0]))
+        r1 = np.sqrt(-2.0 * np.log(u[..., 2]))
+        e = [r0 * np.cos(2 * np.pi * u[..., 1]), r0 * np.sin(2 * np.pi * u[..., 1]),
+             r1 * np.cos(2 * np.pi * u[..., 3]), r1 * np.sin(2 * np.pi * u[..., 3])]
+        for q in range(4):
+            si = 4 * g + q - offset
+            if 0 <= si < S:
+                out[si] = e[q]
+    return out

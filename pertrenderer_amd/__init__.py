@@ -1,0 +1,22 @@
+"""pertrenderer_amd — MI355X-native perturbed differentiable renderer.
+
+Drop-in for quentinll/pertrenderer's ``randomras`` plugin surface (also importable
+as ``randomras``).  The hot path — K-nearest-face rasterization, the Gaussian-
+perturbed Heaviside over signed edge distances and the Monte-Carlo perturbed-
+argmax colour aggregation, forward and backward — runs in hand-written HIP for
+gfx950 (libpertrender.so, C ABI in include/pertrender.h).
+"""
+from . import _native
+from .blend import perturbed_aggregate, perturbed_blend, perturbed_heaviside
+from .noise import Noise, get_noise_source, set_noise_source
+from .random_rasterizer import (RandomPhongShader, RandomSimpleShader, SimpleShader, SoftSimpleShader,
+                                smooth_rgb_blend)
+from .smoothagg import CauchyAgg, GaussianAgg, GaussianAgg_wovr, HardAgg, SoftAgg, UniformAgg
+from .smoothrast import AffineRast, ArctanRast, GaussianRast, GaussianRast_wovr, HardRast, SoftRast
+
+__version__ = "0.1.0"
+
+
+def native_library():
+    """Load libpertrender.so (raises NativeError if it was not built)."""
+    return _native.load()

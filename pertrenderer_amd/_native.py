@@ -1,0 +1,138 @@
+"""ctypes binding of libpertrender.so (the C ABI declared in include/pertrender.h).
+
+The library is the product: every public op of this package calls into it and
+raises if it is missing or the tensors are not on a ROCm device.  There is no
+CPU fallback.
+"""
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpertrender.so")
+
+PR_NOISE_PHILOX = 0
+PR_NOISE_INJECTED = 1
+PR_BLEND_RAST = 1
+PR_BLEND_COLOR = 2
+
+_vp = C.c_void_p
+
+
+class PRBlendParams(C.Structure):
+    _fields_ = [("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("K", C.c_int32),
+                ("Sr", C.c_int32), ("Sa", C.c_int32),
+                ("sample_offset_r", C.c_int32), ("sample_offset_a", C.c_int32),
+                ("sigma", C.c_float), ("gamma", C.c_float), ("alpha", C.c_float), ("eps", C.c_float),
+                ("background", C.c_float * 3), ("noise_mode", C.c_int32),
+                ("seed_r", C.c_uint64), ("seed_a", C.c_uint64),
+                ("noise_r", _vp), ("noise_a", _vp), ("znear", _vp), ("zfar", _vp),
+                ("flags", C.c_int32)]
+
+
+class PRBlendFwdArgs(C.Structure):
+    _fields_ = [("p", PRBlendParams), ("pix_to_face", _vp), ("mask", _vp), ("dists", _vp),
+                ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("image", _vp), ("weights", _vp),
+                ("winners", _vp)]
+
+
+class PRBlendBwdArgs(C.Structure):
+    _fields_ = [("p", PRBlendParams), ("pix_to_face", _vp), ("mask", _vp), ("dists", _vp),
+                ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("winners", _vp),
+                ("grad_image", _vp), ("grad_weights", _vp), ("grad_dists", _vp), ("grad_prob", _vp),
+                ("grad_zbuf", _vp), ("grad_colors", _vp), ("grad_scalars", _vp),
+                ("workspace", _vp), ("workspace_bytes", C.c_size_t)]
+
+
+class PRHeavisideArgs(C.Structure):
+    _fields_ = [("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("K", C.c_int32),
+                ("Sr", C.c_int32), ("sample_offset_r", C.c_int32), ("noise_mode", C.c_int32),
+                ("sigma", C.c_float), ("seed_r", C.c_uint64), ("noise_r", _vp), ("dists", _vp),
+                ("prob", _vp), ("grad_prob", _vp), ("grad_dists", _vp), ("grad_sigma", _vp),
+                ("workspace", _vp), ("workspace_bytes", C.c_size_t)]
+
+
+class PRRastArgs(C.Structure):
+    _fields_ = [("face_verts", _vp), ("mesh_first_face", _vp), ("mesh_num_faces", _vp),
+                ("F", C.c_int64), ("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+                ("K", C.c_int32), ("blur_radius", C.c_float), ("perspective_correct", C.c_int32),
+                ("clip_barycentric_coords", C.c_int32), ("cull_backfaces", C.c_int32),
+                ("pix_to_face", _vp), ("zbuf", _vp), ("bary", _vp), ("dists", _vp),
+                ("grad_zbuf", _vp), ("grad_bary", _vp), ("grad_dists", _vp),
+                ("grad_face_verts", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t)]
+
+
+class PRInterpArgs(C.Structure):
+    _fields_ = [("pix_to_face", _vp), ("bary", _vp), ("face_attr", _vp), ("PK", C.c_int64),
+                ("F", C.c_int64), ("D", C.c_int32), ("out", _vp), ("grad_out", _vp),
+                ("grad_bary", _vp), ("grad_face_attr", _vp)]
+
+
+# every symbol include/pertrender.h declares, with its argument struct (None = no args)
+EXPORTS = {
+    "pr_abi_version": (C.c_int, []),
+    "pr_last_error": (C.c_char_p, []),
+    "pr_blend_fwd": (C.c_int, [C.POINTER(PRBlendFwdArgs), _vp]),
+    "pr_blend_bwd_workspace_size": (C.c_size_t, [C.POINTER(PRBlendBwdArgs)]),
+    "pr_blend_bwd": (C.c_int, [C.POINTER(PRBlendBwdArgs), _vp]),
+    "pr_heaviside_fwd": (C.c_int, [C.POINTER(PRHeavisideArgs), _vp]),
+    "pr_heaviside_bwd_workspace_size": (C.c_size_t, [C.POINTER(PRHeavisideArgs)]),
+    "pr_heaviside_bwd": (C.c_int, [C.POINTER(PRHeavisideArgs), _vp]),
+    "pr_rast_fwd_workspace_size": (C.c_size_t, [C.POINTER(PRRastArgs)]),
+    "pr_rast_fwd": (C.c_int, [C.POINTER(PRRastArgs), _vp]),
+    "pr_rast_bwd_workspace_size": (C.c_size_t, [C.POINTER(PRRastArgs)]),
+    "pr_rast_bwd": (C.c_int, [C.POINTER(PRRastArgs), _vp]),
+    "pr_interp_fwd": (C.c_int, [C.POINTER(PRInterpArgs), _vp]),
+    "pr_interp_bwd": (C.c_int, [C.POINTER(PRInterpArgs), _vp]),
+}
+ABI_VERSION = 1
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load (once) and type the native library.  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeError(
+            f"libpertrender.so not found at {path}; build it with "
+            "`python -m pertrenderer_amd.build_native` (hipcc, gfx950)")
+    lib = C.CDLL(path)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.pr_abi_version() != ABI_VERSION:
+        raise NativeError(f"libpertrender ABI {lib.pr_abi_version()} != {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(code, what):
+    if code != 0:
+        msg = load().pr_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed ({code}): {msg}")
+
+
+def ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    """The current torch stream of `t`'s device, as the hipStream_t handle."""
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise NativeError(
+                "pertrenderer_amd native ops run on ROCm devices only (got a "
+                f"{t.device} tensor); there is no CPU fallback")

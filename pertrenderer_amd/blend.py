@@ -1,0 +1,288 @@
+"""Autograd operators over the native perturbed-blend kernels.
+
+* :func:`perturbed_blend`      — fused smooth_rgb_blend with GaussianRast + GaussianAgg
+  (random_rasterizer.py:34-56 + smoothrast.py:12-59 + smoothagg.py:10-73,185-205):
+  one pr_blend_fwd / pr_blend_bwd launch pair per render.
+* :func:`perturbed_heaviside`  — GaussianRast.rasterize standalone (smoothrast.py:144-147).
+* :func:`perturbed_aggregate`  — GaussianAgg.aggregate standalone (smoothagg.py:196-205).
+
+Gradients follow the reference's custom backward passes, including
+its quirks: d sigma = sum(gmaps * dP) (smoothrast.py:57-58) and |eps|^2 over all K+1
+logits in d gamma (smoothagg.py:54).  sigma / gamma / alpha may be CPU 0-d leaves
+(smoothrast.py:116, smoothagg.py:153-154); their gradients are returned as 0-d
+tensors that autograd moves to the leaves' device.
+"""
+import torch
+
+from . import _native as nat
+from . import noise as noise_mod
+from . import timing as _timing
+from .noise import Noise
+
+F32 = torch.float32
+
+
+def _f(x):
+    return float(x.detach().cpu()) if torch.is_tensor(x) else float(x)
+
+
+def _planes(z, N, device):
+    """znear / zfar as an (N,) float32 device tensor (accepts float, (N,), (N,1,1,1))."""
+    if torch.is_tensor(z):
+        z = z.detach().to(device=device, dtype=F32).reshape(-1)
+        if z.numel() == 1:
+            z = z.expand(N)
+        if z.numel() != N:
+            raise ValueError(f"znear/zfar must have N={N} entries, got {z.numel()}")
+        return z.contiguous()
+    return torch.full((N,), float(z), dtype=F32, device=device)
+
+
+def _background(bg):
+    if torch.is_tensor(bg):
+        bg = bg.detach().cpu().reshape(-1).tolist()
+    bg = [float(v) for v in bg]
+    if len(bg) != 3:
+        raise ValueError("background_color must have 3 entries")
+    return bg
+
+
+def _contig(t, dtype=F32):
+    return t.detach().to(dtype).contiguous()
+
+
+def _params(shape, Sr, Sa, sigma, gamma, alpha, eps, bg, noise, znear, zfar, flags):
+    N, H, W, K = shape
+    p = nat.PRBlendParams()
+    p.N, p.H, p.W, p.K = N, H, W, K
+    p.Sr, p.Sa = int(Sr), int(Sa)
+    p.sample_offset_r, p.sample_offset_a = noise.offset_r, noise.offset_a
+    p.sigma, p.gamma, p.alpha, p.eps = sigma, gamma, alpha, eps
+    for i in range(3):
+        p.background[i] = bg[i]
+    p.noise_mode = noise.mode
+    p.seed_r, p.seed_a = noise.seed_r & (2 ** 64 - 1), noise.seed_a & (2 ** 64 - 1)
+    p.noise_r, p.noise_a = nat.ptr(noise.noise_r), nat.ptr(noise.noise_a)
+    p.znear, p.zfar = nat.ptr(znear), nat.ptr(zfar)
+    p.flags = flags
+    return p
+
+
+def _check_injected(noise, Sr, Sa, shape, need_r, need_a):
+    if noise.mode != nat.PR_NOISE_INJECTED:
+        return
+    N, H, W, K = shape
+    if need_r and (noise.noise_r is None or tuple(noise.noise_r.shape) != (Sr, N, H, W, K)):
+        raise ValueError(f"injected noise_r must have shape {(Sr, N, H, W, K)}")
+    if need_a and (noise.noise_a is None or tuple(noise.noise_a.shape) != (Sa, N, H, W, K + 1)):
+        raise ValueError(f"injected noise_a must have shape {(Sa, N, H, W, K + 1)}")
+
+
+def _scalar_grads(gs, needs, refs):
+    out = []
+    for i, (need, ref) in enumerate(zip(needs, refs)):
+        out.append(gs[i].to(dtype=ref.dtype) if (need and torch.is_tensor(ref)) else None)
+    return out
+
+
+# ============================================================== fused blend
+class _FusedBlendFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dists, zbuf, colors, sigma, gamma, alpha, p2f, znear, zfar, cfg):
+        nat.require_device(dists, zbuf, colors, p2f)
+        lib = nat.load()
+        N, H, W, K = p2f.shape
+        dev = p2f.device
+        p2f_c = p2f.detach().to(torch.int64).contiguous()
+        d_c, z_c, c_c = _contig(dists), _contig(zbuf), _contig(colors)
+        zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
+        noise = cfg["noise"].to(dev)
+        sc = (_f(sigma), _f(gamma), _f(alpha))
+        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], *sc, cfg["eps"], cfg["bg"], noise, zn, zf,
+                    nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR)
+        image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
+        winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
+        a = nat.PRBlendFwdArgs()
+        a.p = p
+        a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
+        a.image, a.winners = nat.ptr(image), nat.ptr(winners)
+        hook = _timing.active()
+        if hook is not None:
+            hook.start("blend_fwd")
+        nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd")
+        if hook is not None:
+            hook.stop("blend_fwd")
+        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, sigma if torch.is_tensor(sigma) else None,
+                              gamma if torch.is_tensor(gamma) else None,
+                              alpha if torch.is_tensor(alpha) else None)
+        ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
+        return image
+
+    @staticmethod
+    def backward(ctx, gimg):
+        p2f_c, d_c, z_c, c_c, zn, zf, winners, sig, gam, alp = ctx.saved_tensors
+        cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
+        lib = nat.load()
+        N, H, W, K = p2f_c.shape
+        dev = p2f_c.device
+        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], *sc, cfg["eps"], cfg["bg"], noise, zn, zf,
+                    nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR)
+        g = gimg.detach().to(F32).contiguous()
+        gd = torch.empty_like(d_c)
+        gz = torch.empty_like(z_c)
+        gc = torch.empty_like(c_c)
+        gsc = torch.empty(3, dtype=F32, device=dev)
+        a = nat.PRBlendBwdArgs()
+        a.p = p
+        a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
+        a.winners, a.grad_image = nat.ptr(winners), nat.ptr(g)
+        a.grad_dists, a.grad_zbuf, a.grad_colors, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gc), nat.ptr(gsc)
+        ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
+        hook = _timing.active()
+        if hook is not None:
+            hook.start("blend_bwd")
+        nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd")
+        if hook is not None:
+            hook.stop("blend_bwd")
+        need = ctx.needs_input_grad
+        s_g, g_g, a_g = _scalar_grads(gsc, need[3:6], (sig, gam, alp))
+        return (gd if need[0] else None, gz if need[1] else None, gc if need[2] else None,
+                s_g, g_g, a_g, None, None, None, None)
+
+
+def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_samples_rast,
+                    nb_samples_agg, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0, zfar=100.0,
+                    noise=None, fixed_noise=False):
+    """smooth_rgb_blend(colors, fragments, GaussianRast, GaussianAgg, ...) as one native op.
+
+    Returns the (N,H,W,4) image; differentiable w.r.t. dists, zbuf, colors and the
+    0-d smoothing tensors sigma, gamma, alpha."""
+    shape = tuple(pix_to_face.shape)
+    N, H, W, K = shape
+    if tuple(colors.shape[:4]) != shape or colors.shape[-1] != 3:
+        raise ValueError(f"colors must be (N,H,W,K,3) = {shape + (3,)}, got {tuple(colors.shape)}")
+    if tuple(dists.shape) != shape or tuple(zbuf.shape) != shape:
+        raise ValueError("dists / zbuf must match pix_to_face's shape")
+    if noise is None:
+        nr = noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device)
+        na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise)
+        noise = Noise(nr.mode, nr.seed_r, na.seed_a, nr.noise_r, na.noise_a, 0, 0)
+    _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
+    cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
+               bg=_background(background), noise=noise)
+    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, pix_to_face, znear, zfar, cfg)
+
+
+# ==================================================== standalone heaviside
+class _HeavisideFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dists, sigma, Sr, noise):
+        nat.require_device(dists)
+        lib = nat.load()
+        N, H, W, K = dists.shape
+        d_c = _contig(dists)
+        noise = noise.to(d_c.device)
+        a = nat.PRHeavisideArgs()
+        a.N, a.H, a.W, a.K, a.Sr = N, H, W, K, int(Sr)
+        a.sample_offset_r, a.noise_mode, a.sigma = noise.offset_r, noise.mode, _f(sigma)
+        a.seed_r, a.noise_r, a.dists = noise.seed_r & (2 ** 64 - 1), nat.ptr(noise.noise_r), nat.ptr(d_c)
+        prob = torch.empty_like(d_c)
+        a.prob = nat.ptr(prob)
+        nat.check(lib.pr_heaviside_fwd(a, nat.stream_of(prob)), "pr_heaviside_fwd")
+        ctx.save_for_backward(d_c, sigma if torch.is_tensor(sigma) else None)
+        ctx.noise, ctx.Sr, ctx.sigma = noise, int(Sr), _f(sigma)
+        return prob
+
+    @staticmethod
+    def backward(ctx, gP):
+        d_c, sig = ctx.saved_tensors
+        lib = nat.load()
+        N, H, W, K = d_c.shape
+        noise = ctx.noise
+        a = nat.PRHeavisideArgs()
+        a.N, a.H, a.W, a.K, a.Sr = N, H, W, K, ctx.Sr
+        a.sample_offset_r, a.noise_mode, a.sigma = noise.offset_r, noise.mode, ctx.sigma
+        a.seed_r, a.noise_r, a.dists = noise.seed_r & (2 ** 64 - 1), nat.ptr(noise.noise_r), nat.ptr(d_c)
+        g = gP.detach().to(F32).contiguous()
+        gd = torch.empty_like(d_c)
+        gs = torch.empty(1, dtype=F32, device=d_c.device)
+        a.grad_prob, a.grad_dists, a.grad_sigma = nat.ptr(g), nat.ptr(gd), nat.ptr(gs)
+        ws = torch.empty(max(1, lib.pr_heaviside_bwd_workspace_size(a)), dtype=torch.uint8, device=d_c.device)
+        a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
+        nat.check(lib.pr_heaviside_bwd(a, nat.stream_of(g)), "pr_heaviside_bwd")
+        need = ctx.needs_input_grad
+        sg = gs[0].to(sig.dtype) if (need[1] and sig is not None) else None
+        return (gd if need[0] else None), sg, None, None
+
+
+def perturbed_heaviside(dists, sigma, nb_samples, noise=None):
+    """GaussianRast.rasterize(dists): P = mean_s H(-dists + sigma*eps_s) (smoothrast.py:144-147)."""
+    if dists.dim() != 4:
+        raise ValueError("dists must be (N,H,W,K)")
+    if noise is None:
+        noise = noise_mod.draw_rast(tuple(dists.shape), nb_samples, dists.device)
+    _check_injected(noise, nb_samples, 0, tuple(dists.shape), True, False)
+    return _HeavisideFn.apply(dists, sigma, int(nb_samples), noise)
+
+
+# ==================================================== standalone aggregate
+class _AggregateFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, zbuf, prob, gamma, alpha, mask, znear, zfar, cfg):
+        nat.require_device(zbuf, prob, mask)
+        lib = nat.load()
+        N, H, W, K = zbuf.shape
+        dev = zbuf.device
+        z_c, p_c = _contig(zbuf), _contig(prob)
+        m_c = mask.detach().to(torch.uint8).contiguous()
+        zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
+        noise = cfg["noise"].to(dev)
+        sc = (1.0, _f(gamma), _f(alpha))
+        p = _params((N, H, W, K), 1, cfg["Sa"], *sc, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf, 0)
+        weights = torch.empty((N, H, W, K + 1), dtype=F32, device=dev)
+        winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
+        a = nat.PRBlendFwdArgs()
+        a.p = p
+        a.mask, a.prob, a.zbuf = nat.ptr(m_c), nat.ptr(p_c), nat.ptr(z_c)
+        a.weights, a.winners = nat.ptr(weights), nat.ptr(winners)
+        nat.check(lib.pr_blend_fwd(a, nat.stream_of(weights)), "pr_blend_fwd(aggregate)")
+        ctx.save_for_backward(z_c, p_c, m_c, zn, zf, winners, gamma if torch.is_tensor(gamma) else None,
+                              alpha if torch.is_tensor(alpha) else None)
+        ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
+        return weights
+
+    @staticmethod
+    def backward(ctx, gW):
+        z_c, p_c, m_c, zn, zf, winners, gam, alp = ctx.saved_tensors
+        cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
+        lib = nat.load()
+        N, H, W, K = z_c.shape
+        dev = z_c.device
+        p = _params((N, H, W, K), 1, cfg["Sa"], *sc, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf, 0)
+        g = gW.detach().to(F32).contiguous()
+        gz, gp = torch.empty_like(z_c), torch.empty_like(p_c)
+        gsc = torch.empty(3, dtype=F32, device=dev)
+        a = nat.PRBlendBwdArgs()
+        a.p = p
+        a.mask, a.prob, a.zbuf, a.winners = nat.ptr(m_c), nat.ptr(p_c), nat.ptr(z_c), nat.ptr(winners)
+        a.grad_weights, a.grad_prob, a.grad_zbuf, a.grad_scalars = nat.ptr(g), nat.ptr(gp), nat.ptr(gz), nat.ptr(gsc)
+        ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
+        nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd(aggregate)")
+        need = ctx.needs_input_grad
+        _, g_g, a_g = _scalar_grads(gsc, (False, need[2], need[3]), (None, gam, alp))
+        return (gz if need[0] else None, gp if need[1] else None, g_g, a_g, None, None, None, None)
+
+
+def perturbed_aggregate(zbuf, zfar, znear, prob_map, mask, gamma, alpha, nb_samples, eps=1e-10,
+                        noise=None, fixed_noise=False):
+    """GaussianAgg.aggregate(zbuf, zfar, znear, prob_map, mask) -> (N,H,W,K+1) weights."""
+    N, H, W, K = zbuf.shape
+    if noise is None:
+        noise = noise_mod.draw_agg((N, H, W, K + 1), nb_samples, zbuf.device, fixed_noise)
+    _check_injected(noise, 0, nb_samples, (N, H, W, K), False, True)
+    mask = mask.expand(N, H, W, K) if mask.shape != zbuf.shape else mask
+    prob_map = prob_map.expand(N, H, W, K) if prob_map.shape != zbuf.shape else prob_map
+    cfg = dict(Sa=int(nb_samples), eps=float(eps), noise=noise)
+    return _AggregateFn.apply(zbuf, prob_map, gamma, alpha, mask, znear, zfar, cfg)

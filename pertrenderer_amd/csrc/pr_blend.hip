@@ -1,0 +1,787 @@
+// Perturbed soft rasterization + perturbed-argmax aggregation (fused blend).
+//
+// Reference semantics (quentinll/pertrenderer, pure Python):
+//   smoothrast.py:12-59   randomHeaviside fwd/bwd   (prob from perturbed signed distances)
+//   smoothagg.py:10-73    randomArgmax fwd/bwd      (Monte-Carlo argmax over K+1 logits)
+//   smoothagg.py:196-205  GaussianAgg.aggregate     (logit assembly, background logit)
+//   smoothagg.py:292-337  log_corrected / prod_corrected backward conventions
+//   random_rasterizer.py:34-56  smooth_rgb_blend    (alpha product, colour mix)
+// Closed-form backward: SURVEY.md §3.2, restated in oracle/blend_oracle.py.
+//
+// MI355X layout: one workgroup (4 waves) owns PB consecutive pixels.  Every
+// fragment byte is read with flat, fully-coalesced loops over the block's
+// contiguous (PB*K)-slot range; per-slot intermediates live in LDS; per-pixel
+// reductions run from LDS; the agg Monte-Carlo loop runs one thread per
+// (pixel, 4-sample Philox group, slot chunk) and combines chunk partials with
+// wave shuffles.  Nothing of size S*P*K is ever materialised: noise is
+// regenerated from Philox (or read from injected tensors in parity mode).
+#include "pr_common.h"
+
+namespace pr {
+namespace {
+
+constexpr float kNegInf = -__builtin_inff();
+
+struct Geo {
+  int64_t P, PK;  // pixels, slots
+  int K, KP1;
+  int PB;         // pixels per block
+};
+
+PR_DEV bool slot_mask(const int64_t* p2f, const uint8_t* mask, int64_t gs) {
+  return p2f ? (p2f[gs] >= 0) : (mask[gs] != 0);
+}
+
+// ---------------------------------------------------------------- rast noise
+// Forward count of "inside" samples for one valid slot.  Injected mode follows
+// smoothrast.py:32-33 literally: H(D + sigma*eps) with H(0)=1.
+template <int NOISE>
+PR_DEV int rast_count(const PRBlendParams& p, float dist, uint32_t gp, int k, int64_t gs, int64_t PK) {
+  int cnt = 0;
+  if constexpr (NOISE == PR_NOISE_INJECTED) {
+    const float D = -dist;
+    for (int s = 0; s < p.Sr; ++s) {
+      const float x = D + p.sigma * p.noise_r[(int64_t)s * PK + gs];
+      cnt += x >= 0.f ? 1 : 0;
+    }
+  } else {
+    const float c = rast_threshold(dist, p.sigma);
+    U4 u{};
+    for (int s = 0; s < p.Sr; ++s) {
+      const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
+      if (s == 0 || (sg & 3u) == 0) u = philox_block(p.seed_r, gp, (uint32_t)k, sg >> 2, kTagRast);
+      cnt += u01(word(u, sg & 3u)) >= c ? 1 : 0;
+    }
+  }
+  return cnt;
+}
+
+// Backward: count and the variance-reduced score sum_s ((m_s - vr) * eps_s) / sigma
+// (smoothrast.py:46,53).  In Philox mode eps = Phi^-1(u) is only evaluated for
+// samples whose decision differs from vr (the term is 0 otherwise).
+template <int NOISE>
+PR_DEV int rast_count_score(const PRBlendParams& p, float dist, uint32_t gp, int k, int64_t gs,
+                            int64_t PK, float& gacc) {
+  int cnt = 0;
+  const float D = -dist;
+  const float vr = heaviside1(D);
+  gacc = 0.f;
+  if constexpr (NOISE == PR_NOISE_INJECTED) {
+    for (int s = 0; s < p.Sr; ++s) {
+      const float e = p.noise_r[(int64_t)s * PK + gs];
+      const float m = heaviside1(D + p.sigma * e);
+      cnt += (int)m;
+      gacc += ((m - vr) * e) / p.sigma;
+    }
+  } else {
+    const float c = rast_threshold(dist, p.sigma);
+    U4 u{};
+    for (int s = 0; s < p.Sr; ++s) {
+      const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
+      if (s == 0 || (sg & 3u) == 0) u = philox_block(p.seed_r, gp, (uint32_t)k, sg >> 2, kTagRast);
+      const float uu = u01(word(u, sg & 3u));
+      const float m = uu >= c ? 1.f : 0.f;
+      cnt += (int)m;
+      if (m != vr) gacc += ((m - vr) * normcdfinvf(uu)) / p.sigma;
+    }
+  }
+  return cnt;
+}
+
+// --------------------------------------------------------------- agg noise
+// 4 consecutive samples [4g, 4g+4) of slot j of pixel gp.  Injected mode reads
+// local sample indices s0.. (sample_offset_a is 0 there).
+template <int NOISE>
+PR_DEV void agg_noise4(const PRBlendParams& p, uint32_t gp, int j, uint32_t g, int64_t P, int KP1,
+                       float e[4]) {
+  if constexpr (NOISE == PR_NOISE_INJECTED) {
+    const int64_t PKa = P * KP1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = (int)(4 * g) + i;
+      e[i] = s < p.Sa ? p.noise_a[(int64_t)s * PKa + (int64_t)gp * KP1 + j] : 0.f;
+    }
+  } else {
+    gauss4(philox_block(p.seed_a, gp, (uint32_t)j, g, kTagAgg), e);
+  }
+}
+
+// sample-group bookkeeping: local samples [0,Sa) map to global [off, off+Sa)
+PR_DEV int agg_first_group(const PRBlendParams& p) { return (p.sample_offset_a) >> 2; }
+PR_DEV int agg_num_groups(const PRBlendParams& p) {
+  return ((p.sample_offset_a + p.Sa - 1) >> 2) - (p.sample_offset_a >> 2) + 1;
+}
+
+// ================================================================== forward
+template <int NOISE, bool RAST, bool COLOR>
+__global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, Geo geo, int NC) {
+  extern __shared__ float smem[];
+  const PRBlendParams& p = a.p;
+  const int K = geo.K, KP1 = geo.KP1, PB = geo.PB;
+  float* A = smem;                       // [PB][KP1] prob, then int win counts
+  float* B = A + PB * KP1;               // [PB][KP1] z_inv, then logits z
+  float* PX = B + PB * KP1;              // [PB][2]   zmax, alpha
+  int* CNT = reinterpret_cast<int*>(A);
+  const int tid = threadIdx.x;
+  const int64_t pix0 = (int64_t)blockIdx.x * PB;
+  const int npix = (int)min((int64_t)PB, geo.P - pix0);
+  if (npix <= 0) return;
+
+  // ---- 1: slots (coalesced): mask, probability, z_inv
+  for (int i = tid; i < npix * K; i += kThreads) {
+    const int pl = i / K, k = i - pl * K;
+    const int64_t gp = pix0 + pl, gs = gp * K + k;
+    const bool m = slot_mask(a.pix_to_face, a.mask, gs);
+    const float mf = m ? 1.f : 0.f;
+    float prob;
+    if constexpr (RAST) {
+      if (m) {
+        const int cnt = rast_count<NOISE>(p, a.dists[gs], (uint32_t)gp, k, gs, geo.PK);
+        prob = ((float)cnt / (float)p.Sr) * mf;
+      } else {
+        prob = 0.f;
+      }
+    } else {
+      prob = a.prob[gs];
+    }
+    const int n = (int)(gp / ((int64_t)p.H * p.W));
+    const float zf = p.zfar[n], zn = p.znear[n];
+    A[pl * KP1 + k] = prob;
+    B[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
+  }
+  __syncthreads();
+
+  // ---- 2: per pixel: alpha = prod(1 - prob), z_max = clamp(max z_inv, eps)
+  if (tid < npix) {
+    float al = 1.f, zm = kNegInf;
+    for (int k = 0; k < K; ++k) {
+      al *= (1.f - A[tid * KP1 + k]);
+      const float zi = B[tid * KP1 + k];
+      if (zi > zm) zm = zi;
+    }
+    PX[tid * 2 + 0] = zm < p.eps ? p.eps : zm;
+    PX[tid * 2 + 1] = al;
+  }
+  __syncthreads();
+
+  // ---- 3: logits z_k = (gamma/alpha)*log prob + z_inv - z_max ; z_K = eps - z_max
+  const float gal = p.gamma / p.alpha;
+  for (int i = tid; i < npix * KP1; i += kThreads) {
+    const int pl = i / KP1, k = i - pl * KP1;
+    const float zmax = PX[pl * 2];
+    float z;
+    if (k < K) {
+      z = gal * logf(A[pl * KP1 + k]) + B[pl * KP1 + k] - zmax;
+    } else {
+      z = p.eps - zmax;
+    }
+    B[pl * KP1 + k] = z;
+    CNT[pl * KP1 + k] = 0;
+  }
+  __syncthreads();
+
+  // ---- 4: Monte-Carlo argmax: thread = (pixel, 4-sample group, slot chunk)
+  {
+    const int ng = agg_num_groups(p), g0 = agg_first_group(p);
+    const int CS = (KP1 + NC - 1) / NC;
+    const int npairs = npix * ng * NC;
+    for (int base = 0; base < npairs; base += kThreads) {
+      const int t = base + tid;
+      const bool act = t < npairs;
+      const int c = t % NC, pg = t / NC;
+      const int pl = act ? pg / ng : 0, gi = act ? pg - (pg / ng) * ng : 0;
+      const uint32_t g = (uint32_t)(g0 + gi);
+      const int64_t gp = pix0 + pl;
+      float best[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
+      int bidx[4] = {-1, -1, -1, -1};
+      if (act) {
+        const int j1 = min(KP1, (c + 1) * CS);
+        for (int j = c * CS; j < j1; ++j) {
+          const float z = B[pl * KP1 + j];
+          if (!(z > kNegInf)) continue;  // -inf logits never win (masked / zero prob)
+          float e[4];
+          if constexpr (NOISE == PR_NOISE_INJECTED) {
+            agg_noise4<NOISE>(p, (uint32_t)gp, j, (uint32_t)gi, geo.P, KP1, e);
+          } else {
+            agg_noise4<NOISE>(p, (uint32_t)gp, j, g, geo.P, KP1, e);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = z + p.gamma * e[q];
+            if (v > best[q]) { best[q] = v; bidx[q] = j; }
+          }
+        }
+      }
+      // combine chunk partials (lanes t..t+NC-1 of one wave), lower index wins ties
+      for (int m = 1; m < NC; m <<= 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float ob = __shfl_xor(best[q], m);
+          const int oi = __shfl_xor(bidx[q], m);
+          if (oi >= 0 && (bidx[q] < 0 || ob > best[q] || (ob == best[q] && oi < bidx[q]))) {
+            best[q] = ob; bidx[q] = oi;
+          }
+        }
+      }
+      if (act && c == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          int s;
+          if constexpr (NOISE == PR_NOISE_INJECTED) s = 4 * gi + q;
+          else s = (int)(4 * g) + q - p.sample_offset_a;
+          if (s < 0 || s >= p.Sa) continue;
+          const int w = bidx[q] < 0 ? K : bidx[q];
+          a.winners[gp * p.Sa + s] = (uint8_t)w;
+          atomicAdd(&CNT[pl * KP1 + w], 1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 5: outputs
+  const float fSa = (float)p.Sa;
+  if constexpr (COLOR) {
+    // 8 lanes per pixel sweep the pixel's contiguous K*3 colours
+    for (int base = 0; base < npix * 8; base += kThreads) {
+      const int t = base + tid;
+      const int pl = t >> 3, l = t & 7;
+      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
+      if (pl < npix) {
+        const int64_t gp = pix0 + pl;
+        const float* col = a.colors + gp * K * 3;
+        for (int k = l; k < K; k += 8) {
+          const float w = (float)CNT[pl * KP1 + k] / fSa;
+          acc0 += w * col[k * 3 + 0];
+          acc1 += w * col[k * 3 + 1];
+          acc2 += w * col[k * 3 + 2];
+        }
+      }
+      for (int m = 1; m < 8; m <<= 1) {
+        acc0 += __shfl_xor(acc0, m);
+        acc1 += __shfl_xor(acc1, m);
+        acc2 += __shfl_xor(acc2, m);
+      }
+      if (pl < npix && l == 0) {
+        const int64_t gp = pix0 + pl;
+        const float wb = (float)CNT[pl * KP1 + K] / fSa;
+        float4 o;
+        o.x = acc0 + wb * p.background[0];
+        o.y = acc1 + wb * p.background[1];
+        o.z = acc2 + wb * p.background[2];
+        o.w = 1.f - PX[pl * 2 + 1];
+        reinterpret_cast<float4*>(a.image)[gp] = o;
+      }
+    }
+  } else {
+    for (int i = tid; i < npix * KP1; i += kThreads) {
+      const int pl = i / KP1, k = i - pl * KP1;
+      a.weights[(pix0 + pl) * KP1 + k] = (float)CNT[pl * KP1 + k] / fSa;
+    }
+  }
+}
+
+// ================================================================= backward
+template <int NOISE, bool RAST, bool COLOR>
+__global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, Geo geo, float* partials) {
+  extern __shared__ float smem[];
+  const PRBlendParams& p = a.p;
+  const int K = geo.K, KP1 = geo.KP1, PB = geo.PB;
+  const int Sa = p.Sa;
+  float* PR = smem;                 // [PB][KP1] prob
+  float* ZZ = PR + PB * KP1;        // [PB][KP1] z_inv -> z
+  float* GM = ZZ + PB * KP1;        // [PB][KP1] rast score mean (gmaps)
+  float* EX = GM + PB * KP1;        // [PB][KP1] exclusive products of (1-prob)
+  float* DW = EX + PB * KP1;        // [PB][KP1] dL/dW
+  float* DZ = DW + PB * KP1;        // [PB][KP1] dL/dz
+  int* CN = reinterpret_cast<int*>(DZ + PB * KP1);  // [PB][KP1] win counts
+  float* AS = reinterpret_cast<float*>(CN + PB * KP1);  // [PB][Sa] a_s
+  float* PX = AS + PB * Sa;         // [PB][8] per-pixel scalars
+  float* RED = PX + PB * 8;         // [kThreads][4] reduction scratch
+  const int tid = threadIdx.x;
+  const int64_t pix0 = (int64_t)blockIdx.x * PB;
+  const int npix = (int)min((int64_t)PB, geo.P - pix0);
+  float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
+  const float gal = p.gamma / p.alpha;
+
+  if (npix > 0) {
+    // ---- B1: slots + background entry: prob, z_inv, rast score, dL/dW
+    for (int i = tid; i < npix * KP1; i += kThreads) {
+      const int pl = i / KP1, k = i - pl * KP1;
+      const int64_t gp = pix0 + pl;
+      CN[pl * KP1 + k] = 0;
+      if (k < K) {
+        const int64_t gs = gp * K + k;
+        const bool m = slot_mask(a.pix_to_face, a.mask, gs);
+        const float mf = m ? 1.f : 0.f;
+        float prob, gm = 0.f;
+        if constexpr (RAST) {
+          if (m) {
+            float gacc;
+            const int cnt = rast_count_score<NOISE>(p, a.dists[gs], (uint32_t)gp, k, gs, geo.PK, gacc);
+            prob = ((float)cnt / (float)p.Sr) * mf;
+            gm = gacc / (float)p.Sr;
+          } else {
+            prob = 0.f;
+          }
+        } else {
+          prob = a.prob[gs];
+        }
+        const int n = (int)(gp / ((int64_t)p.H * p.W));
+        const float zf = p.zfar[n], zn = p.znear[n];
+        PR[pl * KP1 + k] = prob;
+        ZZ[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
+        GM[pl * KP1 + k] = gm;
+        float dw;
+        if constexpr (COLOR) {
+          const float* g = a.grad_image + gp * 4;
+          const float* c = a.colors + gs * 3;
+          dw = (g[0] * c[0] + g[1] * c[1]) + g[2] * c[2];
+        } else {
+          dw = a.grad_weights[gp * KP1 + k];
+        }
+        DW[pl * KP1 + k] = dw;
+      } else {
+        float dw;
+        if constexpr (COLOR) {
+          const float* g = a.grad_image + gp * 4;
+          dw = (g[0] * p.background[0] + g[1] * p.background[1]) + g[2] * p.background[2];
+        } else {
+          dw = a.grad_weights[gp * KP1 + K];
+        }
+        DW[pl * KP1 + K] = dw;
+      }
+    }
+    __syncthreads();
+
+    // ---- B2: per pixel: z_max (first argmax), exclusive products for the alpha grad
+    if (tid < npix) {
+      float zm = kNegInf;
+      int km = 0;
+      for (int k = 0; k < K; ++k) {
+        const float zi = ZZ[tid * KP1 + k];
+        if (zi > zm) { zm = zi; km = k; }
+      }
+      PX[tid * 8 + 0] = zm;                       // raw max
+      PX[tid * 8 + 1] = zm < p.eps ? p.eps : zm;  // clamped
+      PX[tid * 8 + 2] = (float)km;
+      if constexpr (COLOR) {
+        // torch prod backward with zeros: exclusive cumprod forward * reversed (ATen)
+        float suf = 1.f;
+        for (int k = K - 1; k >= 0; --k) {
+          EX[tid * KP1 + k] = suf;
+          suf *= (1.f - PR[tid * KP1 + k]);
+        }
+        float pre = 1.f;
+        for (int k = 0; k < K; ++k) {
+          EX[tid * KP1 + k] = pre * EX[tid * KP1 + k];
+          pre *= (1.f - PR[tid * KP1 + k]);
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- B3: logits
+    for (int i = tid; i < npix * KP1; i += kThreads) {
+      const int pl = i / KP1, k = i - pl * KP1;
+      const float zmax = PX[pl * 8 + 1];
+      ZZ[pl * KP1 + k] = k < K ? gal * logf(PR[pl * KP1 + k]) + ZZ[pl * KP1 + k] - zmax : p.eps - zmax;
+    }
+    __syncthreads();
+
+    // ---- B4: unperturbed argmax j0 over K+1 logits (first index)
+    if (tid < npix) {
+      float zb = kNegInf;
+      int j0 = 0;
+      bool any = false;
+      for (int j = 0; j < KP1; ++j) {
+        const float z = ZZ[tid * KP1 + j];
+        if (!any || z > zb) { zb = z; j0 = j; any = true; }
+      }
+      PX[tid * 8 + 3] = (float)j0;
+    }
+    __syncthreads();
+
+    // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0], win counts
+    for (int i = tid; i < npix * Sa; i += kThreads) {
+      const int pl = i / Sa, s = i - pl * Sa;
+      const int64_t gp = pix0 + pl;
+      const int jw = a.winners[gp * Sa + s];
+      const int j0 = (int)PX[pl * 8 + 3];
+      const float as = DW[pl * KP1 + jw] - DW[pl * KP1 + j0];
+      AS[pl * Sa + s] = as;
+      part_a += as;
+      atomicAdd(&CN[pl * KP1 + jw], 1);
+    }
+    __syncthreads();
+
+    // ---- B6: dz_j = mean_s(a_s * eps_sj / gamma), and sum_s a_s * eps_sj^2 (for d gamma)
+    {
+      const int ng = agg_num_groups(p), g0 = agg_first_group(p);
+      for (int i = tid; i < npix * KP1; i += kThreads) {
+        const int pl = i / KP1, j = i - pl * KP1;
+        const int64_t gp = pix0 + pl;
+        float dz = 0.f, q = 0.f;
+        for (int gi = 0; gi < ng; ++gi) {
+          const uint32_t g = (uint32_t)(g0 + gi);
+          int sbase;
+          if constexpr (NOISE == PR_NOISE_INJECTED) sbase = 4 * gi;
+          else sbase = (int)(4 * g) - p.sample_offset_a;
+          float av[4];
+          bool any = false;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int s = sbase + r;
+            av[r] = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
+            any |= av[r] != 0.f;
+          }
+          if (!any) continue;
+          float e[4];
+          if constexpr (NOISE == PR_NOISE_INJECTED) {
+            agg_noise4<NOISE>(p, (uint32_t)gp, j, (uint32_t)gi, geo.P, KP1, e);
+          } else {
+            agg_noise4<NOISE>(p, (uint32_t)gp, j, g, geo.P, KP1, e);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (av[r] != 0.f) {
+              dz += (av[r] * e[r]) / p.gamma;
+              q += av[r] * (e[r] * e[r]);
+            }
+          }
+        }
+        DZ[pl * KP1 + j] = dz / (float)Sa;
+        part_q += q;
+      }
+    }
+    __syncthreads();
+
+    // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps
+    if (tid < npix) {
+      float s = 0.f;
+      for (int k = 0; k < K; ++k) s += DZ[tid * KP1 + k];
+      float dzm = -s - DZ[tid * KP1 + K];
+      dzm = dzm * (PX[tid * 8 + 0] >= p.eps ? 1.f : 0.f);
+      PX[tid * 8 + 4] = dzm;
+    }
+    __syncthreads();
+
+    // ---- B8: per-slot gradients
+    for (int i = tid; i < npix * K; i += kThreads) {
+      const int pl = i / K, k = i - pl * K;
+      const int64_t gp = pix0 + pl, gs = gp * K + k;
+      const bool m = slot_mask(a.pix_to_face, a.mask, gs);
+      const float mf = m ? 1.f : 0.f;
+      const float dzk = DZ[pl * KP1 + k];
+      const float dzinv = dzk + (k == (int)PX[pl * 8 + 2] ? PX[pl * 8 + 4] : 0.f);
+      const int n = (int)(gp / ((int64_t)p.H * p.W));
+      a.grad_zbuf[gs] = -((dzinv * mf) / (p.zfar[n] - p.znear[n]));
+      const float prob = PR[pl * KP1 + k];
+      const float L = logf(prob);
+      float dL = gal * dzk;
+      if (dL != dL) dL = 0.f;
+      const float lp = __builtin_isinf(L) ? 0.f : L * dzk;
+      if (lp == lp) part_gal += lp;
+      float r = 1.f / prob;
+      if (__builtin_isinf(r)) r = 0.f;
+      float dprob = r * dL;
+      if constexpr (COLOR) {
+        const float ga = a.grad_image[gp * 4 + 3];
+        dprob = -((-ga) * EX[pl * KP1 + k]) + dprob;
+      }
+      if constexpr (RAST) {
+        const float dP = dprob * mf;
+        const float dD = GM[pl * KP1 + k] * dP;
+        a.grad_dists[gs] = -dD;
+        part_sigma += dD;
+      } else {
+        a.grad_prob[gs] = dprob;
+      }
+      if constexpr (COLOR) {
+        const float w = (float)CN[pl * KP1 + k] / (float)Sa;
+        const float* g = a.grad_image + gp * 4;
+        float* dc = a.grad_colors + gs * 3;
+        dc[0] = w * g[0];
+        dc[1] = w * g[1];
+        dc[2] = w * g[2];
+      }
+    }
+  }
+
+  // ---- block reduction of the scalar partials (fixed order -> deterministic)
+  RED[tid * 4 + 0] = part_sigma;
+  RED[tid * 4 + 1] = part_q;
+  RED[tid * 4 + 2] = part_a;
+  RED[tid * 4 + 3] = part_gal;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) RED[tid * 4 + c] += RED[(tid + s) * 4 + c];
+    }
+    __syncthreads();
+  }
+  if (tid < 4) partials[(int64_t)blockIdx.x * 4 + tid] = RED[tid];
+}
+
+// d sigma, d gamma, d alpha from the per-block partials (one workgroup, fixed order)
+__global__ void __launch_bounds__(kThreads) blend_finalize_kernel(const float* partials, int nblk,
+                                                                  PRBlendParams p, int has_rast,
+                                                                  float* out) {
+  __shared__ float red[kThreads * 4];
+  const int tid = threadIdx.x;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = tid; b < nblk; b += kThreads) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] += partials[(int64_t)b * 4 + c];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) red[tid * 4 + c] = acc[c];
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[tid * 4 + c] += red[(tid + s) * 4 + c];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float dsig = red[0], Q = red[1], As = red[2], dgal = red[3];
+    // smoothagg.py:54-56,72 : mean_s sum a_s (|eps_s|^2 - 1) / gamma
+    const float dg1 = ((Q - As) / p.gamma) / (float)p.Sa;
+    out[0] = has_rast ? dsig : 0.f;
+    out[1] = dg1 + dgal / p.alpha;                      // prod_corrected x = gamma/alpha
+    out[2] = -dgal * ((p.gamma / p.alpha) / p.alpha);
+  }
+}
+
+// ====================================================== standalone heaviside
+template <int NOISE>
+__global__ void __launch_bounds__(kThreads) heaviside_fwd_kernel(PRHeavisideArgs a) {
+  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+  PRBlendParams p{};
+  p.Sr = a.Sr; p.sample_offset_r = a.sample_offset_r; p.sigma = a.sigma;
+  p.seed_r = a.seed_r; p.noise_r = a.noise_r;
+  for (int64_t gs = (int64_t)blockIdx.x * kThreads + threadIdx.x; gs < PK;
+       gs += (int64_t)gridDim.x * kThreads) {
+    const int64_t gp = gs / a.K;
+    const int k = (int)(gs - gp * a.K);
+    const int cnt = rast_count<NOISE>(p, a.dists[gs], (uint32_t)gp, k, gs, PK);
+    a.prob[gs] = (float)cnt / (float)a.Sr;
+  }
+}
+
+template <int NOISE>
+__global__ void __launch_bounds__(kThreads) heaviside_bwd_kernel(PRHeavisideArgs a, float* partials) {
+  __shared__ float red[kThreads];
+  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+  PRBlendParams p{};
+  p.Sr = a.Sr; p.sample_offset_r = a.sample_offset_r; p.sigma = a.sigma;
+  p.seed_r = a.seed_r; p.noise_r = a.noise_r;
+  float part = 0.f;
+  for (int64_t gs = (int64_t)blockIdx.x * kThreads + threadIdx.x; gs < PK;
+       gs += (int64_t)gridDim.x * kThreads) {
+    const int64_t gp = gs / a.K;
+    const int k = (int)(gs - gp * a.K);
+    float gacc;
+    rast_count_score<NOISE>(p, a.dists[gs], (uint32_t)gp, k, gs, PK, gacc);
+    const float dD = (gacc / (float)a.Sr) * a.grad_prob[gs];
+    a.grad_dists[gs] = -dD;
+    part += dD;
+  }
+  red[threadIdx.x] = part;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(kThreads) sum_partials_kernel(const float* partials, int n, float* out) {
+  __shared__ float red[kThreads];
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < n; b += kThreads) acc += partials[b];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// ================================================================== host side
+size_t fwd_lds(int PB, int KP1) { return (size_t)(2 * PB * KP1 + 2 * PB) * sizeof(float); }
+size_t bwd_lds(int PB, int KP1, int Sa) {
+  return (size_t)(7 * PB * KP1 + PB * Sa + 8 * PB + kThreads * 4) * sizeof(float);
+}
+constexpr size_t kLdsBudget = 64 * 1024;  // keep >= 2 workgroups (8 waves) per CU
+
+int pick_pb(int KP1, int Sa, bool bwd) {
+  for (int PB = 32; PB >= 1; PB >>= 1) {
+    const size_t b = bwd ? bwd_lds(PB, KP1, Sa) : fwd_lds(PB, KP1);
+    if (b <= kLdsBudget || PB == 1) return PB;
+  }
+  return 1;
+}
+
+int check_params(const PRBlendParams& p, bool need_rast) {
+  if (p.N <= 0 || p.H <= 0 || p.W <= 0 || p.K <= 0) return set_error(PR_ERR_ARG, "blend: empty shape");
+  if (p.K > 255) return set_error(PR_ERR_ARG, "blend: faces_per_pixel must be <= 255");
+  if (p.Sa <= 0 || (need_rast && p.Sr <= 0)) return set_error(PR_ERR_ARG, "blend: nb_samples must be > 0");
+  if (p.noise_mode != PR_NOISE_PHILOX && p.noise_mode != PR_NOISE_INJECTED)
+    return set_error(PR_ERR_ARG, "blend: unknown noise mode");
+  if (p.noise_mode == PR_NOISE_INJECTED && (!p.noise_a || (need_rast && !p.noise_r)))
+    return set_error(PR_ERR_ARG, "blend: injected noise pointers missing");
+  if (p.sample_offset_a < 0 || p.sample_offset_r < 0) return set_error(PR_ERR_ARG, "blend: negative sample offset");
+  if (p.noise_mode == PR_NOISE_INJECTED && (p.sample_offset_a != 0 || p.sample_offset_r != 0))
+    return set_error(PR_ERR_ARG, "blend: injected noise is indexed locally; sample offsets must be 0");
+  if (!p.znear || !p.zfar) return set_error(PR_ERR_ARG, "blend: znear/zfar missing");
+  const int64_t P = (int64_t)p.N * p.H * p.W;
+  if (P >= (int64_t(1) << 32)) return set_error(PR_ERR_ARG, "blend: too many pixels");
+  return PR_OK;
+}
+
+template <int NOISE>
+void launch_fwd(const PRBlendFwdArgs& a, Geo geo, int NC, hipStream_t st, size_t lds, int nblk) {
+  const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
+  if (rast && color) blend_fwd_kernel<NOISE, true, true><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (rast) blend_fwd_kernel<NOISE, true, false><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (color) blend_fwd_kernel<NOISE, false, true><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else blend_fwd_kernel<NOISE, false, false><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+}
+
+template <int NOISE>
+void launch_bwd(const PRBlendBwdArgs& a, Geo geo, hipStream_t st, size_t lds, int nblk, float* part) {
+  const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
+  if (rast && color) blend_bwd_kernel<NOISE, true, true><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (rast) blend_bwd_kernel<NOISE, true, false><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (color) blend_bwd_kernel<NOISE, false, true><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else blend_bwd_kernel<NOISE, false, false><<<nblk, kThreads, lds, st>>>(a, geo, part);
+}
+
+Geo make_geo(const PRBlendParams& p, int PB) {
+  Geo g;
+  g.P = (int64_t)p.N * p.H * p.W;
+  g.PK = g.P * p.K;
+  g.K = p.K;
+  g.KP1 = p.K + 1;
+  g.PB = PB;
+  return g;
+}
+
+int64_t bwd_blocks(const PRBlendParams& p) {
+  const int PB = pick_pb(p.K + 1, p.Sa, true);
+  const int64_t P = (int64_t)p.N * p.H * p.W;
+  return (P + PB - 1) / PB;
+}
+
+}  // namespace
+}  // namespace pr
+
+using namespace pr;
+
+extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
+  if (!args) return set_error(PR_ERR_ARG, "blend_fwd: null args");
+  const PRBlendFwdArgs& a = *args;
+  const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
+  if (int e = check_params(a.p, rast)) return e;
+  if (!a.pix_to_face && !a.mask) return set_error(PR_ERR_ARG, "blend_fwd: need pix_to_face or mask");
+  if (!a.zbuf || !a.winners || (rast && !a.dists) || (!rast && !a.prob) ||
+      (color && (!a.colors || !a.image)) || (!color && !a.weights))
+    return set_error(PR_ERR_ARG, "blend_fwd: missing buffer");
+  const int KP1 = a.p.K + 1;
+  const int PB = pick_pb(KP1, a.p.Sa, false);
+  const Geo geo = make_geo(a.p, PB);
+  // slot chunks per (pixel, sample group) so that ~256 threads share the MC loop
+  const int ng = ((a.p.sample_offset_a + a.p.Sa - 1) >> 2) - (a.p.sample_offset_a >> 2) + 1;
+  int NC = 1;
+  while (NC < 64 && PB * ng * NC * 2 <= kThreads && (KP1 + NC * 2 - 1) / (NC * 2) >= 4) NC <<= 1;
+  const int64_t nblk = (geo.P + PB - 1) / PB;
+  const size_t lds = fwd_lds(PB, KP1);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a.p.noise_mode == PR_NOISE_INJECTED) launch_fwd<PR_NOISE_INJECTED>(a, geo, NC, st, lds, (int)nblk);
+  else launch_fwd<PR_NOISE_PHILOX>(a, geo, NC, st, lds, (int)nblk);
+  return check_launch("blend_fwd");
+}
+
+extern "C" size_t pr_blend_bwd_workspace_size(const PRBlendBwdArgs* args) {
+  if (!args) return 0;
+  return (size_t)bwd_blocks(args->p) * 4 * sizeof(float);
+}
+
+extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
+  if (!args) return set_error(PR_ERR_ARG, "blend_bwd: null args");
+  const PRBlendBwdArgs& a = *args;
+  const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
+  if (int e = check_params(a.p, rast)) return e;
+  if (!a.pix_to_face && !a.mask) return set_error(PR_ERR_ARG, "blend_bwd: need pix_to_face or mask");
+  if (!a.zbuf || !a.winners || !a.grad_zbuf || !a.grad_scalars ||
+      (rast && (!a.dists || !a.grad_dists)) || (!rast && (!a.prob || !a.grad_prob)) ||
+      (color && (!a.colors || !a.grad_image || !a.grad_colors)) || (!color && !a.grad_weights))
+    return set_error(PR_ERR_ARG, "blend_bwd: missing buffer");
+  const size_t need = pr_blend_bwd_workspace_size(args);
+  if (!a.workspace || a.workspace_bytes < need) return set_error(PR_ERR_WORKSPACE, "blend_bwd: workspace too small");
+  const int KP1 = a.p.K + 1;
+  const int PB = pick_pb(KP1, a.p.Sa, true);
+  const Geo geo = make_geo(a.p, PB);
+  const int64_t nblk = (geo.P + PB - 1) / PB;
+  const size_t lds = bwd_lds(PB, KP1, a.p.Sa);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* part = reinterpret_cast<float*>(a.workspace);
+  if (a.p.noise_mode == PR_NOISE_INJECTED) launch_bwd<PR_NOISE_INJECTED>(a, geo, st, lds, (int)nblk, part);
+  else launch_bwd<PR_NOISE_PHILOX>(a, geo, st, lds, (int)nblk, part);
+  if (int e = check_launch("blend_bwd")) return e;
+  blend_finalize_kernel<<<1, kThreads, 0, st>>>(part, (int)nblk, a.p, rast ? 1 : 0, a.grad_scalars);
+  return check_launch("blend_finalize");
+}
+
+static int heaviside_check(const PRHeavisideArgs& a) {
+  if (a.N <= 0 || a.H <= 0 || a.W <= 0 || a.K <= 0 || a.Sr <= 0) return set_error(PR_ERR_ARG, "heaviside: bad shape");
+  if (a.noise_mode == PR_NOISE_INJECTED && !a.noise_r) return set_error(PR_ERR_ARG, "heaviside: noise missing");
+  if (!a.dists) return set_error(PR_ERR_ARG, "heaviside: dists missing");
+  return PR_OK;
+}
+
+static int heaviside_blocks(const PRHeavisideArgs& a) {
+  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+  return (int)std::min<int64_t>((PK + kThreads - 1) / kThreads, 4096);
+}
+
+extern "C" int pr_heaviside_fwd(const PRHeavisideArgs* args, void* stream) {
+  if (!args) return set_error(PR_ERR_ARG, "heaviside_fwd: null args");
+  const PRHeavisideArgs& a = *args;
+  if (int e = heaviside_check(a)) return e;
+  if (!a.prob) return set_error(PR_ERR_ARG, "heaviside_fwd: prob missing");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a.noise_mode == PR_NOISE_INJECTED)
+    heaviside_fwd_kernel<PR_NOISE_INJECTED><<<heaviside_blocks(a), kThreads, 0, st>>>(a);
+  else
+    heaviside_fwd_kernel<PR_NOISE_PHILOX><<<heaviside_blocks(a), kThreads, 0, st>>>(a);
+  return check_launch("heaviside_fwd");
+}
+
+extern "C" size_t pr_heaviside_bwd_workspace_size(const PRHeavisideArgs* args) {
+  if (!args) return 0;
+  return (size_t)heaviside_blocks(*args) * sizeof(float);
+}
+
+extern "C" int pr_heaviside_bwd(const PRHeavisideArgs* args, void* stream) {
+  if (!args) return set_error(PR_ERR_ARG, "heaviside_bwd: null args");
+  const PRHeavisideArgs& a = *args;
+  if (int e = heaviside_check(a)) return e;
+  if (!a.grad_prob || !a.grad_dists || !a.grad_sigma) return set_error(PR_ERR_ARG, "heaviside_bwd: buffer missing");
+  if (!a.workspace || a.workspace_bytes < pr_heaviside_bwd_workspace_size(args))
+    return set_error(PR_ERR_WORKSPACE, "heaviside_bwd: workspace too small");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int nb = heaviside_blocks(a);
+  float* part = reinterpret_cast<float*>(a.workspace);
+  if (a.noise_mode == PR_NOISE_INJECTED)
+    heaviside_bwd_kernel<PR_NOISE_INJECTED><<<nb, kThreads, 0, st>>>(a, part);
+  else
+    heaviside_bwd_kernel<PR_NOISE_PHILOX><<<nb, kThreads, 0, st>>>(a, part);
+  if (int e = check_launch("heaviside_bwd")) return e;
+  sum_partials_kernel<<<1, kThreads, 0, st>>>(part, nb, a.grad_sigma);
+  return check_launch("heaviside_sum");
+}

@@ -1,0 +1,88 @@
+// Shared device helpers for libpertrender (gfx950 / CDNA4, wave64).
+//
+// * Philox4x32-10 counter-based generator (Salmon et al., SC'11): keyed by a
+//   64-bit seed, counter = (pixel, slot, sample-group, stream tag).  One call
+//   yields 4 words = 4 Monte-Carlo samples of one (pixel, slot), so forward and
+//   backward regenerate identical noise without storing it.
+// * Gaussian samples by Box-Muller on the hardware transcendentals
+//   (v_log_f32 = log2, v_sqrt_f32, v_sin/cos_f32 taking revolutions).
+// * Error plumbing for the C ABI (thread-local message).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/pertrender.h"
+
+#define PR_DEV __device__ __forceinline__
+
+namespace pr {
+
+constexpr int kThreads = 256;  // 4 waves per workgroup
+
+// stream tags (4th counter word) so the two draws never share a counter
+constexpr uint32_t kTagRast = 0x52415354u;  // "RAST"
+constexpr uint32_t kTagAgg = 0x41474752u;   // "AGGR"
+
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+PR_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// uniform in (0,1): odd 24-bit integer * 2^-24, exact in fp32, never 0 or 1
+PR_DEV float u01(uint32_t r) { return (float)((r >> 8) | 1u) * 5.9604644775390625e-08f; }
+
+PR_DEV uint32_t word(const U4& u, int i) {
+  return i == 0 ? u.x : (i == 1 ? u.y : (i == 2 ? u.z : u.w));
+}
+
+// 4 N(0,1) samples from one Philox block: two Box-Muller pairs.
+PR_DEV void gauss4(const U4& u, float e[4]) {
+  const float r0 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(u.x)));
+  const float a0 = u01(u.y);
+  const float r1 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(u.z)));
+  const float a1 = u01(u.w);
+  e[0] = r0 * __builtin_amdgcn_cosf(a0);
+  e[1] = r0 * __builtin_amdgcn_sinf(a0);
+  e[2] = r1 * __builtin_amdgcn_cosf(a1);
+  e[3] = r1 * __builtin_amdgcn_sinf(a1);
+}
+
+PR_DEV U4 philox_block(uint64_t seed, uint32_t pixel, uint32_t slot, uint32_t group, uint32_t tag) {
+  return philox4x32_10(U4{pixel, slot, group, tag}, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// --------------------------------------------------------------------- math
+PR_DEV float heaviside1(float x) { return x >= 0.f ? 1.f : 0.f; }  // torch.heaviside(x, 1)
+
+// Rast threshold in Philox mode: the sample is "inside" iff D + sigma*eps >= 0
+// with eps = Phi^-1(u), i.e. iff u >= Phi(-D/sigma) = Phi(dist/sigma).
+PR_DEV float rast_threshold(float dist, float sigma) {
+  const float x = dist / sigma;
+  if (x != x) return 0.f;  // 0/0: D + sigma*eps = 0 -> H(0) = 1
+  return normcdff(x);
+}
+
+template <typename T>
+PR_DEV T ld(const T* p) { return *p; }
+
+}  // namespace pr
+
+// ------------------------------------------------------------------- errors
+namespace pr {
+int set_error(int code, const std::string& msg);
+int check_launch(const char* what);
+}  // namespace pr

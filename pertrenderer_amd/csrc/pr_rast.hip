@@ -1,0 +1,505 @@
+// K-nearest-face mesh rasterizer (forward + backward) and face-attribute
+// interpolation, with the semantics of PyTorch3D 0.4.0's rasterize_meshes
+// (the [p3d] dependency of the reference, requirements.txt:7, called through
+// MeshRasterizer at experiments/eval.py:165-168).  Semantics restated in
+// SURVEY.md §8 a10/a11 and oracle/rast_oracle.c.
+//
+// Forward (MI355X layout): one wave per 8x8 pixel tile, one lane per pixel.
+// The mesh's faces stream through LDS in 64-face chunks; a chunk is culled
+// against the tile's NDC rectangle (expanded face bbox) and compacted with a
+// wave ballot, then every lane tests the surviving faces against its pixel
+// (LDS broadcast reads).  Each lane keeps its K nearest (z, face) keys in a
+// per-lane column of an LDS queue kept sorted by (z, face id), which is exactly
+// PyTorch3D's ordering; barycentrics/distances of the K winners are recomputed
+// once at the end.
+//
+// Backward: flat slot loop; each workgroup pre-reduces its face-gradient
+// contributions in an LDS hash table keyed by face id before one global
+// atomic per (face, component), so hot faces shared by neighbouring pixels
+// do not serialise on global atomics.
+#include "pr_common.h"
+
+namespace pr {
+namespace {
+
+constexpr float kEps = 1e-8f;  // PyTorch3D kEpsilon
+constexpr int kTile = 8;       // 8x8 pixels per wave
+
+struct V2 {
+  float x, y;
+};
+
+PR_DEV float edge_fn(V2 p, V2 a, V2 b) { return (p.x - a.x) * (b.y - a.y) - (p.y - a.y) * (b.x - a.x); }
+
+PR_DEV void bary_fwd(V2 p, V2 v0, V2 v1, V2 v2, float w[3]) {
+  const float area = edge_fn(v2, v0, v1) + kEps;
+  w[0] = edge_fn(p, v1, v2) / area;
+  w[1] = edge_fn(p, v2, v0) / area;
+  w[2] = edge_fn(p, v0, v1) / area;
+}
+
+PR_DEV void persp_fwd(const float b[3], float z0, float z1, float z2, float o[3]) {
+  const float t0 = b[0] * z1 * z2, t1 = z0 * b[1] * z2, t2 = z0 * z1 * b[2];
+  float d = t0 + t1 + t2;
+  d = d > kEps ? d : kEps;
+  o[0] = t0 / d; o[1] = t1 / d; o[2] = t2 / d;
+}
+
+PR_DEV void clip_fwd(const float b[3], float o[3]) {
+  const float w0 = b[0] > 0.f ? b[0] : 0.f, w1 = b[1] > 0.f ? b[1] : 0.f, w2 = b[2] > 0.f ? b[2] : 0.f;
+  float s = w0 + w1 + w2;
+  s = s > 1e-5f ? s : 1e-5f;
+  o[0] = w0 / s; o[1] = w1 / s; o[2] = w2 / s;
+}
+
+// squared distance from p to segment ab
+PR_DEV float seg_dist2(V2 p, V2 a, V2 b) {
+  const float bax = b.x - a.x, bay = b.y - a.y;
+  const float l2 = bax * bax + bay * bay;
+  if (l2 <= kEps) {
+    const float dx = p.x - b.x, dy = p.y - b.y;
+    return dx * dx + dy * dy;
+  }
+  float t = (bax * (p.x - a.x) + bay * (p.y - a.y)) / l2;
+  t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+  const float qx = a.x + t * bax, qy = a.y + t * bay;
+  const float dx = p.x - qx, dy = p.y - qy;
+  return dx * dx + dy * dy;
+}
+
+PR_DEV float tri_dist2(V2 p, V2 v0, V2 v1, V2 v2) {
+  const float e01 = seg_dist2(p, v0, v1), e02 = seg_dist2(p, v0, v2), e12 = seg_dist2(p, v1, v2);
+  float m = e01 < e02 ? e01 : e02;
+  return m < e12 ? m : e12;
+}
+
+PR_DEV float ndc(int i, int S1, int S2) {
+  float range = 2.0f;
+  if (S1 > S2) range = ((float)S1 * range) / (float)S2;
+  const float off = range / 2.0f;
+  return -off + (range * (float)i + off) / (float)S1;
+}
+
+struct FaceRec {  // 64 B, staged through LDS
+  float4 a;  // v0.x v0.y v0.z v1.x
+  float4 b;  // v1.y v1.z v2.x v2.y
+  float4 c;  // v2.z xmin xmax ymin   (bbox grown by sqrt(blur))
+  float4 d;  // ymax valid - -
+};
+
+__global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cull_backfaces, FaceRec* out) {
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < F; f += (int64_t)gridDim.x * blockDim.x) {
+    const float* v = fv + f * 9;
+    const float x0 = v[0], y0 = v[1], z0 = v[2], x1 = v[3], y1 = v[4], z1 = v[5], x2 = v[6], y2 = v[7], z2 = v[8];
+    const float r = sqrtf(blur);
+    const float xmin = fminf(x0, fminf(x1, x2)) - r, xmax = fmaxf(x0, fmaxf(x1, x2)) + r;
+    const float ymin = fminf(y0, fminf(y1, y2)) - r, ymax = fmaxf(y0, fmaxf(y1, y2)) + r;
+    const float zmax = fmaxf(z0, fmaxf(z1, z2));
+    const float area = edge_fn(V2{x0, y0}, V2{x1, y1}, V2{x2, y2});
+    const bool back = area < 0.f;
+    const bool zero_area = area <= kEps && area >= -kEps;
+    const bool valid = !(zmax < 0.f || (cull_backfaces && back) || zero_area);
+    FaceRec rec;
+    rec.a = make_float4(x0, y0, z0, x1);
+    rec.b = make_float4(y1, z1, x2, y2);
+    rec.c = make_float4(z2, xmin, xmax, ymin);
+    rec.d = make_float4(ymax, valid ? 1.f : 0.f, 0.f, 0.f);
+    out[f] = rec;
+  }
+}
+
+PR_DEV bool key_less(float za, int fa, float zb, int fb) { return za < zb || (za == zb && fa < fb); }
+
+// full per-pixel test of one face; returns true and pz if the face is a candidate
+PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, bool persp, bool clip, float& pz) {
+  if (p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x) return false;
+  const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
+  const float z0 = r.a.z, z1 = r.b.y, z2 = r.c.x;
+  float b0[3], b[3], bc[3];
+  bary_fwd(p, v0, v1, v2, b0);
+  if (persp) persp_fwd(b0, z0, z1, z2, b); else { b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; }
+  if (clip) clip_fwd(b, bc); else { bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2]; }
+  pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
+  if (pz < 0.f) return false;
+  const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
+  if (inside) return true;
+  const float d = tri_dist2(p, v0, v1, v2);
+  return d < blur;
+}
+
+__global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* faces) {
+  extern __shared__ float smem[];
+  const int K = a.K;
+  float* qz = smem;                                   // [K][64]
+  int* qf = reinterpret_cast<int*>(qz + K * 64);      // [K][64]
+  FaceRec* fl = reinterpret_cast<FaceRec*>(qf + K * 64);  // [64]
+  const int lane = threadIdx.x;
+  const int n = blockIdx.z;
+  const int row = blockIdx.y * kTile + lane / kTile;
+  const int col = blockIdx.x * kTile + lane % kTile;
+  const int H = a.H, W = a.W;
+  const bool inimg = row < H && col < W;
+  const V2 p{ndc(W - 1 - min(col, W - 1), W, H), ndc(H - 1 - min(row, H - 1), H, W)};
+  // tile rectangle in NDC (pixel centres); +X points left, +Y up
+  const int c0 = blockIdx.x * kTile, c1 = min(c0 + kTile - 1, W - 1);
+  const int r0 = blockIdx.y * kTile, r1 = min(r0 + kTile - 1, H - 1);
+  const float txmax = ndc(W - 1 - c0, W, H), txmin = ndc(W - 1 - c1, W, H);
+  const float tymax = ndc(H - 1 - r0, H, W), tymin = ndc(H - 1 - r1, H, W);
+  const int64_t fb = a.mesh_first_face[n], fe = fb + a.mesh_num_faces[n];
+  const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
+  int qs = 0;
+  for (int64_t base = fb; base < fe; base += 64) {
+    const int64_t f = base + lane;
+    FaceRec r;
+    bool keep = false;
+    if (f < fe) {
+      r = faces[f];
+      keep = r.d.y != 0.f && !(r.c.y > txmax || r.c.z < txmin || r.c.w > tymax || r.d.x < tymin);
+    }
+    const uint64_t bal = __ballot(keep);
+    const int cnt = __popcll(bal);
+    if (keep) {
+      const int idx = __popcll(bal & ((1ull << lane) - 1ull));
+      r.d.z = __int_as_float((int)(f - 0));  // keep the global face id (fits: F < 2^31)
+      fl[idx] = r;
+    }
+    __syncthreads();
+    if (inimg) {
+      for (int i = 0; i < cnt; ++i) {
+        const FaceRec rr = fl[i];
+        float pz;
+        if (!face_test(rr, p, a.blur_radius, persp, clip, pz)) continue;
+        const int fid = __float_as_int(rr.d.z);
+        if (qs == K && !key_less(pz, fid, qz[(K - 1) * 64 + lane], qf[(K - 1) * 64 + lane])) continue;
+        int pos = qs < K ? qs : K - 1;
+        if (qs < K) ++qs;
+        while (pos > 0 && key_less(pz, fid, qz[(pos - 1) * 64 + lane], qf[(pos - 1) * 64 + lane])) {
+          qz[pos * 64 + lane] = qz[(pos - 1) * 64 + lane];
+          qf[pos * 64 + lane] = qf[(pos - 1) * 64 + lane];
+          --pos;
+        }
+        qz[pos * 64 + lane] = pz;
+        qf[pos * 64 + lane] = fid;
+      }
+    }
+    __syncthreads();
+  }
+  if (!inimg) return;
+  const int64_t pix = ((int64_t)n * H + row) * W + col;
+  for (int k = 0; k < K; ++k) {
+    const int64_t o = pix * K + k;
+    if (k < qs) {
+      const int fid = qf[k * 64 + lane];
+      const float* v = a.face_verts + (int64_t)fid * 9;
+      const V2 v0{v[0], v[1]}, v1{v[3], v[4]}, v2{v[6], v[7]};
+      float b0[3], b[3], bc[3];
+      bary_fwd(p, v0, v1, v2, b0);
+      if (persp) persp_fwd(b0, v[2], v[5], v[8], b); else { b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; }
+      if (clip) clip_fwd(b, bc); else { bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2]; }
+      const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
+      const float d = tri_dist2(p, v0, v1, v2);
+      a.pix_to_face[o] = fid;
+      a.zbuf[o] = qz[k * 64 + lane];
+      a.dists[o] = inside ? -d : d;
+      a.bary[o * 3 + 0] = bc[0];
+      a.bary[o * 3 + 1] = bc[1];
+      a.bary[o * 3 + 2] = bc[2];
+    } else {
+      a.pix_to_face[o] = -1;
+      a.zbuf[o] = -1.f;
+      a.dists[o] = -1.f;
+      a.bary[o * 3 + 0] = -1.f;
+      a.bary[o * 3 + 1] = -1.f;
+      a.bary[o * 3 + 2] = -1.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward
+// d/d(p, a, b) of the squared point-segment distance, t held fixed (PyTorch3D form)
+PR_DEV void seg_dist2_bwd(V2 p, V2 a, V2 b, float g, V2& ga, V2& gb) {
+  const float bax = b.x - a.x, bay = b.y - a.y;
+  const float l2 = bax * bax + bay * bay;
+  float t;
+  if (l2 <= kEps) t = 1.f;
+  else {
+    t = (bax * (p.x - a.x) + bay * (p.y - a.y)) / l2;
+    t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+  }
+  const float qx = (1.f - t) * a.x + t * b.x, qy = (1.f - t) * a.y + t * b.y;
+  const float dx = qx - p.x, dy = qy - p.y;
+  ga.x = g * (1.f - t) * 2.f * dx; ga.y = g * (1.f - t) * 2.f * dy;
+  gb.x = g * t * 2.f * dx;         gb.y = g * t * 2.f * dy;
+}
+
+PR_DEV void tri_dist2_bwd(V2 p, V2 v0, V2 v1, V2 v2, float g, V2 gv[3]) {
+  const float e01 = seg_dist2(p, v0, v1), e02 = seg_dist2(p, v0, v2), e12 = seg_dist2(p, v1, v2);
+  gv[0] = V2{0.f, 0.f}; gv[1] = V2{0.f, 0.f}; gv[2] = V2{0.f, 0.f};
+  if (e01 <= e02 && e01 <= e12) seg_dist2_bwd(p, v0, v1, g, gv[0], gv[1]);
+  else if (e02 <= e01 && e02 <= e12) seg_dist2_bwd(p, v0, v2, g, gv[0], gv[2]);
+  else seg_dist2_bwd(p, v1, v2, g, gv[1], gv[2]);
+}
+
+// edge_fn(p, a, b) partials w.r.t. a and b
+PR_DEV void edge_bwd(V2 p, V2 a, V2 b, float g, V2& ga, V2& gb) {
+  ga.x += g * (p.y - b.y);
+  ga.y += g * (b.x - p.x);
+  gb.x += g * (a.y - p.y);
+  gb.y += g * (p.x - a.x);
+}
+
+// b_i = e_i / area, e0 = E(p,v1,v2), e1 = E(p,v2,v0), e2 = E(p,v0,v1), area = E(v2,v0,v1) + eps
+PR_DEV void bary_bwd(V2 p, V2 v0, V2 v1, V2 v2, const float gb[3], V2 gv[3]) {
+  const float area = edge_fn(v2, v0, v1) + kEps;
+  const float e0 = edge_fn(p, v1, v2), e1 = edge_fn(p, v2, v0), e2 = edge_fn(p, v0, v1);
+  const float de0 = gb[0] / area, de1 = gb[1] / area, de2 = gb[2] / area;
+  const float darea = -(gb[0] * e0 + gb[1] * e1 + gb[2] * e2) / (area * area);
+  V2 g0{0.f, 0.f}, g1{0.f, 0.f}, g2{0.f, 0.f};
+  edge_bwd(p, v1, v2, de0, g1, g2);
+  edge_bwd(p, v2, v0, de1, g2, g0);
+  edge_bwd(p, v0, v1, de2, g0, g1);
+  // area = E(v2, v0, v1): also depends on its first argument v2
+  {
+    const V2 a = v0, b = v1, q = v2;
+    g0.x += darea * (q.y - b.y);  g0.y += darea * (b.x - q.x);
+    g1.x += darea * (a.y - q.y);  g1.y += darea * (q.x - a.x);
+    g2.x += darea * (b.y - a.y);  g2.y += darea * (a.x - b.x);
+  }
+  gv[0] = g0; gv[1] = g1; gv[2] = g2;
+}
+
+// o_i = t_i / sum t, t0 = b0 z1 z2, t1 = z0 b1 z2, t2 = z0 z1 b2 (sum clamped at eps)
+PR_DEV void persp_bwd(const float b[3], float z0, float z1, float z2, const float go[3], float gb[3], float gz[3]) {
+  const float t0 = b[0] * z1 * z2, t1 = z0 * b[1] * z2, t2 = z0 * z1 * b[2];
+  const float s = t0 + t1 + t2;
+  float gt[3];
+  if (s > kEps) {
+    const float dot = (go[0] * t0 + go[1] * t1 + go[2] * t2) / (s * s);
+    gt[0] = go[0] / s - dot; gt[1] = go[1] / s - dot; gt[2] = go[2] / s - dot;
+  } else {
+    gt[0] = go[0] / kEps; gt[1] = go[1] / kEps; gt[2] = go[2] / kEps;
+  }
+  gb[0] = gt[0] * z1 * z2; gb[1] = gt[1] * z0 * z2; gb[2] = gt[2] * z0 * z1;
+  gz[0] = gt[1] * b[1] * z2 + gt[2] * z1 * b[2];
+  gz[1] = gt[0] * b[0] * z2 + gt[2] * z0 * b[2];
+  gz[2] = gt[0] * b[0] * z1 + gt[1] * z0 * b[1];
+}
+
+// o_i = max(b_i,0) / max(sum, 1e-5)
+PR_DEV void clip_bwd(const float b[3], const float go[3], float gb[3]) {
+  const float w0 = b[0] > 0.f ? b[0] : 0.f, w1 = b[1] > 0.f ? b[1] : 0.f, w2 = b[2] > 0.f ? b[2] : 0.f;
+  const float s = w0 + w1 + w2;
+  float gw[3];
+  if (s > 1e-5f) {
+    const float dot = (go[0] * w0 + go[1] * w1 + go[2] * w2) / (s * s);
+    gw[0] = go[0] / s - dot; gw[1] = go[1] / s - dot; gw[2] = go[2] / s - dot;
+  } else {
+    gw[0] = go[0] / 1e-5f; gw[1] = go[1] / 1e-5f; gw[2] = go[2] / 1e-5f;
+  }
+  gb[0] = b[0] > 0.f ? gw[0] : 0.f;
+  gb[1] = b[1] > 0.f ? gw[1] : 0.f;
+  gb[2] = b[2] > 0.f ? gw[2] : 0.f;
+}
+
+PR_DEV void slot_grad(const PRRastArgs& a, V2 p, const float* v, int64_t o, float g[9]) {
+  const V2 v0{v[0], v[1]}, v1{v[3], v[4]}, v2{v[6], v[7]};
+  const float z0 = v[2], z1 = v[5], z2 = v[8];
+  const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
+  const float gzb = a.grad_zbuf ? a.grad_zbuf[o] : 0.f;
+  const float gd = a.grad_dists ? a.grad_dists[o] : 0.f;
+  float gbu[3] = {0.f, 0.f, 0.f};
+  if (a.grad_bary) { gbu[0] = a.grad_bary[o * 3]; gbu[1] = a.grad_bary[o * 3 + 1]; gbu[2] = a.grad_bary[o * 3 + 2]; }
+  float bw[3], bp[3], bc[3];
+  bary_fwd(p, v0, v1, v2, bw);
+  if (persp) persp_fwd(bw, z0, z1, z2, bp); else { bp[0] = bw[0]; bp[1] = bw[1]; bp[2] = bw[2]; }
+  if (clip) clip_fwd(bp, bc); else { bc[0] = bp[0]; bc[1] = bp[1]; bc[2] = bp[2]; }
+  const bool inside = bp[0] > 0.f && bp[1] > 0.f && bp[2] > 0.f;
+  V2 gdv[3];
+  tri_dist2_bwd(p, v0, v1, v2, inside ? -gd : gd, gdv);
+  // zbuf = sum_i bc_i z_i
+  float gsum[3] = {gbu[0] + gzb * z0, gbu[1] + gzb * z1, gbu[2] + gzb * z2};
+  float gpp[3] = {gsum[0], gsum[1], gsum[2]};
+  if (clip) clip_bwd(bp, gsum, gpp);
+  float gw[3] = {gpp[0], gpp[1], gpp[2]};
+  float gz[3] = {0.f, 0.f, 0.f};
+  if (persp) persp_bwd(bw, z0, z1, z2, gpp, gw, gz);
+  V2 gbv[3];
+  bary_bwd(p, v0, v1, v2, gw, gbv);
+  g[0] = gbv[0].x + gdv[0].x; g[1] = gbv[0].y + gdv[0].y; g[2] = gzb * bc[0] + gz[0];
+  g[3] = gbv[1].x + gdv[1].x; g[4] = gbv[1].y + gdv[1].y; g[5] = gzb * bc[1] + gz[1];
+  g[6] = gbv[2].x + gdv[2].x; g[7] = gbv[2].y + gdv[2].y; g[8] = gzb * bc[2] + gz[2];
+}
+
+constexpr int kHash = 1024;  // LDS table entries per workgroup
+constexpr int kBwdPix = 32;  // pixels per workgroup
+
+__global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a) {
+  __shared__ int hkey[kHash];
+  __shared__ float hval[kHash * 9];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kHash; i += kThreads) hkey[i] = -1;
+  for (int i = tid; i < kHash * 9; i += kThreads) hval[i] = 0.f;
+  __syncthreads();
+  const int64_t P = (int64_t)a.N * a.H * a.W;
+  const int64_t pix0 = (int64_t)blockIdx.x * kBwdPix;
+  const int npix = (int)min((int64_t)kBwdPix, P - pix0);
+  const int K = a.K;
+  for (int i = tid; i < npix * K; i += kThreads) {
+    const int64_t o = pix0 * K + i;
+    const int64_t f = a.pix_to_face[o];
+    if (f < 0) continue;
+    const int64_t pix = o / K;
+    const int col = (int)(pix % a.W), row = (int)((pix / a.W) % a.H);
+    const V2 p{ndc(a.W - 1 - col, a.W, a.H), ndc(a.H - 1 - row, a.H, a.W)};
+    float g[9];
+    slot_grad(a, p, a.face_verts + f * 9, o, g);
+    // LDS hash pre-reduction
+    uint32_t h = ((uint32_t)f * 2654435761u) & (kHash - 1);
+    bool done = false;
+    for (int probe = 0; probe < 32 && !done; ++probe) {
+      const int cur = atomicCAS(&hkey[h], -1, (int)f);
+      if (cur == -1 || cur == (int)f) {
+#pragma unroll
+        for (int c = 0; c < 9; ++c) atomicAdd(&hval[h * 9 + c], g[c]);
+        done = true;
+      } else {
+        h = (h + 1) & (kHash - 1);
+      }
+    }
+    if (!done) {
+#pragma unroll
+      for (int c = 0; c < 9; ++c) atomicAdd(&a.grad_face_verts[f * 9 + c], g[c]);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < kHash * 9; i += kThreads) {
+    const int e = i / 9;
+    const int f = hkey[e];
+    if (f >= 0) atomicAdd(&a.grad_face_verts[(int64_t)f * 9 + (i - e * 9)], hval[i]);
+  }
+}
+
+// ------------------------------------------------------------ interpolation
+__global__ void interp_fwd_kernel(PRInterpArgs a) {
+  const int64_t total = a.PK * a.D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = i / a.D;
+    const int d = (int)(i - s * a.D);
+    const int64_t f = a.pix_to_face[s];
+    float v = 0.f;
+    if (f >= 0) {
+      const float* w = a.bary + s * 3;
+      const float* at = a.face_attr + f * 3 * a.D;
+      v = (w[0] * at[d] + w[1] * at[a.D + d]) + w[2] * at[2 * a.D + d];
+    }
+    a.out[i] = v;
+  }
+}
+
+__global__ void interp_bwd_kernel(PRInterpArgs a) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < a.PK; s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t f = a.pix_to_face[s];
+    const float* go = a.grad_out + s * a.D;
+    if (f < 0) {
+      if (a.grad_bary) { a.grad_bary[s * 3] = 0.f; a.grad_bary[s * 3 + 1] = 0.f; a.grad_bary[s * 3 + 2] = 0.f; }
+      continue;
+    }
+    const float* w = a.bary + s * 3;
+    const float* at = a.face_attr + f * 3 * a.D;
+    float gb[3] = {0.f, 0.f, 0.f};
+    for (int d = 0; d < a.D; ++d) {
+      const float g = go[d];
+      gb[0] += g * at[d]; gb[1] += g * at[a.D + d]; gb[2] += g * at[2 * a.D + d];
+      if (a.grad_face_attr) {
+        atomicAdd(&a.grad_face_attr[f * 3 * a.D + d], w[0] * g);
+        atomicAdd(&a.grad_face_attr[f * 3 * a.D + a.D + d], w[1] * g);
+        atomicAdd(&a.grad_face_attr[f * 3 * a.D + 2 * a.D + d], w[2] * g);
+      }
+    }
+    if (a.grad_bary) { a.grad_bary[s * 3] = gb[0]; a.grad_bary[s * 3 + 1] = gb[1]; a.grad_bary[s * 3 + 2] = gb[2]; }
+  }
+}
+
+int rast_check(const PRRastArgs& a) {
+  if (a.N <= 0 || a.H <= 0 || a.W <= 0 || a.K <= 0) return set_error(PR_ERR_ARG, "rast: bad shape");
+  if (a.F < 0 || a.F >= (int64_t(1) << 31)) return set_error(PR_ERR_ARG, "rast: face count out of range");
+  if (!a.face_verts && a.F > 0) return set_error(PR_ERR_ARG, "rast: face_verts missing");
+  if (!a.mesh_first_face || !a.mesh_num_faces) return set_error(PR_ERR_ARG, "rast: mesh index missing");
+  if (a.K > 512) return set_error(PR_ERR_ARG, "rast: faces_per_pixel must be <= 512");
+  if ((int64_t)a.H > 65535 * kTile || (int64_t)a.W > 65535 * kTile || a.N > 65535)
+    return set_error(PR_ERR_ARG, "rast: image too large");
+  return PR_OK;
+}
+
+}  // namespace
+}  // namespace pr
+
+using namespace pr;
+
+extern "C" size_t pr_rast_fwd_workspace_size(const PRRastArgs* a) {
+  if (!a) return 0;
+  return (size_t)(a->F > 0 ? a->F : 1) * sizeof(FaceRec);
+}
+
+extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
+  if (!args) return set_error(PR_ERR_ARG, "rast_fwd: null args");
+  const PRRastArgs& a = *args;
+  if (int e = rast_check(a)) return e;
+  if (!a.pix_to_face || !a.zbuf || !a.bary || !a.dists) return set_error(PR_ERR_ARG, "rast_fwd: output missing");
+  if (!a.workspace || a.workspace_bytes < pr_rast_fwd_workspace_size(args))
+    return set_error(PR_ERR_WORKSPACE, "rast_fwd: workspace too small");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  FaceRec* fr = reinterpret_cast<FaceRec*>(a.workspace);
+  if (a.F > 0) {
+    const int nb = (int)std::min<int64_t>((a.F + kThreads - 1) / kThreads, 1024);
+    face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr);
+    if (int e = check_launch("rast_face_prep")) return e;
+  }
+  dim3 grid((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, a.N);
+  const size_t lds = (size_t)a.K * 64 * 8 + 64 * sizeof(FaceRec);
+  rast_fwd_kernel<<<grid, 64, lds, st>>>(a, fr);
+  return check_launch("rast_fwd");
+}
+
+extern "C" size_t pr_rast_bwd_workspace_size(const PRRastArgs*) { return 0; }
+
+extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
+  if (!args) return set_error(PR_ERR_ARG, "rast_bwd: null args");
+  const PRRastArgs& a = *args;
+  if (int e = rast_check(a)) return e;
+  if (!a.pix_to_face || !a.grad_face_verts) return set_error(PR_ERR_ARG, "rast_bwd: buffer missing");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a.F > 0) {
+    if (hipMemsetAsync(a.grad_face_verts, 0, (size_t)a.F * 9 * sizeof(float), st) != hipSuccess)
+      return set_error(PR_ERR_HIP, "rast_bwd: memset failed");
+  }
+  const int64_t P = (int64_t)a.N * a.H * a.W;
+  const int64_t nb = (P + kBwdPix - 1) / kBwdPix;
+  rast_bwd_kernel<<<(int)nb, kThreads, 0, st>>>(a);
+  return check_launch("rast_bwd");
+}
+
+extern "C" int pr_interp_fwd(const PRInterpArgs* args, void* stream) {
+  if (!args || !args->pix_to_face || !args->bary || !args->face_attr || !args->out || args->D <= 0)
+    return set_error(PR_ERR_ARG, "interp_fwd: bad args");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t total = args->PK * args->D;
+  if (total == 0) return PR_OK;
+  const int nb = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 8192);
+  interp_fwd_kernel<<<nb, kThreads, 0, st>>>(*args);
+  return check_launch("interp_fwd");
+}
+
+extern "C" int pr_interp_bwd(const PRInterpArgs* args, void* stream) {
+  if (!args || !args->pix_to_face || !args->bary || !args->face_attr || !args->grad_out || args->D <= 0)
+    return set_error(PR_ERR_ARG, "interp_bwd: bad args");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (args->grad_face_attr && args->F > 0) {
+    if (hipMemsetAsync(args->grad_face_attr, 0, (size_t)args->F * 3 * args->D * sizeof(float), st) != hipSuccess)
+      return set_error(PR_ERR_HIP, "interp_bwd: memset failed");
+  }
+  if (args->PK == 0) return PR_OK;
+  const int nb = (int)std::min<int64_t>((args->PK + kThreads - 1) / kThreads, 8192);
+  interp_bwd_kernel<<<nb, kThreads, 0, st>>>(*args);
+  return check_launch("interp_bwd");
+}

@@ -1,0 +1,89 @@
+"""Noise sources for the perturbed operators.
+
+Two sources, selected globally with :func:`set_noise_source` or per call with a
+:class:`Noise` object:
+
+``"philox"`` (default, production)
+    In-kernel Philox4x32-10.  Each operator call draws one 62-bit key from
+    torch's default CPU generator (so ``torch.manual_seed`` makes runs
+    reproducible, and the rast draw precedes the agg draw exactly as in the
+    reference: smoothrast.py:21 then smoothagg.py:21).  Noise is a pure function
+    of (key, pixel, slot, sample): nothing of size S x P x K is stored, the
+    backward regenerates it, and disjoint sample ranges (``sample_offset``)
+    give independent shards for multi-GPU sample parallelism.
+
+``"torch"`` (reference parity)
+    The N(0,1) tensors are drawn on the CPU with ``torch.randn`` in the shapes
+    and order the reference draws them ((Sr,N,H,W,K) then (Sa,N,H,W,K+1),
+    including ``fixed_noise``'s ``torch.manual_seed(1)``), copied to the device
+    and read by the kernels.  With the same seed this reproduces the
+    reference's CPU outputs.
+"""
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _native as nat
+
+_SOURCE = "philox"
+SOURCES = ("philox", "torch")
+
+
+def set_noise_source(name):
+    global _SOURCE
+    if name not in SOURCES:
+        raise ValueError(f"noise source must be one of {SOURCES}, got {name!r}")
+    _SOURCE = name
+
+
+def get_noise_source():
+    return _SOURCE
+
+
+def draw_key(generator=None):
+    """One 62-bit Philox key from torch's (CPU) generator."""
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, generator=generator).item())
+
+
+@dataclass
+class Noise:
+    """Noise of one operator call (kept by autograd for the backward)."""
+    mode: int
+    seed_r: int = 0
+    seed_a: int = 0
+    noise_r: Optional[torch.Tensor] = None
+    noise_a: Optional[torch.Tensor] = None
+    offset_r: int = 0
+    offset_a: int = 0
+
+    @staticmethod
+    def philox(seed_r=0, seed_a=0, offset_r=0, offset_a=0):
+        return Noise(nat.PR_NOISE_PHILOX, int(seed_r), int(seed_a), None, None, int(offset_r),
+                     int(offset_a))
+
+    @staticmethod
+    def injected(noise_r=None, noise_a=None):
+        return Noise(nat.PR_NOISE_INJECTED, 0, 0, noise_r, noise_a, 0, 0)
+
+    def to(self, device):
+        mv = (lambda t: None if t is None else t.to(device=device, dtype=torch.float32).contiguous())
+        return Noise(self.mode, self.seed_r, self.seed_a, mv(self.noise_r), mv(self.noise_a),
+                     self.offset_r, self.offset_a)
+
+
+def draw_rast(shape, Sr, device):
+    """Noise for one perturbed-Heaviside call over fragments of `shape` (N,H,W,K)."""
+    if _SOURCE == "torch":
+        return Noise.injected(noise_r=torch.randn((Sr,) + tuple(shape)).to(device))
+    return Noise.philox(seed_r=draw_key())
+
+
+def draw_agg(shape, Sa, device, fixed_noise=False):
+    """Noise for one perturbed-argmax call over logits of `shape` (N,H,W,K+1).
+    fixed_noise reseeds the global generator with 1 first, as smoothagg.py:18-19."""
+    if fixed_noise:
+        torch.manual_seed(1)
+    if _SOURCE == "torch":
+        return Noise.injected(noise_a=torch.randn((Sa,) + tuple(shape)).to(device))
+    return Noise.philox(seed_a=draw_key())

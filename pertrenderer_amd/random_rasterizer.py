@@ -1,0 +1,190 @@
+"""Shader plugins and the blend — the reference's ``randomras.random_rasterizer`` surface.
+
+``smooth_rgb_blend`` has the signature and outputs of random_rasterizer.py:34-56.
+When it is handed a (GaussianRast, GaussianAgg) pair it runs ONE fused native
+kernel pair (pr_blend_fwd/bwd) instead of the two-call split; any other pair goes
+through the two duck-typed methods ``smoothrast.rasterize`` / ``smoothagg.aggregate``
+exactly as the reference composes them.
+
+RandomSimpleShader / RandomPhongShader (random_rasterizer.py:60-191) are
+``MeshRenderer`` shaders with the same constructor arguments, attributes and
+smoothing mutators.  SimpleShader / SoftSimpleShader (random_rasterizer.py:194-214)
+wrap the hard / softmax blends.
+"""
+import torch
+import torch.nn as nn
+
+from . import blend as _blend
+from .renderer.cameras import OpenGLPerspectiveCameras, look_at_view_transform
+from .renderer.renderer import BlendParams, Materials, PointLights
+from .renderer.shading import phong_shading
+from .smoothagg import GaussianAgg, SoftAgg
+from .smoothrast import GaussianRast, SoftRast
+
+
+def _is_fusable(smoothrast, smoothagg, fragments):
+    return (type(smoothrast) is GaussianRast and type(smoothagg) is GaussianAgg
+            and fragments.pix_to_face.is_cuda)
+
+
+def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, znear=1.0, zfar=100):
+    """(N,H,W,K,3) colours + Fragments -> (N,H,W,4) RGBA (random_rasterizer.py:34-56)."""
+    N, H, W, K = fragments.pix_to_face.shape
+    device = fragments.pix_to_face.device
+    background = blend_params.background_color
+    if _is_fusable(smoothrast, smoothagg, fragments):
+        return _blend.perturbed_blend(
+            colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
+            smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
+            eps=smoothagg.eps, background=background, znear=znear, zfar=zfar,
+            fixed_noise=smoothagg.fixed_noise)
+    if not torch.is_tensor(background):
+        background = torch.tensor(background, dtype=torch.float32, device=device)
+    else:
+        background = background.to(device)
+    mask = fragments.pix_to_face >= 0
+    prob_map = smoothrast.rasterize(fragments.dists) * mask
+    alpha_chan = torch.prod(1.0 - prob_map, dim=-1)
+    weights = smoothagg.aggregate(fragments.zbuf, zfar, znear, prob_map, mask)
+    rgb = (weights[..., :-1, None] * colors).sum(dim=-2) + weights[..., -1:] * background
+    return torch.cat([rgb, (1.0 - alpha_chan)[..., None]], dim=-1)
+
+
+def _planes_from(cameras, kwargs):
+    znear = kwargs.get("znear", getattr(cameras, "znear", 1.0))
+    zfar = kwargs.get("zfar", getattr(cameras, "zfar", 100.0))
+    shape = lambda z: z[:, None, None, None] if torch.is_tensor(z) and z.dim() == 1 else z
+    return shape(znear), shape(zfar)
+
+
+class _RandomShaderBase(nn.Module):
+    def get_smoothing(self):
+        return self.smoothrast.sigma, self.smoothagg.gamma, self.smoothagg.alpha
+
+    def get_nb_samples(self):
+        return self.smoothagg.nb_samples
+
+    def update_smoothing(self, sigma=4e-4, gamma=4e-2, alpha=1.0):
+        self.smoothrast.update_smoothing(sigma)
+        self.smoothagg.update_smoothing(gamma, alpha)
+
+    def update_nb_samples(self, nb_samples=16):
+        self.smoothrast.update_nb_samples(nb_samples)
+        self.smoothagg.update_nb_samples(nb_samples)
+
+
+class RandomPhongShader(_RandomShaderBase):
+    """Phong-lit texels blended with the perturbed operators (random_rasterizer.py:60-130)."""
+
+    def __init__(self, device="cpu", cameras=None, lights=None, materials=None, smoothrast=SoftRast(),
+                 smoothagg=SoftAgg(), blend_params=None):
+        super().__init__()
+        self.lights = lights if lights is not None else PointLights(device=device)
+        self.materials = materials if materials is not None else Materials(device=device)
+        self.cameras = cameras
+        self.blend_params = blend_params if blend_params is not None else BlendParams()
+        self.smoothrast = smoothrast
+        self.smoothagg = smoothagg
+
+    def to(self, device):
+        self.cameras = self.cameras.to(device)
+        self.materials = self.materials.to(device)
+        self.lights = self.lights.to(device)
+        return self
+
+    def forward(self, fragments, meshes, **kwargs):
+        cameras = kwargs.get("cameras", self.cameras)
+        if cameras is None:
+            raise ValueError("Cameras must be specified either at initialization or in the forward "
+                             "pass of RandomPhongShader")
+        texels = meshes.sample_textures(fragments)
+        lights = kwargs.get("lights", self.lights)
+        materials = kwargs.get("materials", self.materials)
+        blend_params = kwargs.get("blend_params", self.blend_params)
+        colors = phong_shading(meshes=meshes, fragments=fragments, texels=texels, lights=lights,
+                               cameras=cameras, materials=materials)
+        znear, zfar = _planes_from(cameras, kwargs)
+        return smooth_rgb_blend(colors, fragments, self.smoothrast, self.smoothagg, blend_params,
+                                znear=znear, zfar=zfar)
+
+
+class RandomSimpleShader(_RandomShaderBase):
+    """Unlit texels blended with the perturbed operators (random_rasterizer.py:132-191)."""
+
+    def __init__(self, device="cpu", cameras=None, lights=None, materials=None, smoothrast=SoftRast(),
+                 smoothagg=SoftAgg(), blend_params=None):
+        super().__init__()
+        self.lights = lights if lights is not None else PointLights(device=device)
+        self.materials = materials if materials is not None else Materials(device=device)
+        if cameras is not None:
+            self.cameras = cameras
+        else:
+            R, T = look_at_view_transform(dist=2.7, elev=torch.zeros((1)), azim=torch.zeros((1)))
+            self.cameras = OpenGLPerspectiveCameras(device=device, R=R, T=T)
+        self.blend_params = blend_params if blend_params is not None else BlendParams()
+        self.smoothrast = smoothrast
+        self.smoothagg = smoothagg
+
+    def to(self, device):
+        self.cameras = None if self.cameras is None else self.cameras.to(device)
+        self.materials = self.materials.to(device)
+        self.lights = None if self.lights is None else self.lights.to(device)
+        return self
+
+    def forward(self, fragments, meshes, **kwargs):
+        cameras = kwargs.get("cameras", self.cameras)
+        if cameras is None:
+            raise ValueError("Cameras must be specified either at initialization or in the forward "
+                             "pass of RandomSimpleShader")
+        texels = meshes.sample_textures(fragments)
+        blend_params = kwargs.get("blend_params", self.blend_params)
+        znear, zfar = _planes_from(cameras, kwargs)
+        return smooth_rgb_blend(texels, fragments, self.smoothrast, self.smoothagg, blend_params,
+                                znear=znear, zfar=zfar)
+
+
+def hard_rgb_blend(colors, fragments, blend_params):
+    """Nearest-face colour, background where no face covers the pixel (PyTorch3D hard_rgb_blend)."""
+    N, H, W, K = fragments.pix_to_face.shape
+    bg = blend_params.background_color
+    bg = bg.to(colors.device) if torch.is_tensor(bg) else torch.tensor(bg, dtype=colors.dtype, device=colors.device)
+    is_bg = (fragments.pix_to_face[..., 0] < 0)[..., None]
+    rgb = torch.where(is_bg, bg.expand(N, H, W, 3), colors[..., 0, :])
+    return torch.cat([rgb, (~is_bg).to(colors.dtype)], dim=-1)
+
+
+def softmax_rgb_blend(colors, fragments, blend_params, znear=1.0, zfar=100):
+    """SoftRas softmax blend (PyTorch3D softmax_rgb_blend)."""
+    N, H, W, K = fragments.pix_to_face.shape
+    bg = blend_params.background_color
+    bg = bg.to(colors.device) if torch.is_tensor(bg) else torch.tensor(bg, dtype=colors.dtype, device=colors.device)
+    mask = fragments.pix_to_face >= 0
+    prob = torch.sigmoid(-fragments.dists / blend_params.sigma) * mask
+    alpha = torch.prod(1.0 - prob, dim=-1)
+    z_inv = (zfar - fragments.zbuf) / (zfar - znear) * mask
+    z_inv_max = torch.max(z_inv, dim=-1).values[..., None].clamp(min=1e-10)
+    w = prob * torch.exp((z_inv - z_inv_max) / blend_params.gamma)
+    delta = torch.exp((1e-10 - z_inv_max) / blend_params.gamma).clamp(min=1e-10)
+    denom = w.sum(dim=-1)[..., None] + delta
+    rgb = ((w[..., None] * colors).sum(dim=-2) + delta * bg) / denom
+    return torch.cat([rgb, (1.0 - alpha)[..., None]], dim=-1)
+
+
+class SimpleShader(nn.Module):
+    def __init__(self, device="cpu", blend_params=None):
+        super().__init__()
+        self.blend_params = blend_params if blend_params is not None else BlendParams()
+
+    def forward(self, fragments, meshes, **kwargs):
+        blend_params = kwargs.get("blend_params", self.blend_params)
+        return hard_rgb_blend(meshes.sample_textures(fragments), fragments, blend_params)
+
+
+class SoftSimpleShader(nn.Module):
+    def __init__(self, device="cpu", blend_params=None):
+        super().__init__()
+        self.blend_params = blend_params if blend_params is not None else BlendParams()
+
+    def forward(self, fragments, meshes, **kwargs):
+        blend_params = kwargs.get("blend_params", self.blend_params)
+        return softmax_rgb_blend(meshes.sample_textures(fragments), fragments, blend_params)

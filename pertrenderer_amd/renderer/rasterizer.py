@@ -1,0 +1,155 @@
+"""K-nearest-face mesh rasterizer (PyTorch3D 0.4.0 ``MeshRasterizer`` /
+``rasterize_meshes`` semantics) on the native gfx950 kernels pr_rast_fwd/bwd.
+
+MeshRasterizer.forward(meshes_world): world -> view (R,T) -> NDC with view-space z
+kept, then per pixel the K nearest faces (ascending z, ties by face index) within
+``blur_radius`` (a squared-distance threshold).  Output ``Fragments`` as PyTorch3D:
+pix_to_face (N,H,W,K) int64 packed face ids (-1 padded), zbuf, bary_coords
+(N,H,W,K,3), dists (signed squared distance, negative inside).  Called by the
+reference at experiments/eval.py:165-168 (RasterizationSettings at :135-141).
+"""
+from typing import NamedTuple, Optional
+
+import torch
+
+from .. import _native as nat
+from .. import timing as _timing
+
+F32 = torch.float32
+
+
+class Fragments(NamedTuple):
+    pix_to_face: torch.Tensor
+    zbuf: torch.Tensor
+    bary_coords: torch.Tensor
+    dists: torch.Tensor
+
+
+class RasterizationSettings:
+    """Mutable settings object (eval.py:390 assigns blur_radius in place)."""
+
+    def __init__(self, image_size=256, blur_radius=0.0, faces_per_pixel=1, bin_size=None,
+                 max_faces_per_bin=None, perspective_correct=False, clip_barycentric_coords=None,
+                 cull_backfaces=False):
+        self.image_size = image_size
+        self.blur_radius = blur_radius
+        self.faces_per_pixel = faces_per_pixel
+        self.bin_size = bin_size                  # accepted for API parity; the kernel bins per tile
+        self.max_faces_per_bin = max_faces_per_bin  # no overflow: candidate lists are unbounded
+        self.perspective_correct = perspective_correct
+        self.clip_barycentric_coords = clip_barycentric_coords
+        self.cull_backfaces = cull_backfaces
+
+
+def _hw(image_size):
+    if isinstance(image_size, (tuple, list)):
+        return int(image_size[0]), int(image_size[1])
+    return int(image_size), int(image_size)
+
+
+class _RasterizeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, face_verts, first, nfaces, H, W, K, blur, persp, clip, cull):
+        nat.require_device(face_verts, first, nfaces)
+        lib = nat.load()
+        fv = face_verts.detach().to(F32).contiguous()
+        N = first.shape[0]
+        dev = fv.device
+        a = nat.PRRastArgs()
+        a.face_verts, a.mesh_first_face, a.mesh_num_faces = nat.ptr(fv), nat.ptr(first), nat.ptr(nfaces)
+        a.F, a.N, a.H, a.W, a.K = fv.shape[0], N, H, W, K
+        a.blur_radius, a.perspective_correct = float(blur), int(persp)
+        a.clip_barycentric_coords, a.cull_backfaces = int(clip), int(cull)
+        p2f = torch.empty((N, H, W, K), dtype=torch.int64, device=dev)
+        zbuf = torch.empty((N, H, W, K), dtype=F32, device=dev)
+        bary = torch.empty((N, H, W, K, 3), dtype=F32, device=dev)
+        dists = torch.empty((N, H, W, K), dtype=F32, device=dev)
+        a.pix_to_face, a.zbuf, a.bary, a.dists = nat.ptr(p2f), nat.ptr(zbuf), nat.ptr(bary), nat.ptr(dists)
+        ws = torch.empty(max(1, lib.pr_rast_fwd_workspace_size(a)), dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
+        timing = _timing.active()
+        if timing is not None:
+            timing.start("rast_fwd")
+        nat.check(lib.pr_rast_fwd(a, nat.stream_of(fv)), "pr_rast_fwd")
+        if timing is not None:
+            timing.stop("rast_fwd")
+        ctx.save_for_backward(fv, first, nfaces, p2f)
+        ctx.cfg = (H, W, K, float(blur), int(persp), int(clip), int(cull))
+        ctx.mark_non_differentiable(p2f)
+        return p2f, zbuf, bary, dists
+
+    @staticmethod
+    def backward(ctx, gp2f, gzbuf, gbary, gdists):
+        fv, first, nfaces, p2f = ctx.saved_tensors
+        H, W, K, blur, persp, clip, cull = ctx.cfg
+        lib = nat.load()
+        a = nat.PRRastArgs()
+        a.face_verts, a.mesh_first_face, a.mesh_num_faces = nat.ptr(fv), nat.ptr(first), nat.ptr(nfaces)
+        a.F, a.N, a.H, a.W, a.K = fv.shape[0], first.shape[0], H, W, K
+        a.blur_radius, a.perspective_correct, a.clip_barycentric_coords, a.cull_backfaces = blur, persp, clip, cull
+        a.pix_to_face = nat.ptr(p2f)
+        keep = []
+        for name, g in (("grad_zbuf", gzbuf), ("grad_bary", gbary), ("grad_dists", gdists)):
+            if g is not None:
+                g = g.detach().to(F32).contiguous()
+                keep.append(g)
+                setattr(a, name, nat.ptr(g))
+        gfv = torch.empty_like(fv)
+        a.grad_face_verts = nat.ptr(gfv)
+        timing = _timing.active()
+        if timing is not None:
+            timing.start("rast_bwd")
+        nat.check(lib.pr_rast_bwd(a, nat.stream_of(fv)), "pr_rast_bwd")
+        if timing is not None:
+            timing.stop("rast_bwd")
+        return gfv, None, None, None, None, None, None, None, None, None
+
+
+def rasterize_meshes(meshes, image_size=256, blur_radius=0.0, faces_per_pixel=8, bin_size=None,
+                     max_faces_per_bin=None, perspective_correct=False, clip_barycentric_coords=False,
+                     cull_backfaces=False):
+    """PyTorch3D rasterize_meshes on meshes already in NDC (x,y) + view z."""
+    verts = meshes.verts_packed()
+    faces = meshes.faces_packed().to(verts.device)
+    face_verts = verts[faces]
+    first = meshes.mesh_to_faces_packed_first_idx().to(verts.device)
+    nfaces = meshes.num_faces_per_mesh().to(verts.device)
+    H, W = _hw(image_size)
+    return _RasterizeFn.apply(face_verts, first, nfaces, H, W, int(faces_per_pixel), float(blur_radius),
+                              bool(perspective_correct), bool(clip_barycentric_coords), bool(cull_backfaces))
+
+
+class MeshRasterizer(torch.nn.Module):
+    def __init__(self, cameras=None, raster_settings=None):
+        super().__init__()
+        self.cameras = cameras
+        self.raster_settings = raster_settings if raster_settings is not None else RasterizationSettings()
+
+    def to(self, device):
+        if self.cameras is not None:
+            self.cameras = self.cameras.to(device)
+        return self
+
+    def transform(self, meshes_world, **kwargs):
+        cameras = kwargs.get("cameras", self.cameras)
+        if cameras is None:
+            raise ValueError("Cameras must be specified either at initialization or in the forward pass "
+                             "of MeshRasterizer")
+        verts_world = meshes_world.verts_padded()
+        verts_view = cameras.get_world_to_view_transform(**kwargs).transform_points(verts_world)
+        verts_ndc = cameras.get_projection_transform(**kwargs).transform_points(verts_view)
+        verts_ndc = torch.cat([verts_ndc[..., :2], verts_view[..., 2:3]], dim=-1)
+        return meshes_world.update_padded(verts_ndc)
+
+    def forward(self, meshes_world, **kwargs) -> Fragments:
+        meshes_screen = self.transform(meshes_world, **kwargs)
+        rs = kwargs.get("raster_settings", self.raster_settings)
+        clip = rs.clip_barycentric_coords
+        if clip is None:
+            clip = rs.blur_radius > 0.0
+        p2f, zbuf, bary, dists = rasterize_meshes(
+            meshes_screen, image_size=rs.image_size, blur_radius=rs.blur_radius,
+            faces_per_pixel=rs.faces_per_pixel, bin_size=rs.bin_size, max_faces_per_bin=rs.max_faces_per_bin,
+            perspective_correct=rs.perspective_correct, clip_barycentric_coords=clip,
+            cull_backfaces=rs.cull_backfaces)
+        return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)

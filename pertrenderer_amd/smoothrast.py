@@ -1,0 +1,106 @@
+"""Smooth rasterization operators — the reference's ``randomras.smoothrast`` surface.
+
+Class names, constructor signatures, attributes (``sigma`` a CPU 0-d leaf with
+requires_grad, ``nb_samples`` an int) and the ``update_*`` mutators mirror
+smoothrast.py:111-194.  ``GaussianRast.rasterize`` runs on the native kernels
+(pr_heaviside_*); inside ``smooth_rgb_blend`` a GaussianRast + GaussianAgg pair is
+fused into one pr_blend launch.  The deterministic variants (SoftRast, AffineRast,
+HardRast) are elementwise torch expressions, as in the reference.
+"""
+import torch
+from torch.nn import Module
+
+from . import blend as _blend
+from . import variants as _variants
+
+
+class SmoothRastBase(Module):
+    """smoothrast.py:111-123."""
+
+    def __init__(self, sigma=2e-4):
+        super().__init__()
+        self.sigma = torch.tensor(sigma, requires_grad=True)
+        self.nb_samples = 1
+
+    def update_smoothing(self, sigma):
+        self.sigma = torch.tensor(sigma, requires_grad=True)
+
+    def update_nb_samples(self, nb_samples):
+        self.nb_samples = nb_samples
+
+
+class SoftRast(SmoothRastBase):
+    """sigmoid(-d / sigma) (smoothrast.py:126-134)."""
+
+    def __init__(self, sigma=2e-4):
+        super().__init__(sigma)
+
+    def rasterize(self, dists):
+        return torch.sigmoid(-dists / self.sigma)
+
+
+class GaussianRast(SmoothRastBase):
+    """Monte-Carlo perturbed Heaviside with Gaussian noise (smoothrast.py:136-147)."""
+
+    noise_kind = "gaussian"
+    variance_reduction = True
+
+    def __init__(self, nb_samples=16, sigma=2e-4):
+        super().__init__(sigma)
+        self.nb_samples = nb_samples
+
+    def rasterize(self, dists):
+        return _blend.perturbed_heaviside(dists, self.sigma, self.nb_samples)
+
+
+class GaussianRast_wovr(SmoothRastBase):
+    """Gaussian perturbed Heaviside without variance reduction (smoothrast.py:149-160)."""
+
+    noise_kind = "gaussian"
+    variance_reduction = False
+
+    def __init__(self, nb_samples=16, sigma=2e-4):
+        super().__init__(sigma)
+        self.nb_samples = nb_samples
+
+    def rasterize(self, dists):
+        return _variants.perturbed_heaviside_variant(dists, self.sigma, self.nb_samples,
+                                                     "gaussian", variance_reduction=False)
+
+
+class ArctanRast(SmoothRastBase):
+    """Cauchy-perturbed Heaviside (smoothrast.py:162-173)."""
+
+    noise_kind = "cauchy"
+    variance_reduction = True
+
+    def __init__(self, nb_samples=16, sigma=2e-4):
+        super().__init__(sigma)
+        self.nb_samples = nb_samples
+
+    def rasterize(self, dists):
+        return _variants.perturbed_heaviside_variant(dists, self.sigma, self.nb_samples, "cauchy",
+                                                     variance_reduction=True)
+
+
+class AffineRast(SmoothRastBase):
+    """Clamped affine ramp (smoothrast.py:175-185)."""
+
+    def __init__(self, nb_samples=16, sigma=2e-4):
+        super().__init__(sigma)
+        self.nb_samples = nb_samples
+
+    def rasterize(self, dists):
+        x = -dists / self.sigma
+        ramp = torch.where(x > 0.5, torch.ones_like(dists), x + 0.5)
+        return torch.where(ramp < 0.0, torch.zeros_like(ramp), ramp)
+
+
+class HardRast:
+    """Hard inside test H(-d) (smoothrast.py:187-194)."""
+
+    def __init__(self):
+        return
+
+    def rasterize(self, dists):
+        return torch.heaviside(-dists, torch.ones((), dtype=dists.dtype, device=dists.device))

@@ -1,0 +1,53 @@
+"""Per-kernel HIP-event timing for bench.py's roofline leg.
+
+When a :class:`KernelTimer` is active (``with KernelTimer() as t``), every native
+launch site brackets its kernel with two events recorded on the SAME stream the
+kernel is enqueued on (torch's current stream of the tensors' device), so the
+elapsed time is the kernel's own duration on that stream.
+"""
+import collections
+
+import torch
+
+_ACTIVE = None
+
+
+def active():
+    return _ACTIVE
+
+
+class KernelTimer:
+    def __init__(self):
+        self._open = {}
+        self.events = collections.defaultdict(list)
+
+    def __enter__(self):
+        global _ACTIVE
+        self._prev, _ACTIVE = _ACTIVE, self
+        return self
+
+    def __exit__(self, *exc):
+        global _ACTIVE
+        _ACTIVE = self._prev
+        return False
+
+    def start(self, name):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream())
+        self._open[name] = ev
+
+    def stop(self, name):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream())
+        self.events[name].append((self._open.pop(name), ev))
+
+    def reset(self):
+        self.events.clear()
+
+    def summary(self):
+        """{name: (launches, mean ms)} — call after torch.cuda.synchronize()."""
+        out = {}
+        for name, pairs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in pairs]
+            out[name] = (len(ms), sum(ms) / max(1, len(ms)))
+        return out

@@ -1,0 +1,208 @@
+"""GPU parity of the native perturbed blend against the reference (golden vectors) and
+the CPU oracle.  Injected-noise mode is compared element-wise at the 1e-5 relative
+fp32 bar; Philox mode is compared with the numpy Philox restatement (counts are
+integers: bit-exact) and checked statistically."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close, load_golden
+from oracle import blend_oracle as bo
+from oracle import philox_ref
+from pertrenderer_amd import Noise, perturbed_aggregate, perturbed_blend, perturbed_heaviside
+
+pytestmark = pytest.mark.gpu
+BLEND_CASES = ["blend_small", "blend_eval", "blend_edge", "blend_fixed", "blend_k100"]
+SCALAR_RTOL = 2e-5
+
+
+def _leaf(v):
+    return torch.tensor(float(v), requires_grad=True)
+
+
+def _run_fused(f, dev, noise=None):
+    d = torch.tensor(f["dists"], device=dev, requires_grad=True)
+    z = torch.tensor(f["zbuf"], device=dev, requires_grad=True)
+    c = torch.tensor(f["colors"], device=dev, requires_grad=True)
+    p2f = torch.tensor(f["pix_to_face"], device=dev)
+    s, g, a = _leaf(f["sigma"]), _leaf(f["gamma"]), _leaf(f["alpha"])
+    N = p2f.shape[0]
+    zn = torch.full((N, 1, 1, 1), float(f["znear"]), device=dev)
+    zf = torch.full((N, 1, 1, 1), float(f["zfar"]), device=dev)
+    if noise is None:
+        noise = Noise.injected(torch.tensor(f["noise_r"], device=dev), torch.tensor(f["noise_a"], device=dev))
+    img = perturbed_blend(c, p2f, d, z, s, g, a, int(f["Sr"]), int(f["Sa"]), eps=float(f["eps"]),
+                          background=tuple(f["background"]), znear=zn, zfar=zf, noise=noise)
+    (img * torch.tensor(f["grad_image"], device=dev)).sum().backward()
+    return img, dict(dists=d.grad, zbuf=z.grad, colors=c.grad, sigma=s.grad, gamma=g.grad, alpha=a.grad)
+
+
+@pytest.mark.parametrize("case", BLEND_CASES)
+def test_fused_blend_matches_reference_golden(case, device):
+    f = load_golden(case)
+    img, g = _run_fused(f, device)
+    assert_close(img, f["image"], name="image")
+    for k in ("dists", "zbuf", "colors"):
+        assert_close(g[k], f["grad_" + k], name=k)
+    for k in ("sigma", "gamma", "alpha"):
+        assert g[k].device.type == "cpu" and g[k].dim() == 0
+        assert_close(g[k], f["grad_" + k], rtol=SCALAR_RTOL, name=k)
+
+
+def test_standalone_rasterize_matches_reference_golden(device):
+    f = load_golden("rast_only")
+    d = torch.tensor(f["dists"], device=device, requires_grad=True)
+    s = _leaf(f["sigma"])
+    P = perturbed_heaviside(d, s, int(f["Sr"]), noise=Noise.injected(torch.tensor(f["noise_r"], device=device)))
+    (P * torch.tensor(f["grad_P"], device=device)).sum().backward()
+    np.testing.assert_array_equal(P.detach().cpu().numpy(), f["P"])
+    assert_close(d.grad, f["grad_dists"], name="dists")
+    assert_close(s.grad, f["grad_sigma"], rtol=SCALAR_RTOL, name="sigma")
+
+
+def test_standalone_aggregate_matches_reference_golden(device):
+    f = load_golden("agg_only")
+    z = torch.tensor(f["zbuf"], device=device, requires_grad=True)
+    pr = torch.tensor(f["prob"], device=device, requires_grad=True)
+    mask = torch.tensor(f["pix_to_face"], device=device) >= 0
+    g, a = _leaf(f["gamma"]), _leaf(f["alpha"])
+    N = z.shape[0]
+    W = perturbed_aggregate(z, torch.full((N, 1, 1, 1), float(f["zfar"]), device=device),
+                            torch.full((N, 1, 1, 1), float(f["znear"]), device=device), pr, mask, g, a,
+                            int(f["Sa"]), eps=float(f["eps"]),
+                            noise=Noise.injected(noise_a=torch.tensor(f["noise_a"], device=device)))
+    (W * torch.tensor(f["grad_W"], device=device)).sum().backward()
+    np.testing.assert_array_equal(W.detach().cpu().numpy(), f["W"])
+    assert_close(z.grad, f["grad_zbuf"], name="zbuf")
+    assert_close(pr.grad, f["grad_prob"], name="prob")
+    assert_close(g.grad, f["grad_gamma"], rtol=SCALAR_RTOL, name="gamma")
+    assert_close(a.grad, f["grad_alpha"], rtol=SCALAR_RTOL, name="alpha")
+
+
+def _synthetic(N, H, W, K, Sr, Sa, seed, sigma=1e-3, p_valid=0.6, packed=True):
+    g = torch.Generator().manual_seed(seed)
+    valid = torch.rand((N, H, W, K), generator=g) < p_valid
+    if packed:
+        cnt = valid.sum(-1, keepdim=True)
+        valid = torch.arange(K).expand(N, H, W, K) < cnt
+    p2f = torch.where(valid, torch.randint(0, 5000, (N, H, W, K), generator=g), torch.full((N, H, W, K), -1))
+    dists = torch.where(valid, (torch.rand((N, H, W, K), generator=g) - 0.5) * 6 * sigma, torch.full((N, H, W, K), -1.0))
+    zbuf = torch.where(valid, 5.0 + torch.rand((N, H, W, K), generator=g), torch.full((N, H, W, K), -1.0))
+    colors = torch.rand((N, H, W, K, 3), generator=g)
+    f = dict(pix_to_face=p2f.numpy(), dists=dists.numpy(), zbuf=zbuf.numpy(), colors=colors.numpy(),
+             sigma=np.float32(sigma), gamma=np.float32(1e-2), alpha=np.float32(1.0), eps=1e-10,
+             background=np.array([0.1, 0.2, 0.3], np.float32), znear=1.0, zfar=100.0, Sr=Sr, Sa=Sa)
+    f["noise_r"] = torch.randn((Sr, N, H, W, K), generator=g).numpy()
+    f["noise_a"] = torch.randn((Sa, N, H, W, K + 1), generator=g).numpy()
+    f["grad_image"] = torch.randn((N, H, W, 4), generator=g).numpy()
+    return f
+
+
+def _oracle(f):
+    T = lambda a: torch.from_numpy(np.asarray(a))
+    N = f["pix_to_face"].shape[0]
+    zn, zf = torch.full((N, 1, 1, 1), float(f["znear"])), torch.full((N, 1, 1, 1), float(f["zfar"]))
+    img, s = bo.blend_forward(T(f["pix_to_face"]), T(f["dists"]), T(f["zbuf"]), T(f["colors"]), T(f["noise_r"]),
+                              T(f["noise_a"]), T(f["sigma"]), T(f["gamma"]), T(f["alpha"]), float(f["eps"]),
+                              T(f["background"]), zn, zf)
+    return img, bo.blend_backward(T(f["grad_image"]), s), s
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 20, 50, 8, 8), (1, 8, 8, 150, 16, 4), (1, 12, 9, 7, 3, 5),
+                                   (1, 4, 4, 255, 4, 4)])
+def test_fused_blend_matches_oracle_random(shape, device):
+    N, H, W, K, Sr, Sa = shape
+    f = _synthetic(N, H, W, K, Sr, Sa, seed=sum(shape), packed=K != 7)
+    img, g = _run_fused(f, device)
+    oimg, og, saved = _oracle(f)
+    # the Monte-Carlo weights are counts / Sa: exact, so the image matches to fp32 summation order
+    assert_close(img, oimg, name="image")
+    for k in ("dists", "zbuf", "colors"):
+        assert_close(g[k], og[k], name=k)
+    for k in ("sigma", "gamma", "alpha"):
+        assert_close(g[k], og[k], rtol=1e-4, atol_rel=0, name=k)
+
+
+def test_empty_and_fully_masked_pixels(device):
+    f = _synthetic(1, 4, 4, 6, 4, 4, seed=3, p_valid=0.0)
+    img, g = _run_fused(f, device)
+    bg = f["background"]
+    np.testing.assert_allclose(img[..., :3].detach().cpu().numpy(), np.broadcast_to(bg, (1, 4, 4, 3)), rtol=0)
+    np.testing.assert_array_equal(img[..., 3].detach().cpu().numpy(), 0.0)
+    assert torch.all(g["dists"] == 0) and torch.all(g["zbuf"] == 0) and torch.all(g["colors"] == 0)
+
+
+# ------------------------------------------------------------------ Philox mode
+def test_philox_heaviside_counts_match_numpy_stream(device):
+    N, H, W, K, S = 1, 6, 7, 9, 12
+    g = torch.Generator().manual_seed(0)
+    sigma = 1e-3
+    d = ((torch.rand((N, H, W, K), generator=g) - 0.5) * 4 * sigma)
+    seed = 0x1234_5678_9ABC
+    P = perturbed_heaviside(d.to(device), torch.tensor(sigma), S, noise=Noise.philox(seed_r=seed)).cpu().numpy()
+    u = philox_ref.rast_uniforms(seed, N * H * W, K, S).reshape((S, N, H, W, K))
+    thr = 0.5 * np.array([math.erfc(-x / math.sqrt(2)) for x in (d.numpy().astype(np.float64) / sigma).ravel()]
+                         ).reshape(d.shape)
+    cnt = (u >= thr[None]).sum(0)
+    ref = (cnt.astype(np.float32) / np.float32(S))
+    mismatch = (P != ref).mean()
+    assert mismatch < 2e-3, mismatch  # only u within an ulp of the threshold may differ
+
+
+def test_philox_sharding_is_additive(device):
+    """Disjoint sample ranges partition the estimator: (P[0:4] + P[4:8]) / 2 == P[0:8]."""
+    d = ((torch.rand((1, 8, 8, 20), generator=torch.Generator().manual_seed(1)) - 0.5) * 4e-3).to(device)
+    s = torch.tensor(1e-3)
+    full = perturbed_heaviside(d, s, 8, noise=Noise.philox(seed_r=77))
+    a = perturbed_heaviside(d, s, 4, noise=Noise.philox(seed_r=77, offset_r=0))
+    b = perturbed_heaviside(d, s, 4, noise=Noise.philox(seed_r=77, offset_r=4))
+    torch.testing.assert_close((a + b) / 2, full, rtol=0, atol=0)
+
+
+def test_philox_heaviside_is_unbiased(device):
+    """E[P] = Phi(D/sigma) and E[dP/dD estimate] = phi(D/sigma)/sigma (smoothrast.py:46,53)."""
+    sigma = 1.0
+    Dv = torch.linspace(-2.0, 2.0, 9)
+    S = 256
+    reps = 256
+    d = (-Dv).reshape(1, 1, 1, -1).repeat(1, reps, 1, 1).to(device).requires_grad_(True)
+    P = perturbed_heaviside(d, torch.tensor(sigma), S, noise=Noise.philox(seed_r=2024))
+    P.sum().backward()
+    est_p = P.detach().mean(dim=(0, 1, 2)).cpu().double()
+    est_g = -d.grad.mean(dim=(0, 1, 2)).cpu().double()
+    phi = torch.exp(-0.5 * Dv.double() ** 2) / math.sqrt(2 * math.pi)
+    Phi = 0.5 * torch.erfc(-Dv.double() / math.sqrt(2))
+    n = S * reps
+    assert torch.all((est_p - Phi).abs() <= 5 * torch.sqrt(Phi * (1 - Phi) / n) + 1e-3)
+    assert torch.all((est_g - phi / sigma).abs() <= 0.02), (est_g, phi)
+
+
+def test_philox_argmax_frequencies(device):
+    """Perturbed-argmax weights converge to P(argmax_j z_j + gamma*eps_j) (Gaussian, 3 logits)."""
+    N, reps, K = 1, 4096, 2
+    zbuf = torch.tensor([5.0, 5.02]).reshape(1, 1, 1, 2).repeat(1, reps, 1, 1).to(device)
+    prob = torch.ones_like(zbuf) * 0.5
+    mask = torch.ones_like(zbuf, dtype=torch.bool)
+    gamma = torch.tensor(1e-2)
+    W = perturbed_aggregate(zbuf, 100.0, 1.0, prob, mask, gamma, torch.tensor(1.0), 16, noise=Noise.philox(seed_a=9))
+    w = W.mean(dim=(0, 1, 2)).cpu().double()
+    # Monte-Carlo reference probabilities with numpy normals
+    z_inv = (100.0 - np.array([5.0, 5.02])) / 99.0
+    zk = 1e-2 * np.log(0.5) + z_inv - z_inv.max()
+    z = np.concatenate([zk, [1e-10 - z_inv.max()]])
+    rng = np.random.default_rng(0)
+    e = rng.standard_normal((400000, 3))
+    ref = np.bincount(np.argmax(z + 1e-2 * e, axis=1), minlength=3) / 400000.0
+    assert np.all(np.abs(w.numpy() - ref) < 0.01), (w, ref)
+
+
+def test_philox_is_deterministic_per_seed(device):
+    f = _synthetic(1, 8, 8, 20, 8, 8, seed=5)
+    n = Noise.philox(seed_r=11, seed_a=12)
+    i1, g1 = _run_fused(f, device, noise=n)
+    i2, g2 = _run_fused(f, device, noise=n)
+    assert torch.equal(i1, i2)
+    for k in ("dists", "zbuf", "colors"):
+        assert torch.equal(g1[k], g2[k])
