@@ -1,0 +1,311 @@
+"""Benchmark of the perturbed-renderer hot path (BASELINE.json configs[1]).
+
+One step = one pose-optimisation iteration of experiments/eval.py:343-370 on one
+frame per GPU: rotate the mesh (so3 exp map), MeshRasterizer (native K-nearest
+rasterizer, 256x256, faces_per_pixel=50, blur = ln(1/1e-4 - 1)*sigma),
+RandomSimpleShader with GaussianRast(nb_samples=8) + GaussianAgg(nb_samples=8)
+(fused native blend), L2 loss to a fixed synthetic target, backward through
+blend -> interpolation -> rasterizer -> vertices -> pose, and (N>1) one RCCL
+all-reduce averaging the pose/smoothing gradients across ranks.  Per-GPU work is
+fixed (one frame per rank per step): weak scaling.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Prints ONE JSON line on rank 0.  `value` = frames/s over all ranks (forward +
+backward per frame); `roofline` is the dominant native kernel's algorithmic HBM
+bytes / its mean HIP-event duration inside the timed region; `cpu_baseline` times
+the CPU oracle (test-infrastructure restatement of the reference + PyTorch3D
+rasterizer) on a bounded sample of the same workload, on rank 0 at N=1.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import pertrenderer_amd as pa  # noqa: E402
+from pertrenderer_amd.renderer import (FoVPerspectiveCameras, MeshRasterizer, MeshRenderer, Meshes,  # noqa: E402
+                                       RasterizationSettings, TexturesVertex, load_obj, look_at_view_transform)
+from pertrenderer_amd.renderer.transforms import Rotate, so3_exponential_map  # noqa: E402
+from pertrenderer_amd.timing import KernelTimer  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def load_sphere(device):
+    verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
+    center = verts.mean(0)
+    verts = verts - center
+    verts = verts / verts.abs().max()
+    return verts.to(device), faces.verts_idx.to(device)
+
+
+class Workload:
+    def __init__(self, device, image_size=256, K=50, samples=8, sigma=1e-3, gamma=1e-2, dist_cam=2.7, seed=0):
+        self.device = device
+        g = torch.Generator().manual_seed(seed)
+        verts, faces = load_sphere(device)
+        colors = torch.rand((1, verts.shape[0], 3), generator=g).to(device)
+        self.base = Meshes([verts], [faces], TexturesVertex(colors))
+        R, T = look_at_view_transform(dist_cam, 30.0, 120.0, device=device)
+        self.cameras = FoVPerspectiveCameras(R=R, T=T, device=device, fov=60.0)
+        self.settings = RasterizationSettings(image_size=image_size,
+                                              blur_radius=math.log(1.0 / 1e-4 - 1.0) * sigma,
+                                              faces_per_pixel=K, max_faces_per_bin=50000,
+                                              perspective_correct=False)
+        self.rast = pa.GaussianRast(nb_samples=samples, sigma=sigma)
+        self.agg = pa.GaussianAgg(nb_samples=samples, gamma=gamma, alpha=1.0)
+        self.renderer = MeshRenderer(
+            rasterizer=MeshRasterizer(cameras=self.cameras, raster_settings=self.settings),
+            shader=pa.RandomSimpleShader(device=device, cameras=self.cameras, smoothrast=self.rast,
+                                         smoothagg=self.agg,
+                                         blend_params=pa.random_rasterizer.BlendParams(sigma, gamma, (0.0, 0.0, 0.0))))
+        self.log_rot = (0.3 * torch.randn((1, 3), generator=g)).to(device).requires_grad_(True)
+        self.target = torch.rand((1, image_size, image_size, 3), generator=g).to(device)
+        self.K, self.S, self.H = K, samples, image_size
+        self.F = faces.shape[0]
+
+    def params(self):
+        return [self.log_rot, self.rast.sigma, self.agg.gamma, self.agg.alpha]
+
+    def forward(self):
+        R = so3_exponential_map(self.log_rot)
+        mesh = self.base.update_padded(Rotate(R).transform_points(self.base.verts_padded()))
+        images = self.renderer(mesh, cameras=self.cameras)
+        return ((images[..., :3] - self.target) ** 2).mean()
+
+    def zero_grad(self):
+        for p in self.params():
+            p.grad = None
+
+
+def allreduce_grads(params, world):
+    """The single gradient reduction of the data-parallel step: one flattened RCCL
+    all-reduce (sum) of every gradient, then / world."""
+    grads = [p.grad.to("cuda", non_blocking=True).reshape(-1) for p in params if p.grad is not None]
+    flat = torch.cat(grads)
+    dist.all_reduce(flat)
+    flat /= world
+    off = 0
+    for p in params:
+        if p.grad is not None:
+            n = p.grad.numel()
+            p.grad.copy_(flat[off:off + n].reshape(p.grad.shape).to(p.grad.device))
+            off += n
+
+
+def kernel_bytes(name, P, K, S, F):
+    """Algorithmic HBM bytes per launch (int64 pix_to_face)."""
+    slots = P * K
+    return {
+        "blend_fwd": slots * (8 + 4 + 4 + 12) + P * 16 + P * S,           # p2f,dists,zbuf,colors | image, winners
+        "blend_bwd": slots * (8 + 4 + 4 + 12 + 4 + 4 + 12) + P * 16 + P * S,  # + d dists,d zbuf,d colors | d image
+        "rast_fwd": slots * (8 + 4 + 12 + 4) + F * 36,                   # p2f,zbuf,bary,dists | face verts
+        "rast_bwd": slots * (8 + 4 + 12 + 4) + F * 36 * 2,               # p2f + 3 upstream grads | verts, grads
+    }.get(name)
+
+
+def dense_roofline(device, P_side=256, K=50, S=8, iters=20):
+    """Blend kernels on dense synthetic fragments (every slot valid) — the bandwidth microbench."""
+    g = torch.Generator().manual_seed(0)
+    N, H, W = 1, P_side, P_side
+    p2f = torch.randint(0, 5000, (N, H, W, K), generator=g).to(device)
+    dists = ((torch.rand((N, H, W, K), generator=g) - 0.5) * 6e-3).to(device).requires_grad_(True)
+    zbuf = (5.0 + 2.0 * torch.rand((N, H, W, K), generator=g)).sort(-1).values.to(device).requires_grad_(True)
+    colors = torch.rand((N, H, W, K, 3), generator=g).to(device).requires_grad_(True)
+    sig, gam, alp = (torch.tensor(v, device=device, requires_grad=True) for v in (1e-3, 1e-2, 1.0))
+    gimg = torch.randn((N, H, W, 4), device=device)
+    with KernelTimer() as kt:
+        for it in range(iters + 3):
+            if it == 3:
+                torch.cuda.synchronize()
+                kt.reset()
+            img = pa.perturbed_blend(colors, p2f, dists, zbuf, sig, gam, alp, S, S, background=(0, 0, 0))
+            img.backward(gimg)
+        torch.cuda.synchronize()
+    out = {}
+    for name, (n, ms) in kt.summary().items():
+        b = kernel_bytes(name, N * H * W, K, S, 0)
+        out[name] = {"achieved": round(b / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms": round(ms, 4),
+                     "bytes": b, "launches": n}
+    return out
+
+
+def cpu_baseline(frames, threads):
+    """CPU oracle of one step of the same workload (rasterizer in C/OpenMP, blend in torch-CPU)."""
+    from oracle import blend_oracle as bo
+    from oracle import rast_ref
+    torch.set_num_threads(threads)
+    dev = torch.device("cpu")
+    wl = WorkloadCPU()
+    t0 = time.perf_counter()
+    for i in range(frames):
+        wl.step(bo, rast_ref, i)
+    dt = time.perf_counter() - t0
+    return frames / dt, dt
+
+
+class WorkloadCPU:
+    """Same frame as Workload, on the CPU oracles (no torch device code)."""
+
+    def __init__(self, image_size=256, K=50, samples=8, sigma=1e-3, gamma=1e-2):
+        dev = torch.device("cpu")
+        g = torch.Generator().manual_seed(0)
+        verts, faces = load_sphere(dev)
+        self.colors_v = torch.rand((verts.shape[0], 3), generator=g)
+        R, T = look_at_view_transform(2.7, 30.0, 120.0)
+        self.cams = FoVPerspectiveCameras(R=R, T=T, fov=60.0)
+        self.verts, self.faces = verts, faces
+        self.log_rot = 0.3 * torch.randn((1, 3), generator=g)
+        self.target = torch.rand((1, image_size, image_size, 3), generator=g)
+        self.H, self.K, self.S, self.sigma, self.gamma = image_size, K, samples, sigma, gamma
+        self.blur = math.log(1.0 / 1e-4 - 1.0) * sigma
+
+    def step(self, bo, rast_ref, i):
+        H, K, S = self.H, self.K, self.S
+        R = so3_exponential_map(self.log_rot)
+        v = Rotate(R).transform_points(self.verts[None])
+        vv = self.cams.get_world_to_view_transform().transform_points(v)
+        vn = self.cams.get_projection_transform().transform_points(vv)
+        vn = torch.cat([vn[..., :2], vv[..., 2:3]], -1)[0]
+        fv = vn[self.faces].numpy()
+        p2f, zbuf, bary, dists = rast_ref.rast_fwd(fv, [0], [fv.shape[0]], H, H, K, self.blur, False, True, False)
+        attr = self.colors_v[self.faces].numpy()
+        texels = torch.from_numpy(rast_ref.interp(p2f, bary, attr))
+        zn, zf = torch.ones((1, 1, 1, 1)), torch.full((1, 1, 1, 1), 100.0)
+        nr = torch.randn((S, 1, H, H, K))
+        na = torch.randn((S, 1, H, H, K + 1))
+        img, saved = bo.blend_forward(torch.from_numpy(p2f), torch.from_numpy(dists), torch.from_numpy(zbuf), texels,
+                                      nr, na, torch.tensor(self.sigma), torch.tensor(self.gamma), torch.tensor(1.0),
+                                      1e-10, (0.0, 0.0, 0.0), zn, zf)
+        gimg = torch.zeros_like(img)
+        gimg[..., :3] = 2.0 * (img[..., :3] - self.target) / self.target.numel()
+        g = bo.blend_backward(gimg, saved)
+        gbary = np.einsum("...kc,...kvc->...kv", g["colors"].numpy(),
+                          attr[np.where(p2f >= 0, p2f, 0)]) * (p2f >= 0)[..., None]
+        rast_ref.rast_bwd(fv, p2f, g["zbuf"].numpy(), gbary.astype(np.float32), g["dists"].numpy(), False, True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--image-size", type=int, default=256)
+    ap.add_argument("--faces-per-pixel", type=int, default=50)
+    ap.add_argument("--samples", type=int, default=8)
+    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dense", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.manual_seed(1234 + rank)
+    pa.native_library()
+
+    wl = Workload(device, args.image_size, args.faces_per_pixel, args.samples, seed=rank)
+    P = args.image_size * args.image_size
+
+    def step():
+        loss = wl.forward()
+        loss.backward()
+        if world > 1:
+            allreduce_grads(wl.params(), world)
+        wl.zero_grad()
+
+    for _ in range(args.warmup):
+        step()
+    fwd_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+               torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    with KernelTimer() as kt:
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            a, b, c = fwd_ev[i]
+            a.record()
+            loss = wl.forward()
+            b.record()
+            loss.backward()
+            c.record()
+            if world > 1:
+                allreduce_grads(wl.params(), world)
+            wl.zero_grad()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_fwd = float(np.mean([a.elapsed_time(b) for a, b, _ in fwd_ev]))
+    ms_bwd = float(np.mean([b.elapsed_time(c) for _, b, c in fwd_ev]))
+    kern = {}
+    for name, (n, ms) in kt.summary().items():
+        bts = kernel_bytes(name, P, wl.K, wl.S, wl.F)
+        kern[name] = {"launches": n, "ms": round(ms, 4), "bytes": bts,
+                      "GBps": round(bts / (ms * 1e-3) / 1e9, 1)}
+    dom = max(kern, key=lambda k: kern[k]["ms"] * kern[k]["launches"])
+    d = kern[dom]
+    roof = {"kernel": dom, "bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(d["GBps"] / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_per_launch": d["bytes"], "ms_per_launch": d["ms"]}
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        tr = json.load(open(pmc)).get(dom)
+        if tr:
+            roof["traffic"] = tr.get("bytes_per_launch")
+
+    frames = args.steps * world
+    value = frames / elapsed
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "frames/s (fwd+bwd)", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (sphere_642 mesh from the reference data, random vertex colours, random target)",
+        "config": {"workload": "pose-opt step: sphere_642 (1280 faces) 256x256, faces_per_pixel=50, "
+                               "Sr=Sa=8 Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, fwd+bwd",
+                   "image_size": args.image_size, "faces_per_pixel": args.faces_per_pixel,
+                   "nb_samples": args.samples, "frames_per_rank_per_step": 1,
+                   "parallelism": f"dp{world} (one frame per rank, RCCL gradient all-reduce)"},
+        "ms_forward": round(ms_fwd, 4), "ms_backward": round(ms_bwd, 4),
+        "fwd_frames_per_s": round(world * 1e3 / ms_fwd, 2), "kernels": kern, "roofline": roof,
+    }
+    if rank == 0 and not args.no_dense:
+        out["roofline_dense"] = dense_roofline(device)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+        os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+        v, dt = cpu_baseline(args.cpu_frames, threads)
+        out["cpu_baseline"] = {"value": round(v, 4), "unit": "frames/s (fwd+bwd)", "cores": threads,
+                               "kind": "port",
+                               "sample": f"{args.cpu_frames} frames of the same workload ({dt:.1f} s): C/OpenMP "
+                                         "rasterizer oracle + torch-CPU blend oracle fwd+bwd + rasterizer bwd"}
+        out["speedup_vs_cpu"] = round(value / v, 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

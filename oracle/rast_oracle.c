@@ -101,11 +101,12 @@ static real ndc(int i, int S1, int S2) {
 void rast_fwd(const real* fv, const int64_t* first, const int64_t* nfaces, int N, int H, int W, int K,
               real blur, int perspective_correct, int clip_bary, int cull_backfaces, int64_t* p2f,
               real* zbuf, real* bary, real* dists) {
-  real* qz = (real*)malloc(sizeof(real) * (size_t)(K + 1));
-  int64_t* qf = (int64_t*)malloc(sizeof(int64_t) * (size_t)(K + 1));
   const real rb = (real)sqrt((double)blur);
+#pragma omp parallel for collapse(2) schedule(dynamic, 1)
   for (int n = 0; n < N; ++n) {
     for (int row = 0; row < H; ++row) {
+      real* qz = (real*)malloc(sizeof(real) * (size_t)(K + 1));
+      int64_t* qf = (int64_t*)malloc(sizeof(int64_t) * (size_t)(K + 1));
       const real py = ndc(H - 1 - row, H, W);
       for (int col = 0; col < W; ++col) {
         const real px = ndc(W - 1 - col, W, H);
@@ -160,10 +161,10 @@ void rast_fwd(const real* fv, const int64_t* first, const int64_t* nfaces, int N
           }
         }
       }
+      free(qz);
+      free(qf);
     }
   }
-  free(qz);
-  free(qf);
 }
 
 /* ------------------------------------------------------------------ backward */

@@ -1,0 +1,89 @@
+"""SO(3) helpers and Rotate with PyTorch3D conventions (experiments/eval.py:49-55, 343-346,
+428-430): row-vector rotation points @ R, so3_exponential_map = Rodrigues' formula."""
+import math
+
+import torch
+
+F32 = torch.float32
+
+
+def hat(v):
+    N = v.shape[0]
+    h = v.new_zeros(N, 3, 3)
+    x, y, z = v.unbind(1)
+    h[:, 0, 1], h[:, 0, 2] = -z, y
+    h[:, 1, 0], h[:, 1, 2] = z, -x
+    h[:, 2, 0], h[:, 2, 1] = -y, x
+    return h
+
+
+def so3_exponential_map(log_rot, eps=0.0001):
+    nrms = (log_rot * log_rot).sum(1)
+    angles = torch.clamp(nrms, eps).sqrt()
+    inv = 1.0 / angles
+    fac1 = inv * angles.sin()
+    fac2 = inv * inv * (1.0 - angles.cos())
+    skews = hat(log_rot)
+    skews2 = torch.bmm(skews, skews)
+    eye = torch.eye(3, dtype=log_rot.dtype, device=log_rot.device)[None]
+    return fac1[:, None, None] * skews + fac2[:, None, None] * skews2 + eye
+
+
+so3_exp_map = so3_exponential_map
+
+
+def so3_rotation_angle(R, eps=1e-4, cos_angle=False):
+    tr = R[:, 0, 0] + R[:, 1, 1] + R[:, 2, 2]
+    phi_cos = (tr - 1.0) * 0.5
+    if cos_angle:
+        return phi_cos
+    return torch.acos(torch.clamp(phi_cos, -1.0 + eps, 1.0 - eps)) if eps > 0 else torch.acos(phi_cos)
+
+
+def so3_relative_angle(R1, R2, cos_angle=False):
+    return so3_rotation_angle(torch.bmm(R1, R2.permute(0, 2, 1)), cos_angle=cos_angle)
+
+
+def so3_log_map(R, eps=0.0001):
+    phi = so3_rotation_angle(R)
+    phi_sin = phi.sin()
+    phi_denom = torch.clamp(phi_sin.abs(), eps) * phi_sin.sign() + (phi_sin == 0).type_as(phi) * eps
+    log_rot_hat = (phi / (2.0 * phi_denom))[:, None, None] * (R - R.permute(0, 2, 1))
+    return torch.stack((log_rot_hat[:, 2, 1], log_rot_hat[:, 0, 2], log_rot_hat[:, 1, 0]), dim=1)
+
+
+def random_quaternions(n, dtype=F32, device=None):
+    o = torch.randn((n, 4), dtype=dtype, device=device)
+    s = (o * o).sum(1)
+    return o / torch.where(o[:, 0] < 0, -torch.sqrt(s), torch.sqrt(s))[:, None]
+
+
+def quaternion_to_matrix(q):
+    r, i, j, k = torch.unbind(q, -1)
+    two_s = 2.0 / (q * q).sum(-1)
+    o = torch.stack((1 - two_s * (j * j + k * k), two_s * (i * j - k * r), two_s * (i * k + j * r),
+                     two_s * (i * j + k * r), 1 - two_s * (i * i + k * k), two_s * (j * k - i * r),
+                     two_s * (i * k - j * r), two_s * (j * k + i * r), 1 - two_s * (i * i + j * j)), -1)
+    return o.reshape(q.shape[:-1] + (3, 3))
+
+
+def random_rotations(n, dtype=F32, device=None):
+    return quaternion_to_matrix(random_quaternions(n, dtype=dtype, device=device))
+
+
+class Rotate:
+    """points @ R (PyTorch3D Rotate)."""
+
+    def __init__(self, R, device=None):
+        self.R = R if R.dim() == 3 else R[None]
+
+    def transform_points(self, points):
+        pts = points if points.dim() == 3 else points[None]
+        out = torch.bmm(pts, self.R.to(pts.device).expand(pts.shape[0], 3, 3))
+        return out if points.dim() == 3 else out[0]
+
+    def get_matrix(self):
+        N = self.R.shape[0]
+        M = torch.eye(4, dtype=self.R.dtype, device=self.R.device).repeat(N, 1, 1)
+        M[:, :3, :3] = self.R
+        return M
