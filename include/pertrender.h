@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 1
+#define PR_ABI_VERSION 2
 
 /* error codes */
 #define PR_OK 0
@@ -71,6 +71,11 @@ typedef struct PRBlendParams {
   const float* znear;        /* (N,) camera near plane per batch element */
   const float* zfar;         /* (N,) */
   int32_t flags;             /* PR_BLEND_* */
+  /* graph-capture support (both nullable):                                    */
+  const float* scalars;      /* device [sigma, gamma, alpha]; overrides the by-value fields */
+  const uint64_t* seeds;     /* device [base]; Philox keys become mix64(base ^ seed_r/a),  */
+                             /* so a captured graph draws fresh noise after pr_seed_advance; */
+                             /* a seed_r/seed_a with bit 63 set is used as-is (fixed noise) */
 } PRBlendParams;
 
 typedef struct PRBlendFwdArgs {
@@ -118,6 +123,8 @@ typedef struct PRHeavisideArgs {
   float* grad_sigma;          /* bwd out (1,) */
   void* workspace;
   size_t workspace_bytes;
+  const float* sigma_dev;     /* nullable device sigma (overrides `sigma`) */
+  const uint64_t* seeds;      /* nullable device seed base (see PRBlendParams.seeds) */
 } PRHeavisideArgs;
 
 typedef struct PRRastArgs {
@@ -147,7 +154,31 @@ typedef struct PRInterpArgs {
   const float* grad_out;       /* bwd in (P*K,D) */
   float* grad_bary;            /* bwd out (P*K,3), nullable */
   float* grad_face_attr;       /* bwd out (F,3,D), overwritten, nullable */
+  const int64_t* faces;        /* nullable: if set, face_attr is per-VERTEX (V,D) and the kernel */
+  int64_t V;                   /* gathers attr[faces[f][i]] itself; grad_face_attr is then (V,D) */
 } PRInterpArgs;
+
+/* World -> NDC projection of every face corner (MeshRasterizer.transform + the
+ * face gather of rasterize_meshes, experiments/eval.py:165-168):
+ *   v_view = [v,1] @ world_to_view[n] ; v_clip = [v_view,1] @ proj[n]
+ *   face_verts[f,i] = (x_clip/w_clip, y_clip/w_clip, z_view)   (row-vector 4x4 matrices,
+ *   PyTorch3D Transform3d convention).  Backward scatters d face_verts into d verts. */
+typedef struct PRProjectArgs {
+  const float* verts;          /* (V,3) packed world vertices */
+  const int64_t* faces;        /* (F,3) packed vertex indices */
+  const int64_t* mesh_first_face; /* (N,) */
+  const int64_t* mesh_num_faces;  /* (N,) */
+  const float* world_to_view;  /* (N,4,4) */
+  const float* proj;           /* (N,4,4) */
+  int64_t V, F;
+  int32_t N;
+  float* face_verts;           /* fwd out (F,3,3) */
+  const float* grad_face_verts;/* bwd in (F,3,3) */
+  float* grad_verts;           /* bwd out (V,3), overwritten */
+} PRProjectArgs;
+
+int pr_project_fwd(const PRProjectArgs* args, void* stream);
+int pr_project_bwd(const PRProjectArgs* args, void* stream);
 
 int pr_abi_version(void);
 const char* pr_last_error(void);
@@ -167,6 +198,9 @@ int pr_rast_bwd(const PRRastArgs* args, void* stream);
 
 int pr_interp_fwd(const PRInterpArgs* args, void* stream);
 int pr_interp_bwd(const PRInterpArgs* args, void* stream);
+
+/* seeds[i] <- splitmix64(seeds[i]) for i < n, on the stream (capturable). */
+int pr_seed_advance(uint64_t* seeds, int32_t n, void* stream);
 
 #ifdef __cplusplus
 }

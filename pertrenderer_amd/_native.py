@@ -28,7 +28,7 @@ class PRBlendParams(C.Structure):
                 ("background", C.c_float * 3), ("noise_mode", C.c_int32),
                 ("seed_r", C.c_uint64), ("seed_a", C.c_uint64),
                 ("noise_r", _vp), ("noise_a", _vp), ("znear", _vp), ("zfar", _vp),
-                ("flags", C.c_int32)]
+                ("flags", C.c_int32), ("scalars", _vp), ("seeds", _vp)]
 
 
 class PRBlendFwdArgs(C.Structure):
@@ -50,7 +50,7 @@ class PRHeavisideArgs(C.Structure):
                 ("Sr", C.c_int32), ("sample_offset_r", C.c_int32), ("noise_mode", C.c_int32),
                 ("sigma", C.c_float), ("seed_r", C.c_uint64), ("noise_r", _vp), ("dists", _vp),
                 ("prob", _vp), ("grad_prob", _vp), ("grad_dists", _vp), ("grad_sigma", _vp),
-                ("workspace", _vp), ("workspace_bytes", C.c_size_t)]
+                ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("sigma_dev", _vp), ("seeds", _vp)]
 
 
 class PRRastArgs(C.Structure):
@@ -66,7 +66,13 @@ class PRRastArgs(C.Structure):
 class PRInterpArgs(C.Structure):
     _fields_ = [("pix_to_face", _vp), ("bary", _vp), ("face_attr", _vp), ("PK", C.c_int64),
                 ("F", C.c_int64), ("D", C.c_int32), ("out", _vp), ("grad_out", _vp),
-                ("grad_bary", _vp), ("grad_face_attr", _vp)]
+                ("grad_bary", _vp), ("grad_face_attr", _vp), ("faces", _vp), ("V", C.c_int64)]
+
+
+class PRProjectArgs(C.Structure):
+    _fields_ = [("verts", _vp), ("faces", _vp), ("mesh_first_face", _vp), ("mesh_num_faces", _vp),
+                ("world_to_view", _vp), ("proj", _vp), ("V", C.c_int64), ("F", C.c_int64), ("N", C.c_int32),
+                ("face_verts", _vp), ("grad_face_verts", _vp), ("grad_verts", _vp)]
 
 
 # every symbol include/pertrender.h declares, with its argument struct (None = no args)
@@ -85,8 +91,11 @@ EXPORTS = {
     "pr_rast_bwd": (C.c_int, [C.POINTER(PRRastArgs), _vp]),
     "pr_interp_fwd": (C.c_int, [C.POINTER(PRInterpArgs), _vp]),
     "pr_interp_bwd": (C.c_int, [C.POINTER(PRInterpArgs), _vp]),
+    "pr_seed_advance": (C.c_int, [_vp, C.c_int32, _vp]),
+    "pr_project_fwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
+    "pr_project_bwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
 }
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 

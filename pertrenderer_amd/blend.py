@@ -9,8 +9,9 @@
 Gradients follow the reference's custom backward passes, including
 its quirks: d sigma = sum(gmaps * dP) (smoothrast.py:57-58) and |eps|^2 over all K+1
 logits in d gamma (smoothagg.py:54).  sigma / gamma / alpha may be CPU 0-d leaves
-(smoothrast.py:116, smoothagg.py:153-154); their gradients are returned as 0-d
-tensors that autograd moves to the leaves' device.
+(smoothrast.py:116, smoothagg.py:153-154: values passed by value, gradients returned
+as 0-d tensors that autograd moves to the CPU) or device tensors (passed by pointer:
+no host synchronisation, so the step can be captured in a HIP graph).
 """
 import torch
 
@@ -20,10 +21,7 @@ from . import timing as _timing
 from .noise import Noise
 
 F32 = torch.float32
-
-
-def _f(x):
-    return float(x.detach().cpu()) if torch.is_tensor(x) else float(x)
+_ABS = 1 << 63  # absolute-key marker (see PRBlendParams.seeds)
 
 
 def _planes(z, N, device):
@@ -51,13 +49,22 @@ def _contig(t, dtype=F32):
     return t.detach().to(dtype).contiguous()
 
 
-def _params(shape, Sr, Sa, sigma, gamma, alpha, eps, bg, noise, znear, zfar, flags):
+def _scalars(vals, device):
+    """(host floats, device tensor or None) for the smoothing scalars.  All-device inputs are
+    passed by pointer (capture-safe); otherwise their values are read on the host."""
+    if all(torch.is_tensor(v) and v.is_cuda for v in vals):
+        dev = torch.stack([v.detach().reshape(()).to(F32) for v in vals]).contiguous()
+        return (0.0,) * len(vals), dev
+    return tuple(float(v.detach().cpu()) if torch.is_tensor(v) else float(v) for v in vals), None
+
+
+def _params(shape, Sr, Sa, sc, sc_dev, eps, bg, noise, znear, zfar, flags):
     N, H, W, K = shape
     p = nat.PRBlendParams()
     p.N, p.H, p.W, p.K = N, H, W, K
     p.Sr, p.Sa = int(Sr), int(Sa)
     p.sample_offset_r, p.sample_offset_a = noise.offset_r, noise.offset_a
-    p.sigma, p.gamma, p.alpha, p.eps = sigma, gamma, alpha, eps
+    p.sigma, p.gamma, p.alpha, p.eps = sc[0], sc[1], sc[2], eps
     for i in range(3):
         p.background[i] = bg[i]
     p.noise_mode = noise.mode
@@ -65,6 +72,8 @@ def _params(shape, Sr, Sa, sigma, gamma, alpha, eps, bg, noise, znear, zfar, fla
     p.noise_r, p.noise_a = nat.ptr(noise.noise_r), nat.ptr(noise.noise_a)
     p.znear, p.zfar = nat.ptr(znear), nat.ptr(zfar)
     p.flags = flags
+    p.scalars = nat.ptr(sc_dev)
+    p.seeds = nat.ptr(noise.seeds)
     return p
 
 
@@ -78,11 +87,30 @@ def _check_injected(noise, Sr, Sa, shape, need_r, need_a):
         raise ValueError(f"injected noise_a must have shape {(Sa, N, H, W, K + 1)}")
 
 
+def _merge(nr, na):
+    """One Noise for the fused call from the rast draw and the agg draw."""
+    if nr.mode != na.mode:
+        raise ValueError("rast and agg noise must use the same source")
+    seeds = nr.seeds if nr.seeds is not None else na.seeds
+    seed_r, seed_a = nr.seed_r, na.seed_a
+    if seeds is not None:  # a host-keyed draw next to a device-seeded one keeps its key verbatim
+        seed_r = seed_r if nr.seeds is not None else seed_r | _ABS
+        seed_a = seed_a if na.seeds is not None else seed_a | _ABS
+    return Noise(nr.mode, seed_r, seed_a, nr.noise_r, na.noise_a, nr.offset_r, na.offset_a, seeds)
+
+
 def _scalar_grads(gs, needs, refs):
-    out = []
-    for i, (need, ref) in enumerate(zip(needs, refs)):
-        out.append(gs[i].to(dtype=ref.dtype) if (need and torch.is_tensor(ref)) else None)
-    return out
+    return [gs[i].to(dtype=ref.dtype) if (need and torch.is_tensor(ref)) else None
+            for i, (need, ref) in enumerate(zip(needs, refs))]
+
+
+def _timed(name, fn):
+    hook = _timing.active()
+    if hook is not None:
+        hook.start(name)
+    fn()
+    if hook is not None:
+        hook.stop(name)
 
 
 # ============================================================== fused blend
@@ -97,8 +125,8 @@ class _FusedBlendFn(torch.autograd.Function):
         d_c, z_c, c_c = _contig(dists), _contig(zbuf), _contig(colors)
         zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
         noise = cfg["noise"].to(dev)
-        sc = (_f(sigma), _f(gamma), _f(alpha))
-        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], *sc, cfg["eps"], cfg["bg"], noise, zn, zf,
+        sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
+        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf,
                     nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR)
         image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
@@ -106,31 +134,23 @@ class _FusedBlendFn(torch.autograd.Function):
         a.p = p
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
         a.image, a.winners = nat.ptr(image), nat.ptr(winners)
-        hook = _timing.active()
-        if hook is not None:
-            hook.start("blend_fwd")
-        nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd")
-        if hook is not None:
-            hook.stop("blend_fwd")
-        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, sigma if torch.is_tensor(sigma) else None,
-                              gamma if torch.is_tensor(gamma) else None,
-                              alpha if torch.is_tensor(alpha) else None)
+        _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
+        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, sc_dev)
         ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
+        ctx.refs = (sigma, gamma, alpha)
         return image
 
     @staticmethod
     def backward(ctx, gimg):
-        p2f_c, d_c, z_c, c_c, zn, zf, winners, sig, gam, alp = ctx.saved_tensors
+        p2f_c, d_c, z_c, c_c, zn, zf, winners, sc_dev = ctx.saved_tensors
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
         lib = nat.load()
         N, H, W, K = p2f_c.shape
         dev = p2f_c.device
-        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], *sc, cfg["eps"], cfg["bg"], noise, zn, zf,
+        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf,
                     nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR)
         g = gimg.detach().to(F32).contiguous()
-        gd = torch.empty_like(d_c)
-        gz = torch.empty_like(z_c)
-        gc = torch.empty_like(c_c)
+        gd, gz, gc = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(c_c)
         gsc = torch.empty(3, dtype=F32, device=dev)
         a = nat.PRBlendBwdArgs()
         a.p = p
@@ -139,14 +159,9 @@ class _FusedBlendFn(torch.autograd.Function):
         a.grad_dists, a.grad_zbuf, a.grad_colors, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gc), nat.ptr(gsc)
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
-        hook = _timing.active()
-        if hook is not None:
-            hook.start("blend_bwd")
-        nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd")
-        if hook is not None:
-            hook.stop("blend_bwd")
+        _timed("blend_bwd", lambda: nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd"))
         need = ctx.needs_input_grad
-        s_g, g_g, a_g = _scalar_grads(gsc, need[3:6], (sig, gam, alp))
+        s_g, g_g, a_g = _scalar_grads(gsc, need[3:6], ctx.refs)
         return (gd if need[0] else None, gz if need[1] else None, gc if need[2] else None,
                 s_g, g_g, a_g, None, None, None, None)
 
@@ -167,7 +182,7 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
     if noise is None:
         nr = noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device)
         na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise)
-        noise = Noise(nr.mode, nr.seed_r, na.seed_a, nr.noise_r, na.noise_a, 0, 0)
+        noise = _merge(nr, na)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise)
@@ -175,35 +190,37 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
 
 
 # ==================================================== standalone heaviside
+def _heaviside_args(shape, Sr, noise, sigma_val, sigma_dev, d_c):
+    N, H, W, K = shape
+    a = nat.PRHeavisideArgs()
+    a.N, a.H, a.W, a.K, a.Sr = N, H, W, K, int(Sr)
+    a.sample_offset_r, a.noise_mode, a.sigma = noise.offset_r, noise.mode, sigma_val
+    a.seed_r, a.noise_r, a.dists = noise.seed_r & (2 ** 64 - 1), nat.ptr(noise.noise_r), nat.ptr(d_c)
+    a.sigma_dev, a.seeds = nat.ptr(sigma_dev), nat.ptr(noise.seeds)
+    return a
+
+
 class _HeavisideFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, dists, sigma, Sr, noise):
         nat.require_device(dists)
         lib = nat.load()
-        N, H, W, K = dists.shape
         d_c = _contig(dists)
         noise = noise.to(d_c.device)
-        a = nat.PRHeavisideArgs()
-        a.N, a.H, a.W, a.K, a.Sr = N, H, W, K, int(Sr)
-        a.sample_offset_r, a.noise_mode, a.sigma = noise.offset_r, noise.mode, _f(sigma)
-        a.seed_r, a.noise_r, a.dists = noise.seed_r & (2 ** 64 - 1), nat.ptr(noise.noise_r), nat.ptr(d_c)
+        (sv,), sdev = _scalars((sigma,), d_c.device)
+        a = _heaviside_args(tuple(d_c.shape), Sr, noise, sv, sdev, d_c)
         prob = torch.empty_like(d_c)
         a.prob = nat.ptr(prob)
         nat.check(lib.pr_heaviside_fwd(a, nat.stream_of(prob)), "pr_heaviside_fwd")
-        ctx.save_for_backward(d_c, sigma if torch.is_tensor(sigma) else None)
-        ctx.noise, ctx.Sr, ctx.sigma = noise, int(Sr), _f(sigma)
+        ctx.save_for_backward(d_c, sdev)
+        ctx.noise, ctx.Sr, ctx.sv, ctx.sigma_ref = noise, int(Sr), sv, sigma
         return prob
 
     @staticmethod
     def backward(ctx, gP):
-        d_c, sig = ctx.saved_tensors
+        d_c, sdev = ctx.saved_tensors
         lib = nat.load()
-        N, H, W, K = d_c.shape
-        noise = ctx.noise
-        a = nat.PRHeavisideArgs()
-        a.N, a.H, a.W, a.K, a.Sr = N, H, W, K, ctx.Sr
-        a.sample_offset_r, a.noise_mode, a.sigma = noise.offset_r, noise.mode, ctx.sigma
-        a.seed_r, a.noise_r, a.dists = noise.seed_r & (2 ** 64 - 1), nat.ptr(noise.noise_r), nat.ptr(d_c)
+        a = _heaviside_args(tuple(d_c.shape), ctx.Sr, ctx.noise, ctx.sv, sdev, d_c)
         g = gP.detach().to(F32).contiguous()
         gd = torch.empty_like(d_c)
         gs = torch.empty(1, dtype=F32, device=d_c.device)
@@ -212,7 +229,8 @@ class _HeavisideFn(torch.autograd.Function):
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         nat.check(lib.pr_heaviside_bwd(a, nat.stream_of(g)), "pr_heaviside_bwd")
         need = ctx.needs_input_grad
-        sg = gs[0].to(sig.dtype) if (need[1] and sig is not None) else None
+        ref = ctx.sigma_ref
+        sg = gs[0].to(ref.dtype) if (need[1] and torch.is_tensor(ref)) else None
         return (gd if need[0] else None), sg, None, None
 
 
@@ -238,8 +256,9 @@ class _AggregateFn(torch.autograd.Function):
         m_c = mask.detach().to(torch.uint8).contiguous()
         zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
         noise = cfg["noise"].to(dev)
-        sc = (1.0, _f(gamma), _f(alpha))
-        p = _params((N, H, W, K), 1, cfg["Sa"], *sc, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf, 0)
+        one = torch.ones((), dtype=F32, device=dev) if (torch.is_tensor(gamma) and gamma.is_cuda) else 1.0
+        sc, sc_dev = _scalars((one, gamma, alpha), dev)
+        p = _params((N, H, W, K), 1, cfg["Sa"], sc, sc_dev, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf, 0)
         weights = torch.empty((N, H, W, K + 1), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
         a = nat.PRBlendFwdArgs()
@@ -247,19 +266,18 @@ class _AggregateFn(torch.autograd.Function):
         a.mask, a.prob, a.zbuf = nat.ptr(m_c), nat.ptr(p_c), nat.ptr(z_c)
         a.weights, a.winners = nat.ptr(weights), nat.ptr(winners)
         nat.check(lib.pr_blend_fwd(a, nat.stream_of(weights)), "pr_blend_fwd(aggregate)")
-        ctx.save_for_backward(z_c, p_c, m_c, zn, zf, winners, gamma if torch.is_tensor(gamma) else None,
-                              alpha if torch.is_tensor(alpha) else None)
-        ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
+        ctx.save_for_backward(z_c, p_c, m_c, zn, zf, winners, sc_dev)
+        ctx.cfg, ctx.noise, ctx.sc, ctx.refs = cfg, noise, sc, (gamma, alpha)
         return weights
 
     @staticmethod
     def backward(ctx, gW):
-        z_c, p_c, m_c, zn, zf, winners, gam, alp = ctx.saved_tensors
+        z_c, p_c, m_c, zn, zf, winners, sc_dev = ctx.saved_tensors
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
         lib = nat.load()
         N, H, W, K = z_c.shape
         dev = z_c.device
-        p = _params((N, H, W, K), 1, cfg["Sa"], *sc, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf, 0)
+        p = _params((N, H, W, K), 1, cfg["Sa"], sc, sc_dev, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf, 0)
         g = gW.detach().to(F32).contiguous()
         gz, gp = torch.empty_like(z_c), torch.empty_like(p_c)
         gsc = torch.empty(3, dtype=F32, device=dev)
@@ -271,7 +289,7 @@ class _AggregateFn(torch.autograd.Function):
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd(aggregate)")
         need = ctx.needs_input_grad
-        _, g_g, a_g = _scalar_grads(gsc, (False, need[2], need[3]), (None, gam, alp))
+        _, g_g, a_g = _scalar_grads(gsc, (False, need[2], need[3]), (None,) + ctx.refs)
         return (gz if need[0] else None, gp if need[1] else None, g_g, a_g, None, None, None, None)
 
 

@@ -8,59 +8,106 @@
 //   random_rasterizer.py:34-56  smooth_rgb_blend    (alpha product, colour mix)
 // Closed-form backward: SURVEY.md §3.2, restated in oracle/blend_oracle.py.
 //
-// MI355X layout: one workgroup (4 waves) owns PB consecutive pixels.  Every
-// fragment byte is read with flat, fully-coalesced loops over the block's
-// contiguous (PB*K)-slot range; per-slot intermediates live in LDS; per-pixel
-// reductions run from LDS; the agg Monte-Carlo loop runs one thread per
-// (pixel, 4-sample Philox group, slot chunk) and combines chunk partials with
-// wave shuffles.  Nothing of size S*P*K is ever materialised: noise is
-// regenerated from Philox (or read from injected tensors in parity mode).
+// MI355X layout.  One 256-thread workgroup (4 waves) owns PB <= 32 consecutive
+// pixels, i.e. one contiguous (PB*K)-slot range of every fragment tensor:
+//   * slot phases: thread t walks slots t, t+256, ... of the range (fully
+//     coalesced loads/stores, (pixel, slot) tracked incrementally: no integer
+//     division in the loop); per-slot intermediates go to LDS;
+//   * pixel phases: 8 lanes per pixel (32 pixels = 256 threads) reduce over the
+//     pixel's slots with xor-shuffles inside the 8-lane group;
+//   * the agg Monte-Carlo argmax runs one thread per (pixel, 4-sample Philox
+//     group, slot chunk) and merges chunk partials with shuffles.
+// Nothing of size S x P x K is materialised: noise is regenerated from Philox
+// (or read from injected tensors in parity mode).  In Philox mode two exact
+// skips remove RNG work without changing any result: a rast slot whose
+// threshold Phi(d/sigma) lies outside [2^-24, 1-2^-24] has the same outcome for
+// every 24-bit uniform, and an agg logit more than 2*5.8*gamma below the
+// pixel's largest logit can never win (Box-Muller |eps| <= 5.77 for 24-bit u).
 #include "pr_common.h"
 
 namespace pr {
 namespace {
 
 constexpr float kNegInf = -__builtin_inff();
+constexpr float kEpsMaxBM = 5.8f;               // > sqrt(-2 ln 2^-24) = 5.7683
+constexpr float kULo = 5.9604644775390625e-08f;  // smallest uniform (2^-24)
+constexpr float kUHi = 1.0f - 5.9604644775390625e-08f;
 
 struct Geo {
   int64_t P, PK;  // pixels, slots
-  int K, KP1;
-  int PB;         // pixels per block
+  int K, KP1, PB, HW;
+  int qK, rK, qK1, rK1, qS, rS;  // 256 / {K, K+1, Sa} and remainders
+  int ck;                        // contiguous per-lane chunk for 8-lane pixel phases: ceil((K+1)/8)
 };
+
+struct Sc {
+  float sigma, gamma, alpha;
+  uint64_t kr, ka;
+};
+
+PR_DEV uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+PR_DEV Sc resolve(const PRBlendParams& p) {
+  Sc s{p.sigma, p.gamma, p.alpha, p.seed_r, p.seed_a};
+  if (p.scalars) { s.sigma = p.scalars[0]; s.gamma = p.scalars[1]; s.alpha = p.scalars[2]; }
+  if (p.seeds) {  // bit 63 marks an absolute key that ignores the device base (fixed noise)
+    const uint64_t b = p.seeds[0];
+    if (!(p.seed_r >> 63)) s.kr = mix64(b ^ p.seed_r);
+    if (!(p.seed_a >> 63)) s.ka = mix64(b ^ p.seed_a);
+  }
+  return s;
+}
 
 PR_DEV bool slot_mask(const int64_t* p2f, const uint8_t* mask, int64_t gs) {
   return p2f ? (p2f[gs] >= 0) : (mask[gs] != 0);
 }
 
+// image index of block pixel pl (n0 / rem0 = image and offset of the block's first pixel)
+PR_DEV int image_of(int n0, int rem0, int pl, int HW) {
+  int r = rem0 + pl, n = n0;
+  while (r >= HW) { r -= HW; ++n; }
+  return n;
+}
+
+// slot loop over [0, n) of a block with row length L: thread walks i = tid + 256*it,
+// (pl, k) = divmod(i, L) maintained incrementally
+#define PR_FOR_SLOTS(L, Q, R, NTOT)                                                      \
+  for (int i_ = tid, pl = tid / (L), k = tid - (tid / (L)) * (L); i_ < (NTOT);          \
+       i_ += kThreads, pl += (Q), k += (R), (k >= (L) ? (k -= (L), ++pl) : 0))
+
 // ---------------------------------------------------------------- rast noise
-// Forward count of "inside" samples for one valid slot.  Injected mode follows
-// smoothrast.py:32-33 literally: H(D + sigma*eps) with H(0)=1.
+// Count of "inside" samples for one valid slot.  Injected mode is smoothrast.py:32-33
+// literally: H(D + sigma*eps) with H(0)=1, D = -dist.
 template <int NOISE>
-PR_DEV int rast_count(const PRBlendParams& p, float dist, uint32_t gp, int k, int64_t gs, int64_t PK) {
+PR_DEV int rast_count(const PRBlendParams& p, const Sc& sc, float dist, uint32_t gp, int k, int64_t gs,
+                      int64_t PK) {
   int cnt = 0;
   if constexpr (NOISE == PR_NOISE_INJECTED) {
     const float D = -dist;
-    for (int s = 0; s < p.Sr; ++s) {
-      const float x = D + p.sigma * p.noise_r[(int64_t)s * PK + gs];
-      cnt += x >= 0.f ? 1 : 0;
-    }
+    for (int s = 0; s < p.Sr; ++s) cnt += (D + sc.sigma * p.noise_r[(int64_t)s * PK + gs]) >= 0.f ? 1 : 0;
   } else {
-    const float c = rast_threshold(dist, p.sigma);
+    const float c = rast_threshold(dist, sc.sigma);
+    if (c <= kULo) return p.Sr;   // every uniform is >= c
+    if (c > kUHi) return 0;       // every uniform is < c
     U4 u{};
     for (int s = 0; s < p.Sr; ++s) {
       const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
-      if (s == 0 || (sg & 3u) == 0) u = philox_block(p.seed_r, gp, (uint32_t)k, sg >> 2, kTagRast);
+      if (s == 0 || (sg & 3u) == 0) u = philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast);
       cnt += u01(word(u, sg & 3u)) >= c ? 1 : 0;
     }
   }
   return cnt;
 }
 
-// Backward: count and the variance-reduced score sum_s ((m_s - vr) * eps_s) / sigma
-// (smoothrast.py:46,53).  In Philox mode eps = Phi^-1(u) is only evaluated for
-// samples whose decision differs from vr (the term is 0 otherwise).
+// Count and the variance-reduced score sum_s ((m_s - vr) * eps_s) / sigma
+// (smoothrast.py:46,53).  Philox mode evaluates eps = Phi^-1(u) only where the
+// sample's decision differs from vr (the term is 0 otherwise).
 template <int NOISE>
-PR_DEV int rast_count_score(const PRBlendParams& p, float dist, uint32_t gp, int k, int64_t gs,
+PR_DEV int rast_count_score(const PRBlendParams& p, const Sc& sc, float dist, uint32_t gp, int k, int64_t gs,
                             int64_t PK, float& gacc) {
   int cnt = 0;
   const float D = -dist;
@@ -69,31 +116,33 @@ PR_DEV int rast_count_score(const PRBlendParams& p, float dist, uint32_t gp, int
   if constexpr (NOISE == PR_NOISE_INJECTED) {
     for (int s = 0; s < p.Sr; ++s) {
       const float e = p.noise_r[(int64_t)s * PK + gs];
-      const float m = heaviside1(D + p.sigma * e);
+      const float m = heaviside1(D + sc.sigma * e);
       cnt += (int)m;
-      gacc += ((m - vr) * e) / p.sigma;
+      gacc += ((m - vr) * e) / sc.sigma;
     }
   } else {
-    const float c = rast_threshold(dist, p.sigma);
+    const float c = rast_threshold(dist, sc.sigma);
+    if (c <= kULo) return p.Sr;  // all inside: m = vr = 1, no score
+    if (c > kUHi) return 0;      // all outside: m = vr = 0
     U4 u{};
     for (int s = 0; s < p.Sr; ++s) {
       const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
-      if (s == 0 || (sg & 3u) == 0) u = philox_block(p.seed_r, gp, (uint32_t)k, sg >> 2, kTagRast);
+      if (s == 0 || (sg & 3u) == 0) u = philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast);
       const float uu = u01(word(u, sg & 3u));
       const float m = uu >= c ? 1.f : 0.f;
       cnt += (int)m;
-      if (m != vr) gacc += ((m - vr) * normcdfinvf(uu)) / p.sigma;
+      if (m != vr) gacc += ((m - vr) * normcdfinvf(uu)) / sc.sigma;
     }
   }
   return cnt;
 }
 
 // --------------------------------------------------------------- agg noise
-// 4 consecutive samples [4g, 4g+4) of slot j of pixel gp.  Injected mode reads
-// local sample indices s0.. (sample_offset_a is 0 there).
+// 4 consecutive samples [4g, 4g+4) of slot j of pixel gp.  Injected mode reads the
+// caller's (Sa, P, K+1) tensor at local sample indices (sample offsets are 0 there).
 template <int NOISE>
-PR_DEV void agg_noise4(const PRBlendParams& p, uint32_t gp, int j, uint32_t g, int64_t P, int KP1,
-                       float e[4]) {
+PR_DEV void agg_noise4(const PRBlendParams& p, const Sc& sc, uint32_t gp, int j, uint32_t g, int64_t P,
+                       int KP1, float e[4]) {
   if constexpr (NOISE == PR_NOISE_INJECTED) {
     const int64_t PKa = P * KP1;
 #pragma unroll
@@ -102,117 +151,116 @@ PR_DEV void agg_noise4(const PRBlendParams& p, uint32_t gp, int j, uint32_t g, i
       e[i] = s < p.Sa ? p.noise_a[(int64_t)s * PKa + (int64_t)gp * KP1 + j] : 0.f;
     }
   } else {
-    gauss4(philox_block(p.seed_a, gp, (uint32_t)j, g, kTagAgg), e);
+    gauss4(philox_block(sc.ka, gp, (uint32_t)j, g, kTagAgg), e);
   }
 }
 
-// sample-group bookkeeping: local samples [0,Sa) map to global [off, off+Sa)
-PR_DEV int agg_first_group(const PRBlendParams& p) { return (p.sample_offset_a) >> 2; }
+PR_DEV int agg_first_group(const PRBlendParams& p) { return p.sample_offset_a >> 2; }
 PR_DEV int agg_num_groups(const PRBlendParams& p) {
   return ((p.sample_offset_a + p.Sa - 1) >> 2) - (p.sample_offset_a >> 2) + 1;
 }
 
 // ================================================================== forward
 template <int NOISE, bool RAST, bool COLOR>
-__global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, Geo geo, int NC) {
+__global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, Geo g, int NC) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
-  const int K = geo.K, KP1 = geo.KP1, PB = geo.PB;
-  float* A = smem;                       // [PB][KP1] prob, then int win counts
-  float* B = A + PB * KP1;               // [PB][KP1] z_inv, then logits z
-  float* PX = B + PB * KP1;              // [PB][2]   zmax, alpha
+  const Sc sc = resolve(p);
+  const int K = g.K, KP1 = g.KP1, PB = g.PB;
+  float* A = smem;                 // [PB][KP1] prob, then int win counts
+  float* B = A + PB * KP1;         // [PB][KP1] z_inv, then logits z
+  float* PX = B + PB * KP1;        // [PB][4] z_max, alpha, max logit
   int* CNT = reinterpret_cast<int*>(A);
   const int tid = threadIdx.x;
   const int64_t pix0 = (int64_t)blockIdx.x * PB;
-  const int npix = (int)min((int64_t)PB, geo.P - pix0);
-  if (npix <= 0) return;
+  const int npix = (int)min((int64_t)PB, g.P - pix0);
+  const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
 
-  // ---- 1: slots (coalesced): mask, probability, z_inv
-  for (int i = tid; i < npix * K; i += kThreads) {
-    const int pl = i / K, k = i - pl * K;
+  // ---- 1: slots: mask, probability, z_inv
+  PR_FOR_SLOTS(K, g.qK, g.rK, npix * K) {
     const int64_t gp = pix0 + pl, gs = gp * K + k;
     const bool m = slot_mask(a.pix_to_face, a.mask, gs);
     const float mf = m ? 1.f : 0.f;
     float prob;
     if constexpr (RAST) {
-      if (m) {
-        const int cnt = rast_count<NOISE>(p, a.dists[gs], (uint32_t)gp, k, gs, geo.PK);
-        prob = ((float)cnt / (float)p.Sr) * mf;
-      } else {
-        prob = 0.f;
-      }
+      prob = m ? ((float)rast_count<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK) / (float)p.Sr) * mf
+               : 0.f;
     } else {
       prob = a.prob[gs];
     }
-    const int n = (int)(gp / ((int64_t)p.H * p.W));
+    const int n = image_of(n0, rem0, pl, g.HW);
     const float zf = p.zfar[n], zn = p.znear[n];
     A[pl * KP1 + k] = prob;
     B[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
   }
   __syncthreads();
 
-  // ---- 2: per pixel: alpha = prod(1 - prob), z_max = clamp(max z_inv, eps)
-  if (tid < npix) {
+  // ---- 2: per pixel (8 lanes): alpha, z_max, logits, largest logit
+  {
+    const int pl = tid >> 3, l = tid & 7;
+    const bool act = pl < npix;
+    const int j0 = l * g.ck, j1 = min(KP1, j0 + g.ck), k1 = min(K, j1);
     float al = 1.f, zm = kNegInf;
-    for (int k = 0; k < K; ++k) {
-      al *= (1.f - A[tid * KP1 + k]);
-      const float zi = B[tid * KP1 + k];
-      if (zi > zm) zm = zi;
+    if (act)
+      for (int k = j0; k < k1; ++k) {
+        al *= (1.f - A[pl * KP1 + k]);
+        zm = fmaxf(zm, B[pl * KP1 + k]);
+      }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      al *= __shfl_xor(al, m);
+      zm = fmaxf(zm, __shfl_xor(zm, m));
     }
-    PX[tid * 2 + 0] = zm < p.eps ? p.eps : zm;
-    PX[tid * 2 + 1] = al;
+    const float zmax = zm < p.eps ? p.eps : zm;
+    const float gal = sc.gamma / sc.alpha;
+    float zl = kNegInf;
+    if (act)
+      for (int j = j0; j < j1; ++j) {
+        const float z = j < K ? gal * logf(A[pl * KP1 + j]) + B[pl * KP1 + j] - zmax : p.eps - zmax;
+        B[pl * KP1 + j] = z;
+        CNT[pl * KP1 + j] = 0;
+        zl = fmaxf(zl, z);
+      }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) zl = fmaxf(zl, __shfl_xor(zl, m));
+    if (act && l == 0) {
+      PX[pl * 4 + 0] = zmax;
+      PX[pl * 4 + 1] = al;
+      PX[pl * 4 + 2] = zl;
+    }
   }
   __syncthreads();
 
-  // ---- 3: logits z_k = (gamma/alpha)*log prob + z_inv - z_max ; z_K = eps - z_max
-  const float gal = p.gamma / p.alpha;
-  for (int i = tid; i < npix * KP1; i += kThreads) {
-    const int pl = i / KP1, k = i - pl * KP1;
-    const float zmax = PX[pl * 2];
-    float z;
-    if (k < K) {
-      z = gal * logf(A[pl * KP1 + k]) + B[pl * KP1 + k] - zmax;
-    } else {
-      z = p.eps - zmax;
-    }
-    B[pl * KP1 + k] = z;
-    CNT[pl * KP1 + k] = 0;
-  }
-  __syncthreads();
-
-  // ---- 4: Monte-Carlo argmax: thread = (pixel, 4-sample group, slot chunk)
+  // ---- 3: Monte-Carlo argmax: thread = (pixel, 4-sample group, slot chunk)
   {
     const int ng = agg_num_groups(p), g0 = agg_first_group(p);
     const int CS = (KP1 + NC - 1) / NC;
     const int npairs = npix * ng * NC;
+    const float skipm = NOISE == PR_NOISE_PHILOX ? 2.f * kEpsMaxBM * sc.gamma : __builtin_inff();
     for (int base = 0; base < npairs; base += kThreads) {
       const int t = base + tid;
       const bool act = t < npairs;
-      const int c = t % NC, pg = t / NC;
-      const int pl = act ? pg / ng : 0, gi = act ? pg - (pg / ng) * ng : 0;
-      const uint32_t g = (uint32_t)(g0 + gi);
+      const int c = t & (NC - 1), pg = t / NC;
+      const int pl = act ? pg / ng : 0, gi = act ? pg - pl * ng : 0;
+      const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
       const int64_t gp = pix0 + pl;
       float best[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
       int bidx[4] = {-1, -1, -1, -1};
       if (act) {
+        const float zfloor = PX[pl * 4 + 2] - skipm;
         const int j1 = min(KP1, (c + 1) * CS);
         for (int j = c * CS; j < j1; ++j) {
           const float z = B[pl * KP1 + j];
-          if (!(z > kNegInf)) continue;  // -inf logits never win (masked / zero prob)
+          if (!(z > kNegInf) || !(z >= zfloor)) continue;  // can never be the argmax
           float e[4];
-          if constexpr (NOISE == PR_NOISE_INJECTED) {
-            agg_noise4<NOISE>(p, (uint32_t)gp, j, (uint32_t)gi, geo.P, KP1, e);
-          } else {
-            agg_noise4<NOISE>(p, (uint32_t)gp, j, g, geo.P, KP1, e);
-          }
+          agg_noise4<NOISE>(p, sc, (uint32_t)gp, j, gg, g.P, KP1, e);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float v = z + p.gamma * e[q];
+            const float v = z + sc.gamma * e[q];
             if (v > best[q]) { best[q] = v; bidx[q] = j; }
           }
         }
       }
-      // combine chunk partials (lanes t..t+NC-1 of one wave), lower index wins ties
       for (int m = 1; m < NC; m <<= 1) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -226,9 +274,7 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
       if (act && c == 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          int s;
-          if constexpr (NOISE == PR_NOISE_INJECTED) s = 4 * gi + q;
-          else s = (int)(4 * g) + q - p.sample_offset_a;
+          const int s = (int)(4 * gg) + q - (NOISE == PR_NOISE_INJECTED ? 0 : p.sample_offset_a);
           if (s < 0 || s >= p.Sa) continue;
           const int w = bidx[q] < 0 ? K : bidx[q];
           a.winners[gp * p.Sa + s] = (uint8_t)w;
@@ -239,43 +285,40 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
   }
   __syncthreads();
 
-  // ---- 5: outputs
+  // ---- 4: outputs
   const float fSa = (float)p.Sa;
   if constexpr (COLOR) {
-    // 8 lanes per pixel sweep the pixel's contiguous K*3 colours
-    for (int base = 0; base < npix * 8; base += kThreads) {
-      const int t = base + tid;
-      const int pl = t >> 3, l = t & 7;
-      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
-      if (pl < npix) {
-        const int64_t gp = pix0 + pl;
-        const float* col = a.colors + gp * K * 3;
-        for (int k = l; k < K; k += 8) {
-          const float w = (float)CNT[pl * KP1 + k] / fSa;
-          acc0 += w * col[k * 3 + 0];
-          acc1 += w * col[k * 3 + 1];
-          acc2 += w * col[k * 3 + 2];
-        }
-      }
-      for (int m = 1; m < 8; m <<= 1) {
-        acc0 += __shfl_xor(acc0, m);
-        acc1 += __shfl_xor(acc1, m);
-        acc2 += __shfl_xor(acc2, m);
-      }
-      if (pl < npix && l == 0) {
-        const int64_t gp = pix0 + pl;
-        const float wb = (float)CNT[pl * KP1 + K] / fSa;
-        float4 o;
-        o.x = acc0 + wb * p.background[0];
-        o.y = acc1 + wb * p.background[1];
-        o.z = acc2 + wb * p.background[2];
-        o.w = 1.f - PX[pl * 2 + 1];
-        reinterpret_cast<float4*>(a.image)[gp] = o;
+    // 8 lanes per pixel sweep the pixel's contiguous K*3 colours (8 slots = 96 B per step)
+    const int pl = tid >> 3, l = tid & 7;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
+    if (pl < npix) {
+      const float* col = a.colors + (pix0 + pl) * K * 3;
+      for (int k = l; k < K; k += 8) {
+        const int cw = CNT[pl * KP1 + k];
+        if (cw == 0) continue;
+        const float w = (float)cw / fSa;
+        acc0 += w * col[k * 3 + 0];
+        acc1 += w * col[k * 3 + 1];
+        acc2 += w * col[k * 3 + 2];
       }
     }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      acc0 += __shfl_xor(acc0, m);
+      acc1 += __shfl_xor(acc1, m);
+      acc2 += __shfl_xor(acc2, m);
+    }
+    if (pl < npix && l == 0) {
+      const float wb = (float)CNT[pl * KP1 + K] / fSa;
+      float4 o;
+      o.x = acc0 + wb * p.background[0];
+      o.y = acc1 + wb * p.background[1];
+      o.z = acc2 + wb * p.background[2];
+      o.w = 1.f - PX[pl * 4 + 1];
+      reinterpret_cast<float4*>(a.image)[pix0 + pl] = o;
+    }
   } else {
-    for (int i = tid; i < npix * KP1; i += kThreads) {
-      const int pl = i / KP1, k = i - pl * KP1;
+    PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
       a.weights[(pix0 + pl) * KP1 + k] = (float)CNT[pl * KP1 + k] / fSa;
     }
   }
@@ -283,245 +326,264 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
 
 // ================================================================= backward
 template <int NOISE, bool RAST, bool COLOR>
-__global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, Geo geo, float* partials) {
+__global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
-  const int K = geo.K, KP1 = geo.KP1, PB = geo.PB;
+  const Sc sc = resolve(p);
+  const int K = g.K, KP1 = g.KP1, PB = g.PB;
   const int Sa = p.Sa;
-  float* PR = smem;                 // [PB][KP1] prob
-  float* ZZ = PR + PB * KP1;        // [PB][KP1] z_inv -> z
-  float* GM = ZZ + PB * KP1;        // [PB][KP1] rast score mean (gmaps)
-  float* EX = GM + PB * KP1;        // [PB][KP1] exclusive products of (1-prob)
-  float* DW = EX + PB * KP1;        // [PB][KP1] dL/dW
-  float* DZ = DW + PB * KP1;        // [PB][KP1] dL/dz
-  int* CN = reinterpret_cast<int*>(DZ + PB * KP1);  // [PB][KP1] win counts
+  float* PR = smem;                    // [PB][KP1] prob
+  float* ZZ = PR + PB * KP1;           // [PB][KP1] z_inv -> z -> dL/dz
+  float* GM = ZZ + PB * KP1;           // [PB][KP1] rast score mean (gmaps)
+  float* EX = GM + PB * KP1;           // [PB][KP1] exclusive products of (1 - prob)
+  float* DW = EX + PB * KP1;           // [PB][KP1] dL/dW
+  int* CN = reinterpret_cast<int*>(DW + PB * KP1);      // [PB][KP1] win counts
   float* AS = reinterpret_cast<float*>(CN + PB * KP1);  // [PB][Sa] a_s
-  float* PX = AS + PB * Sa;         // [PB][8] per-pixel scalars
-  float* RED = PX + PB * 8;         // [kThreads][4] reduction scratch
+  float* PX = AS + PB * Sa;            // [PB][8] per-pixel scalars
   const int tid = threadIdx.x;
   const int64_t pix0 = (int64_t)blockIdx.x * PB;
-  const int npix = (int)min((int64_t)PB, geo.P - pix0);
+  const int npix = (int)min((int64_t)PB, g.P - pix0);
+  const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
+  const float gal = sc.gamma / sc.alpha;
   float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
-  const float gal = p.gamma / p.alpha;
 
-  if (npix > 0) {
-    // ---- B1: slots + background entry: prob, z_inv, rast score, dL/dW
-    for (int i = tid; i < npix * KP1; i += kThreads) {
-      const int pl = i / KP1, k = i - pl * KP1;
-      const int64_t gp = pix0 + pl;
-      CN[pl * KP1 + k] = 0;
-      if (k < K) {
-        const int64_t gs = gp * K + k;
-        const bool m = slot_mask(a.pix_to_face, a.mask, gs);
-        const float mf = m ? 1.f : 0.f;
-        float prob, gm = 0.f;
-        if constexpr (RAST) {
-          if (m) {
-            float gacc;
-            const int cnt = rast_count_score<NOISE>(p, a.dists[gs], (uint32_t)gp, k, gs, geo.PK, gacc);
-            prob = ((float)cnt / (float)p.Sr) * mf;
-            gm = gacc / (float)p.Sr;
-          } else {
-            prob = 0.f;
-          }
-        } else {
-          prob = a.prob[gs];
-        }
-        const int n = (int)(gp / ((int64_t)p.H * p.W));
-        const float zf = p.zfar[n], zn = p.znear[n];
-        PR[pl * KP1 + k] = prob;
-        ZZ[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
-        GM[pl * KP1 + k] = gm;
-        float dw;
-        if constexpr (COLOR) {
-          const float* g = a.grad_image + gp * 4;
-          const float* c = a.colors + gs * 3;
-          dw = (g[0] * c[0] + g[1] * c[1]) + g[2] * c[2];
-        } else {
-          dw = a.grad_weights[gp * KP1 + k];
-        }
-        DW[pl * KP1 + k] = dw;
-      } else {
-        float dw;
-        if constexpr (COLOR) {
-          const float* g = a.grad_image + gp * 4;
-          dw = (g[0] * p.background[0] + g[1] * p.background[1]) + g[2] * p.background[2];
-        } else {
-          dw = a.grad_weights[gp * KP1 + K];
-        }
-        DW[pl * KP1 + K] = dw;
-      }
-    }
-    __syncthreads();
-
-    // ---- B2: per pixel: z_max (first argmax), exclusive products for the alpha grad
-    if (tid < npix) {
-      float zm = kNegInf;
-      int km = 0;
-      for (int k = 0; k < K; ++k) {
-        const float zi = ZZ[tid * KP1 + k];
-        if (zi > zm) { zm = zi; km = k; }
-      }
-      PX[tid * 8 + 0] = zm;                       // raw max
-      PX[tid * 8 + 1] = zm < p.eps ? p.eps : zm;  // clamped
-      PX[tid * 8 + 2] = (float)km;
-      if constexpr (COLOR) {
-        // torch prod backward with zeros: exclusive cumprod forward * reversed (ATen)
-        float suf = 1.f;
-        for (int k = K - 1; k >= 0; --k) {
-          EX[tid * KP1 + k] = suf;
-          suf *= (1.f - PR[tid * KP1 + k]);
-        }
-        float pre = 1.f;
-        for (int k = 0; k < K; ++k) {
-          EX[tid * KP1 + k] = pre * EX[tid * KP1 + k];
-          pre *= (1.f - PR[tid * KP1 + k]);
-        }
-      }
-    }
-    __syncthreads();
-
-    // ---- B3: logits
-    for (int i = tid; i < npix * KP1; i += kThreads) {
-      const int pl = i / KP1, k = i - pl * KP1;
-      const float zmax = PX[pl * 8 + 1];
-      ZZ[pl * KP1 + k] = k < K ? gal * logf(PR[pl * KP1 + k]) + ZZ[pl * KP1 + k] - zmax : p.eps - zmax;
-    }
-    __syncthreads();
-
-    // ---- B4: unperturbed argmax j0 over K+1 logits (first index)
-    if (tid < npix) {
-      float zb = kNegInf;
-      int j0 = 0;
-      bool any = false;
-      for (int j = 0; j < KP1; ++j) {
-        const float z = ZZ[tid * KP1 + j];
-        if (!any || z > zb) { zb = z; j0 = j; any = true; }
-      }
-      PX[tid * 8 + 3] = (float)j0;
-    }
-    __syncthreads();
-
-    // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0], win counts
-    for (int i = tid; i < npix * Sa; i += kThreads) {
-      const int pl = i / Sa, s = i - pl * Sa;
-      const int64_t gp = pix0 + pl;
-      const int jw = a.winners[gp * Sa + s];
-      const int j0 = (int)PX[pl * 8 + 3];
-      const float as = DW[pl * KP1 + jw] - DW[pl * KP1 + j0];
-      AS[pl * Sa + s] = as;
-      part_a += as;
-      atomicAdd(&CN[pl * KP1 + jw], 1);
-    }
-    __syncthreads();
-
-    // ---- B6: dz_j = mean_s(a_s * eps_sj / gamma), and sum_s a_s * eps_sj^2 (for d gamma)
-    {
-      const int ng = agg_num_groups(p), g0 = agg_first_group(p);
-      for (int i = tid; i < npix * KP1; i += kThreads) {
-        const int pl = i / KP1, j = i - pl * KP1;
-        const int64_t gp = pix0 + pl;
-        float dz = 0.f, q = 0.f;
-        for (int gi = 0; gi < ng; ++gi) {
-          const uint32_t g = (uint32_t)(g0 + gi);
-          int sbase;
-          if constexpr (NOISE == PR_NOISE_INJECTED) sbase = 4 * gi;
-          else sbase = (int)(4 * g) - p.sample_offset_a;
-          float av[4];
-          bool any = false;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int s = sbase + r;
-            av[r] = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
-            any |= av[r] != 0.f;
-          }
-          if (!any) continue;
-          float e[4];
-          if constexpr (NOISE == PR_NOISE_INJECTED) {
-            agg_noise4<NOISE>(p, (uint32_t)gp, j, (uint32_t)gi, geo.P, KP1, e);
-          } else {
-            agg_noise4<NOISE>(p, (uint32_t)gp, j, g, geo.P, KP1, e);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (av[r] != 0.f) {
-              dz += (av[r] * e[r]) / p.gamma;
-              q += av[r] * (e[r] * e[r]);
-            }
-          }
-        }
-        DZ[pl * KP1 + j] = dz / (float)Sa;
-        part_q += q;
-      }
-    }
-    __syncthreads();
-
-    // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps
-    if (tid < npix) {
-      float s = 0.f;
-      for (int k = 0; k < K; ++k) s += DZ[tid * KP1 + k];
-      float dzm = -s - DZ[tid * KP1 + K];
-      dzm = dzm * (PX[tid * 8 + 0] >= p.eps ? 1.f : 0.f);
-      PX[tid * 8 + 4] = dzm;
-    }
-    __syncthreads();
-
-    // ---- B8: per-slot gradients
-    for (int i = tid; i < npix * K; i += kThreads) {
-      const int pl = i / K, k = i - pl * K;
-      const int64_t gp = pix0 + pl, gs = gp * K + k;
+  // ---- B1: slots + background entry: prob, z_inv, rast score, dL/dW
+  PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
+    const int64_t gp = pix0 + pl;
+    CN[pl * KP1 + k] = 0;
+    if (k < K) {
+      const int64_t gs = gp * K + k;
       const bool m = slot_mask(a.pix_to_face, a.mask, gs);
       const float mf = m ? 1.f : 0.f;
-      const float dzk = DZ[pl * KP1 + k];
-      const float dzinv = dzk + (k == (int)PX[pl * 8 + 2] ? PX[pl * 8 + 4] : 0.f);
-      const int n = (int)(gp / ((int64_t)p.H * p.W));
-      a.grad_zbuf[gs] = -((dzinv * mf) / (p.zfar[n] - p.znear[n]));
-      const float prob = PR[pl * KP1 + k];
-      const float L = logf(prob);
-      float dL = gal * dzk;
-      if (dL != dL) dL = 0.f;
-      const float lp = __builtin_isinf(L) ? 0.f : L * dzk;
-      if (lp == lp) part_gal += lp;
-      float r = 1.f / prob;
-      if (__builtin_isinf(r)) r = 0.f;
-      float dprob = r * dL;
-      if constexpr (COLOR) {
-        const float ga = a.grad_image[gp * 4 + 3];
-        dprob = -((-ga) * EX[pl * KP1 + k]) + dprob;
-      }
+      float prob, gm = 0.f;
       if constexpr (RAST) {
-        const float dP = dprob * mf;
-        const float dD = GM[pl * KP1 + k] * dP;
-        a.grad_dists[gs] = -dD;
-        part_sigma += dD;
+        if (m) {
+          float gacc;
+          const int cnt = rast_count_score<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK, gacc);
+          prob = ((float)cnt / (float)p.Sr) * mf;
+          gm = gacc / (float)p.Sr;
+        } else {
+          prob = 0.f;
+        }
       } else {
-        a.grad_prob[gs] = dprob;
+        prob = a.prob[gs];
       }
+      const int n = image_of(n0, rem0, pl, g.HW);
+      const float zf = p.zfar[n], zn = p.znear[n];
+      PR[pl * KP1 + k] = prob;
+      ZZ[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
+      GM[pl * KP1 + k] = gm;
+      float dw;
       if constexpr (COLOR) {
-        const float w = (float)CN[pl * KP1 + k] / (float)Sa;
-        const float* g = a.grad_image + gp * 4;
-        float* dc = a.grad_colors + gs * 3;
-        dc[0] = w * g[0];
-        dc[1] = w * g[1];
-        dc[2] = w * g[2];
+        const float* gi = a.grad_image + gp * 4;
+        const float* c = a.colors + gs * 3;
+        dw = (gi[0] * c[0] + gi[1] * c[1]) + gi[2] * c[2];
+      } else {
+        dw = a.grad_weights[gp * KP1 + k];
       }
+      DW[pl * KP1 + k] = dw;
+    } else {
+      float dw;
+      if constexpr (COLOR) {
+        const float* gi = a.grad_image + gp * 4;
+        dw = (gi[0] * p.background[0] + gi[1] * p.background[1]) + gi[2] * p.background[2];
+      } else {
+        dw = a.grad_weights[gp * KP1 + K];
+      }
+      DW[pl * KP1 + K] = dw;
+    }
+  }
+  __syncthreads();
+
+  // ---- B2: per pixel (8 lanes, contiguous chunks): z_max + first argmax, exclusive
+  //          products for the alpha gradient, logits, unperturbed argmax j0
+  {
+    const int pl = tid >> 3, l = tid & 7;
+    const bool act = pl < npix;
+    const int j0c = l * g.ck, j1c = min(KP1, j0c + g.ck), k1c = min(K, j1c);
+    float zm = kNegInf, tp = 1.f;
+    int km = 1 << 30;
+    if (act)
+      for (int k = j0c; k < k1c; ++k) {
+        const float zi = ZZ[pl * KP1 + k];
+        if (zi > zm) { zm = zi; km = k; }
+        tp *= (1.f - PR[pl * KP1 + k]);
+      }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      const float oz = __shfl_xor(zm, m);
+      const int ok = __shfl_xor(km, m);
+      if (oz > zm || (oz == zm && ok < km)) { zm = oz; km = ok; }
+    }
+    if (km == (1 << 30)) km = 0;
+    const float zmax = zm < p.eps ? p.eps : zm;
+    if constexpr (COLOR) {
+      // exclusive products across the 8 lane chunks, then within the chunk
+      float pre = 1.f, suf = 1.f;
+      const int lane8 = (tid & 63) & ~7;
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        const float t = __shfl(tp, lane8 + o);
+        if (o < l) pre *= t;
+        if (o > l) suf *= t;
+      }
+      if (act) {
+        for (int k = k1c - 1; k >= j0c; --k) {
+          EX[pl * KP1 + k] = suf;
+          suf *= (1.f - PR[pl * KP1 + k]);
+        }
+        for (int k = j0c; k < k1c; ++k) {
+          EX[pl * KP1 + k] = pre * EX[pl * KP1 + k];
+          pre *= (1.f - PR[pl * KP1 + k]);
+        }
+      }
+    }
+    float zb = kNegInf;
+    int jb = 1 << 30;
+    if (act)
+      for (int j = j0c; j < j1c; ++j) {
+        const float z = j < K ? gal * logf(PR[pl * KP1 + j]) + ZZ[pl * KP1 + j] - zmax : p.eps - zmax;
+        if (z > zb || jb == (1 << 30)) { zb = z; jb = j; }
+      }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      const float oz = __shfl_xor(zb, m);
+      const int oj = __shfl_xor(jb, m);
+      if (oj != (1 << 30) && (jb == (1 << 30) || oz > zb || (oz == zb && oj < jb))) { zb = oz; jb = oj; }
+    }
+    if (act && l == 0) {
+      PX[pl * 8 + 0] = zm;          // raw max z_inv (clamp test)
+      PX[pl * 8 + 2] = (float)km;   // its first index
+      PX[pl * 8 + 3] = (float)jb;   // unperturbed argmax of the K+1 logits
+    }
+  }
+  __syncthreads();
+
+  // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0], win counts
+  PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
+    const int s = k;
+    const int64_t gp = pix0 + pl;
+    const int jw = a.winners[gp * Sa + s];
+    const int j0 = (int)PX[pl * 8 + 3];
+    const float as = DW[pl * KP1 + jw] - DW[pl * KP1 + j0];
+    AS[pl * Sa + s] = as;
+    part_a += as;
+    atomicAdd(&CN[pl * KP1 + jw], 1);
+  }
+  __syncthreads();
+
+  // ---- B6: dz_j = mean_s(a_s * eps_sj / gamma) and sum_s a_s * eps_sj^2 (d gamma)
+  {
+    const int ng = agg_num_groups(p), g0 = agg_first_group(p);
+    PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
+      const int j = k;
+      const int64_t gp = pix0 + pl;
+      float dz = 0.f, q = 0.f;
+      for (int gi = 0; gi < ng; ++gi) {
+        const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
+        const int sbase = (int)(4 * gg) - (NOISE == PR_NOISE_INJECTED ? 0 : p.sample_offset_a);
+        float av[4];
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int s = sbase + r;
+          av[r] = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
+          any |= av[r] != 0.f;
+        }
+        if (!any) continue;
+        float e[4];
+        agg_noise4<NOISE>(p, sc, (uint32_t)gp, j, gg, g.P, KP1, e);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (av[r] != 0.f) {
+            dz += (av[r] * e[r]) / sc.gamma;
+            q += av[r] * (e[r] * e[r]);
+          }
+        }
+      }
+      ZZ[pl * KP1 + j] = dz / (float)Sa;  // ZZ now holds dL/dz
+      part_q += q;
+    }
+  }
+  __syncthreads();
+
+  // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps
+  {
+    const int pl = tid >> 3, l = tid & 7;
+    const bool act = pl < npix;
+    const int j0c = l * g.ck, k1c = min(K, j0c + g.ck);
+    float s = 0.f;
+    if (act)
+      for (int k = j0c; k < k1c; ++k) s += ZZ[pl * KP1 + k];
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) s += __shfl_xor(s, m);
+    if (act && l == 0) {
+      float dzm = -s - ZZ[pl * KP1 + K];
+      dzm = dzm * (PX[pl * 8 + 0] >= p.eps ? 1.f : 0.f);
+      PX[pl * 8 + 4] = dzm;
+    }
+  }
+  __syncthreads();
+
+  // ---- B8: per-slot gradients
+  PR_FOR_SLOTS(K, g.qK, g.rK, npix * K) {
+    const int64_t gp = pix0 + pl, gs = gp * K + k;
+    const bool m = slot_mask(a.pix_to_face, a.mask, gs);
+    const float mf = m ? 1.f : 0.f;
+    const float dzk = ZZ[pl * KP1 + k];
+    const float dzinv = dzk + (k == (int)PX[pl * 8 + 2] ? PX[pl * 8 + 4] : 0.f);
+    const int n = image_of(n0, rem0, pl, g.HW);
+    a.grad_zbuf[gs] = -((dzinv * mf) / (p.zfar[n] - p.znear[n]));
+    const float prob = PR[pl * KP1 + k];
+    const float L = logf(prob);
+    float dL = gal * dzk;
+    if (dL != dL) dL = 0.f;
+    const float lp = __builtin_isinf(L) ? 0.f : L * dzk;
+    if (lp == lp) part_gal += lp;
+    float r = 1.f / prob;
+    if (__builtin_isinf(r)) r = 0.f;
+    float dprob = r * dL;
+    if constexpr (COLOR) {
+      const float ga = a.grad_image[gp * 4 + 3];
+      dprob = -((-ga) * EX[pl * KP1 + k]) + dprob;
+    }
+    if constexpr (RAST) {
+      const float dD = GM[pl * KP1 + k] * (dprob * mf);
+      a.grad_dists[gs] = -dD;
+      part_sigma += dD;
+    } else {
+      a.grad_prob[gs] = dprob;
+    }
+    if constexpr (COLOR) {
+      const float w = (float)CN[pl * KP1 + k] / (float)Sa;
+      const float* gi = a.grad_image + gp * 4;
+      float* dc = a.grad_colors + gs * 3;
+      dc[0] = w * gi[0];
+      dc[1] = w * gi[1];
+      dc[2] = w * gi[2];
     }
   }
 
   // ---- block reduction of the scalar partials (fixed order -> deterministic)
-  RED[tid * 4 + 0] = part_sigma;
-  RED[tid * 4 + 1] = part_q;
-  RED[tid * 4 + 2] = part_a;
-  RED[tid * 4 + 3] = part_gal;
-  __syncthreads();
-  for (int s = kThreads / 2; s > 0; s >>= 1) {
-    if (tid < s) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) RED[tid * 4 + c] += RED[(tid + s) * 4 + c];
-    }
-    __syncthreads();
+  for (int m = 32; m >= 1; m >>= 1) {
+    part_sigma += __shfl_xor(part_sigma, m);
+    part_q += __shfl_xor(part_q, m);
+    part_a += __shfl_xor(part_a, m);
+    part_gal += __shfl_xor(part_gal, m);
   }
-  if (tid < 4) partials[(int64_t)blockIdx.x * 4 + tid] = RED[tid];
+  __syncthreads();
+  float* RED = smem;  // all per-slot arrays are dead now
+  if ((tid & 63) == 0) {
+    RED[(tid >> 6) * 4 + 0] = part_sigma;
+    RED[(tid >> 6) * 4 + 1] = part_q;
+    RED[(tid >> 6) * 4 + 2] = part_a;
+    RED[(tid >> 6) * 4 + 3] = part_gal;
+  }
+  __syncthreads();
+  if (tid < 4) {
+    partials[(int64_t)blockIdx.x * 4 + tid] = (RED[tid] + RED[4 + tid]) + (RED[8 + tid] + RED[12 + tid]);
+  }
 }
 
 // d sigma, d gamma, d alpha from the per-block partials (one workgroup, fixed order)
@@ -530,6 +592,7 @@ __global__ void __launch_bounds__(kThreads) blend_finalize_kernel(const float* p
                                                                   float* out) {
   __shared__ float red[kThreads * 4];
   const int tid = threadIdx.x;
+  const Sc sc = resolve(p);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int b = tid; b < nblk; b += kThreads) {
 #pragma unroll
@@ -548,25 +611,33 @@ __global__ void __launch_bounds__(kThreads) blend_finalize_kernel(const float* p
   if (tid == 0) {
     const float dsig = red[0], Q = red[1], As = red[2], dgal = red[3];
     // smoothagg.py:54-56,72 : mean_s sum a_s (|eps_s|^2 - 1) / gamma
-    const float dg1 = ((Q - As) / p.gamma) / (float)p.Sa;
+    const float dg1 = ((Q - As) / sc.gamma) / (float)p.Sa;
     out[0] = has_rast ? dsig : 0.f;
-    out[1] = dg1 + dgal / p.alpha;                      // prod_corrected x = gamma/alpha
-    out[2] = -dgal * ((p.gamma / p.alpha) / p.alpha);
+    out[1] = dg1 + dgal / sc.alpha;                       // prod_corrected x = gamma/alpha
+    out[2] = -dgal * ((sc.gamma / sc.alpha) / sc.alpha);
   }
 }
 
 // ====================================================== standalone heaviside
-template <int NOISE>
-__global__ void __launch_bounds__(kThreads) heaviside_fwd_kernel(PRHeavisideArgs a) {
-  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+PR_DEV PRBlendParams heaviside_params(const PRHeavisideArgs& a) {
   PRBlendParams p{};
   p.Sr = a.Sr; p.sample_offset_r = a.sample_offset_r; p.sigma = a.sigma;
   p.seed_r = a.seed_r; p.noise_r = a.noise_r;
+  p.seeds = a.seeds;
+  if (a.sigma_dev) p.sigma = a.sigma_dev[0];
+  return p;
+}
+
+template <int NOISE>
+__global__ void __launch_bounds__(kThreads) heaviside_fwd_kernel(PRHeavisideArgs a) {
+  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+  const PRBlendParams p = heaviside_params(a);
+  const Sc sc = resolve(p);
   for (int64_t gs = (int64_t)blockIdx.x * kThreads + threadIdx.x; gs < PK;
        gs += (int64_t)gridDim.x * kThreads) {
     const int64_t gp = gs / a.K;
     const int k = (int)(gs - gp * a.K);
-    const int cnt = rast_count<NOISE>(p, a.dists[gs], (uint32_t)gp, k, gs, PK);
+    const int cnt = rast_count<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, PK);
     a.prob[gs] = (float)cnt / (float)a.Sr;
   }
 }
@@ -575,16 +646,15 @@ template <int NOISE>
 __global__ void __launch_bounds__(kThreads) heaviside_bwd_kernel(PRHeavisideArgs a, float* partials) {
   __shared__ float red[kThreads];
   const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
-  PRBlendParams p{};
-  p.Sr = a.Sr; p.sample_offset_r = a.sample_offset_r; p.sigma = a.sigma;
-  p.seed_r = a.seed_r; p.noise_r = a.noise_r;
+  const PRBlendParams p = heaviside_params(a);
+  const Sc sc = resolve(p);
   float part = 0.f;
   for (int64_t gs = (int64_t)blockIdx.x * kThreads + threadIdx.x; gs < PK;
        gs += (int64_t)gridDim.x * kThreads) {
     const int64_t gp = gs / a.K;
     const int k = (int)(gs - gp * a.K);
     float gacc;
-    rast_count_score<NOISE>(p, a.dists[gs], (uint32_t)gp, k, gs, PK, gacc);
+    rast_count_score<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, PK, gacc);
     const float dD = (gacc / (float)a.Sr) * a.grad_prob[gs];
     a.grad_dists[gs] = -dD;
     part += dD;
@@ -611,12 +681,18 @@ __global__ void __launch_bounds__(kThreads) sum_partials_kernel(const float* par
   if (threadIdx.x == 0) out[0] = red[0];
 }
 
-// ================================================================== host side
-size_t fwd_lds(int PB, int KP1) { return (size_t)(2 * PB * KP1 + 2 * PB) * sizeof(float); }
-size_t bwd_lds(int PB, int KP1, int Sa) {
-  return (size_t)(7 * PB * KP1 + PB * Sa + 8 * PB + kThreads * 4) * sizeof(float);
+__global__ void seed_advance_kernel(uint64_t* seeds, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) seeds[i] = mix64(seeds[i] + 0x9E3779B97F4A7C15ull);
 }
-constexpr size_t kLdsBudget = 64 * 1024;  // keep >= 2 workgroups (8 waves) per CU
+
+// ================================================================== host side
+size_t fwd_lds(int PB, int KP1) { return (size_t)(2 * PB * KP1 + 4 * PB) * sizeof(float); }
+size_t bwd_lds(int PB, int KP1, int Sa) {
+  const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + 8 * PB) * sizeof(float);
+  return b < 16 * sizeof(float) ? 16 * sizeof(float) : b;
+}
+constexpr size_t kLdsBudget = 48 * 1024;  // >= 3 workgroups (12 waves) per CU
 
 int pick_pb(int KP1, int Sa, bool bwd) {
   for (int PB = 32; PB >= 1; PB >>= 1) {
@@ -630,6 +706,7 @@ int check_params(const PRBlendParams& p, bool need_rast) {
   if (p.N <= 0 || p.H <= 0 || p.W <= 0 || p.K <= 0) return set_error(PR_ERR_ARG, "blend: empty shape");
   if (p.K > 255) return set_error(PR_ERR_ARG, "blend: faces_per_pixel must be <= 255");
   if (p.Sa <= 0 || (need_rast && p.Sr <= 0)) return set_error(PR_ERR_ARG, "blend: nb_samples must be > 0");
+  if (p.Sa > 4096 || p.Sr > (1 << 24)) return set_error(PR_ERR_ARG, "blend: nb_samples too large");
   if (p.noise_mode != PR_NOISE_PHILOX && p.noise_mode != PR_NOISE_INJECTED)
     return set_error(PR_ERR_ARG, "blend: unknown noise mode");
   if (p.noise_mode == PR_NOISE_INJECTED && (!p.noise_a || (need_rast && !p.noise_r)))
@@ -639,7 +716,8 @@ int check_params(const PRBlendParams& p, bool need_rast) {
     return set_error(PR_ERR_ARG, "blend: injected noise is indexed locally; sample offsets must be 0");
   if (!p.znear || !p.zfar) return set_error(PR_ERR_ARG, "blend: znear/zfar missing");
   const int64_t P = (int64_t)p.N * p.H * p.W;
-  if (P >= (int64_t(1) << 32)) return set_error(PR_ERR_ARG, "blend: too many pixels");
+  if (P >= (int64_t(1) << 31) || (int64_t)p.H * p.W >= (int64_t(1) << 31))
+    return set_error(PR_ERR_ARG, "blend: too many pixels");
   return PR_OK;
 }
 
@@ -668,6 +746,11 @@ Geo make_geo(const PRBlendParams& p, int PB) {
   g.K = p.K;
   g.KP1 = p.K + 1;
   g.PB = PB;
+  g.HW = p.H * p.W;
+  g.qK = kThreads / g.K; g.rK = kThreads % g.K;
+  g.qK1 = kThreads / g.KP1; g.rK1 = kThreads % g.KP1;
+  g.qS = kThreads / p.Sa; g.rS = kThreads % p.Sa;
+  g.ck = (g.KP1 + 7) / 8;
   return g;
 }
 
@@ -739,8 +822,12 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
 
 static int heaviside_check(const PRHeavisideArgs& a) {
   if (a.N <= 0 || a.H <= 0 || a.W <= 0 || a.K <= 0 || a.Sr <= 0) return set_error(PR_ERR_ARG, "heaviside: bad shape");
-  if (a.noise_mode == PR_NOISE_INJECTED && !a.noise_r) return set_error(PR_ERR_ARG, "heaviside: noise missing");
+  if (a.noise_mode != PR_NOISE_PHILOX && a.noise_mode != PR_NOISE_INJECTED)
+    return set_error(PR_ERR_ARG, "heaviside: unknown noise mode");
+  if (a.noise_mode == PR_NOISE_INJECTED && (!a.noise_r || a.sample_offset_r != 0))
+    return set_error(PR_ERR_ARG, "heaviside: injected noise missing or offset != 0");
   if (!a.dists) return set_error(PR_ERR_ARG, "heaviside: dists missing");
+  if ((int64_t)a.N * a.H * a.W >= (int64_t(1) << 32)) return set_error(PR_ERR_ARG, "heaviside: too many pixels");
   return PR_OK;
 }
 
@@ -784,4 +871,10 @@ extern "C" int pr_heaviside_bwd(const PRHeavisideArgs* args, void* stream) {
   if (int e = check_launch("heaviside_bwd")) return e;
   sum_partials_kernel<<<1, kThreads, 0, st>>>(part, nb, a.grad_sigma);
   return check_launch("heaviside_sum");
+}
+
+extern "C" int pr_seed_advance(uint64_t* seeds, int32_t n, void* stream) {
+  if (!seeds || n <= 0) return set_error(PR_ERR_ARG, "seed_advance: bad args");
+  seed_advance_kernel<<<(n + 63) / 64, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(seeds, n);
+  return check_launch("seed_advance");
 }

@@ -127,90 +127,155 @@ PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, bool persp, bool clip,
   return d < blur;
 }
 
-__global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* faces) {
+constexpr int kCap = 256;  // per-round tile face list (faces beyond it are handled in later rounds)
+
+PR_DEV float zmin3(const FaceRec& r) { return fminf(r.a.z, fminf(r.b.y, r.c.x)); }
+
+// Bitonic sort (ascending key) of n2 (power of two) LDS entries by one wave.
+PR_DEV void bitonic_sort(float* key, int* val, int n2, int lane) {
+  for (int k = 2; k <= n2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = lane; i < n2; i += 64) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const float a = key[i], b = key[ixj];
+          if ((a > b) == up) {
+            key[i] = b; key[ixj] = a;
+            const int t = val[i]; val[i] = val[ixj]; val[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces) {
   extern __shared__ float smem[];
   const int K = a.K;
-  float* qz = smem;                                   // [K][64]
-  int* qf = reinterpret_cast<int*>(qz + K * 64);      // [K][64]
-  FaceRec* fl = reinterpret_cast<FaceRec*>(qf + K * 64);  // [64]
+  float2* q = reinterpret_cast<float2*>(smem);             // [K][64] (z, face id bits), sorted per lane
+  int* lfid = reinterpret_cast<int*>(q + K * 64);           // [kCap] tile face list
+  float* lkey = reinterpret_cast<float*>(lfid + kCap);      // [kCap] its z_min (sort key)
+  int* qsz = reinterpret_cast<int*>(lkey + kCap);           // [64] queue sizes
   const int lane = threadIdx.x;
   const int n = blockIdx.z;
-  const int row = blockIdx.y * kTile + lane / kTile;
-  const int col = blockIdx.x * kTile + lane % kTile;
   const int H = a.H, W = a.W;
+  const int row0 = blockIdx.y * kTile, col0 = blockIdx.x * kTile;
+  const int row = row0 + lane / kTile, col = col0 + lane % kTile;
   const bool inimg = row < H && col < W;
   const V2 p{ndc(W - 1 - min(col, W - 1), W, H), ndc(H - 1 - min(row, H - 1), H, W)};
   // tile rectangle in NDC (pixel centres); +X points left, +Y up
-  const int c0 = blockIdx.x * kTile, c1 = min(c0 + kTile - 1, W - 1);
-  const int r0 = blockIdx.y * kTile, r1 = min(r0 + kTile - 1, H - 1);
-  const float txmax = ndc(W - 1 - c0, W, H), txmin = ndc(W - 1 - c1, W, H);
-  const float tymax = ndc(H - 1 - r0, H, W), tymin = ndc(H - 1 - r1, H, W);
+  const int c1 = min(col0 + kTile - 1, W - 1), r1 = min(row0 + kTile - 1, H - 1);
+  const float txmax = ndc(W - 1 - col0, W, H), txmin = ndc(W - 1 - c1, W, H);
+  const float tymax = ndc(H - 1 - row0, H, W), tymin = ndc(H - 1 - r1, H, W);
   const int64_t fb = a.mesh_first_face[n], fe = fb + a.mesh_num_faces[n];
   const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
   int qs = 0;
-  for (int64_t base = fb; base < fe; base += 64) {
-    const int64_t f = base + lane;
-    FaceRec r;
-    bool keep = false;
-    if (f < fe) {
-      r = faces[f];
-      keep = r.d.y != 0.f && !(r.c.y > txmax || r.c.z < txmin || r.c.w > tymax || r.d.x < tymin);
+  float qlast_z = __builtin_inff();
+  int qlast_f = 0x7fffffff;
+  bool done = !inimg;
+  int64_t base = fb;
+  while (base < fe) {
+    // ---- gather this round's culled faces (expanded bbox overlaps the tile)
+    int nl = 0;
+    while (base < fe && nl <= kCap - 64) {
+      const int64_t f = base + lane;
+      bool keep = false;
+      float zk = 0.f;
+      if (f < fe) {
+        const FaceRec r = faces[f];
+        keep = r.d.y != 0.f && !(r.c.y > txmax || r.c.z < txmin || r.c.w > tymax || r.d.x < tymin);
+        zk = zmin3(r);
+      }
+      const uint64_t bal = __ballot(keep);
+      if (keep) {
+        const int idx = nl + __popcll(bal & ((1ull << lane) - 1ull));
+        lfid[idx] = (int)f;
+        lkey[idx] = zk;
+      }
+      nl += __popcll(bal);
+      base += 64;
     }
-    const uint64_t bal = __ballot(keep);
-    const int cnt = __popcll(bal);
-    if (keep) {
-      const int idx = __popcll(bal & ((1ull << lane) - 1ull));
-      r.d.z = __int_as_float((int)(f - 0));  // keep the global face id (fits: F < 2^31)
-      fl[idx] = r;
-    }
+    if (nl == 0) continue;
+    done = !inimg;  // the early exit below is only valid inside one z-sorted round
+    // ---- sort by z_min: near faces first, so inserts are mostly appends and lanes
+    //      whose K-queue is full can stop early (pz >= z_min when barycentrics are clipped)
+    int n2 = 1;
+    while (n2 < nl) n2 <<= 1;
+    for (int i = nl + lane; i < n2; i += 64) { lkey[i] = __builtin_inff(); lfid[i] = 0x7fffffff; }
     __syncthreads();
-    if (inimg) {
-      for (int i = 0; i < cnt; ++i) {
-        const FaceRec rr = fl[i];
-        float pz;
-        if (!face_test(rr, p, a.blur_radius, persp, clip, pz)) continue;
-        const int fid = __float_as_int(rr.d.z);
-        if (qs == K && !key_less(pz, fid, qz[(K - 1) * 64 + lane], qf[(K - 1) * 64 + lane])) continue;
-        int pos = qs < K ? qs : K - 1;
-        if (qs < K) ++qs;
-        while (pos > 0 && key_less(pz, fid, qz[(pos - 1) * 64 + lane], qf[(pos - 1) * 64 + lane])) {
-          qz[pos * 64 + lane] = qz[(pos - 1) * 64 + lane];
-          qf[pos * 64 + lane] = qf[(pos - 1) * 64 + lane];
-          --pos;
-        }
-        qz[pos * 64 + lane] = pz;
-        qf[pos * 64 + lane] = fid;
+    bitonic_sort(lkey, lfid, n2, lane);
+    for (int i = 0; i < nl; ++i) {
+      const float zk = lkey[i];
+      // clipped barycentrics make pz a convex combination of the vertex depths, so
+      // pz >= z_min (up to rounding: keep a 1e-6 relative margin)
+      if (clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
+      if (__ballot(!done) == 0) break;
+      if (done) continue;
+      const int fid = __builtin_amdgcn_readfirstlane(lfid[i]);
+      const FaceRec rr = faces[fid];
+      float pz;
+      if (!face_test(rr, p, a.blur_radius, persp, clip, pz)) continue;
+      if (qs == K && !key_less(pz, fid, qlast_z, qlast_f)) continue;
+      int pos = qs < K ? qs : K - 1;
+      if (qs < K) ++qs;
+      while (pos > 0) {
+        const float2 prev = q[(pos - 1) * 64 + lane];
+        if (!key_less(pz, fid, prev.x, __float_as_int(prev.y))) break;
+        q[pos * 64 + lane] = prev;
+        --pos;
+      }
+      q[pos * 64 + lane] = make_float2(pz, __int_as_float(fid));
+      if (qs == K) {
+        const float2 last = q[(K - 1) * 64 + lane];
+        qlast_z = last.x;
+        qlast_f = __float_as_int(last.y);
       }
     }
     __syncthreads();
   }
-  if (!inimg) return;
-  const int64_t pix = ((int64_t)n * H + row) * W + col;
-  for (int k = 0; k < K; ++k) {
-    const int64_t o = pix * K + k;
-    if (k < qs) {
-      const int fid = qf[k * 64 + lane];
-      const float* v = a.face_verts + (int64_t)fid * 9;
-      const V2 v0{v[0], v[1]}, v1{v[3], v[4]}, v2{v[6], v[7]};
-      float b0[3], b[3], bc[3];
-      bary_fwd(p, v0, v1, v2, b0);
-      if (persp) persp_fwd(b0, v[2], v[5], v[8], b); else { b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; }
-      if (clip) clip_fwd(b, bc); else { bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2]; }
-      const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
-      const float d = tri_dist2(p, v0, v1, v2);
-      a.pix_to_face[o] = fid;
-      a.zbuf[o] = qz[k * 64 + lane];
-      a.dists[o] = inside ? -d : d;
-      a.bary[o * 3 + 0] = bc[0];
-      a.bary[o * 3 + 1] = bc[1];
-      a.bary[o * 3 + 2] = bc[2];
-    } else {
-      a.pix_to_face[o] = -1;
-      a.zbuf[o] = -1.f;
-      a.dists[o] = -1.f;
-      a.bary[o * 3 + 0] = -1.f;
-      a.bary[o * 3 + 1] = -1.f;
-      a.bary[o * 3 + 2] = -1.f;
+  qsz[lane] = inimg ? qs : 0;
+  __syncthreads();
+  // ---- coalesced output: each tile row's 8 pixels own a contiguous 8*K slot range
+  const int q64 = 64 / K, r64 = 64 % K;
+  for (int r = 0; r < kTile; ++r) {
+    const int prow = row0 + r;
+    if (prow >= H) break;
+    const int ncols = min(kTile, W - col0);
+    const int total = ncols * K;
+    const int64_t obase = (((int64_t)n * H + prow) * W + col0) * K;
+    const float py = ndc(H - 1 - prow, H, W);
+    for (int i = lane, c = lane / K, k = lane - (lane / K) * K; i < total;
+         i += 64, c += q64, k += r64, (k >= K ? (k -= K, ++c) : 0)) {
+      const int tl = r * kTile + c;
+      const int64_t o = obase + i;
+      if (k < qsz[tl]) {
+        const float2 e = q[k * 64 + tl];
+        const int fid = __float_as_int(e.y);
+        const V2 pp{ndc(W - 1 - (col0 + c), W, H), py};
+        const float* v = a.face_verts + (int64_t)fid * 9;
+        const V2 v0{v[0], v[1]}, v1{v[3], v[4]}, v2{v[6], v[7]};
+        float b0[3], b[3], bc[3];
+        bary_fwd(pp, v0, v1, v2, b0);
+        if (persp) persp_fwd(b0, v[2], v[5], v[8], b); else { b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; }
+        if (clip) clip_fwd(b, bc); else { bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2]; }
+        const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
+        const float d = tri_dist2(pp, v0, v1, v2);
+        a.pix_to_face[o] = fid;
+        a.zbuf[o] = e.x;
+        a.dists[o] = inside ? -d : d;
+        a.bary[o * 3 + 0] = bc[0];
+        a.bary[o * 3 + 1] = bc[1];
+        a.bary[o * 3 + 2] = bc[2];
+      } else {
+        a.pix_to_face[o] = -1;
+        a.zbuf[o] = -1.f;
+        a.dists[o] = -1.f;
+        a.bary[o * 3 + 0] = -1.f;
+        a.bary[o * 3 + 1] = -1.f;
+        a.bary[o * 3 + 2] = -1.f;
+      }
     }
   }
 }
@@ -380,19 +445,25 @@ __global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a) {
 }
 
 // ------------------------------------------------------------ interpolation
+// Row offset of corner i of face f in the attribute table: per-face-corner (F,3,D)
+// or, with a.faces, per-vertex (V,D) gathered through the face indices.
+PR_DEV int64_t attr_row(const PRInterpArgs& a, int64_t f, int i) {
+  return a.faces ? a.faces[f * 3 + i] * a.D : (f * 3 + i) * a.D;
+}
+
 __global__ void interp_fwd_kernel(PRInterpArgs a) {
-  const int64_t total = a.PK * a.D;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = i / a.D;
-    const int d = (int)(i - s * a.D);
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < a.PK; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t f = a.pix_to_face[s];
-    float v = 0.f;
-    if (f >= 0) {
-      const float* w = a.bary + s * 3;
-      const float* at = a.face_attr + f * 3 * a.D;
-      v = (w[0] * at[d] + w[1] * at[a.D + d]) + w[2] * at[2 * a.D + d];
+    float* o = a.out + s * a.D;
+    if (f < 0) {
+      for (int d = 0; d < a.D; ++d) o[d] = 0.f;
+      continue;
     }
-    a.out[i] = v;
+    const float w0 = a.bary[s * 3], w1 = a.bary[s * 3 + 1], w2 = a.bary[s * 3 + 2];
+    const float* r0 = a.face_attr + attr_row(a, f, 0);
+    const float* r1 = a.face_attr + attr_row(a, f, 1);
+    const float* r2 = a.face_attr + attr_row(a, f, 2);
+    for (int d = 0; d < a.D; ++d) o[d] = (w0 * r0[d] + w1 * r1[d]) + w2 * r2[d];
   }
 }
 
@@ -404,19 +475,77 @@ __global__ void interp_bwd_kernel(PRInterpArgs a) {
       if (a.grad_bary) { a.grad_bary[s * 3] = 0.f; a.grad_bary[s * 3 + 1] = 0.f; a.grad_bary[s * 3 + 2] = 0.f; }
       continue;
     }
-    const float* w = a.bary + s * 3;
-    const float* at = a.face_attr + f * 3 * a.D;
+    const float w[3] = {a.bary[s * 3], a.bary[s * 3 + 1], a.bary[s * 3 + 2]};
+    const int64_t rows[3] = {attr_row(a, f, 0), attr_row(a, f, 1), attr_row(a, f, 2)};
     float gb[3] = {0.f, 0.f, 0.f};
     for (int d = 0; d < a.D; ++d) {
       const float g = go[d];
-      gb[0] += g * at[d]; gb[1] += g * at[a.D + d]; gb[2] += g * at[2 * a.D + d];
-      if (a.grad_face_attr) {
-        atomicAdd(&a.grad_face_attr[f * 3 * a.D + d], w[0] * g);
-        atomicAdd(&a.grad_face_attr[f * 3 * a.D + a.D + d], w[1] * g);
-        atomicAdd(&a.grad_face_attr[f * 3 * a.D + 2 * a.D + d], w[2] * g);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        gb[i] += g * a.face_attr[rows[i] + d];
+        if (a.grad_face_attr && g != 0.f) atomicAdd(&a.grad_face_attr[rows[i] + d], w[i] * g);
       }
     }
     if (a.grad_bary) { a.grad_bary[s * 3] = gb[0]; a.grad_bary[s * 3 + 1] = gb[1]; a.grad_bary[s * 3 + 2] = gb[2]; }
+  }
+}
+
+// ---------------------------------------------------------------- projection
+PR_DEV int mesh_of(const int64_t* first, const int64_t* nf, int N, int64_t f) {
+  for (int n = 0; n < N; ++n)
+    if (f >= first[n] && f < first[n] + nf[n]) return n;
+  return 0;
+}
+
+// [x,y,z,1] @ M (row-vector, PyTorch3D Transform3d) followed by the w division
+PR_DEV void xform(const float* M, float x, float y, float z, float o[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) o[c] = ((x * M[c] + y * M[4 + c]) + z * M[8 + c]) + M[12 + c];
+}
+
+__global__ void project_fwd_kernel(PRProjectArgs a) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.F * 3; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t f = t / 3;
+    const int n = mesh_of(a.mesh_first_face, a.mesh_num_faces, a.N, f);
+    const float* v = a.verts + a.faces[t] * 3;
+    float o[4], c[4];
+    xform(a.world_to_view + n * 16, v[0], v[1], v[2], o);
+    const float vx = o[0] / o[3], vy = o[1] / o[3], vz = o[2] / o[3];
+    xform(a.proj + n * 16, vx, vy, vz, c);
+    a.face_verts[t * 3 + 0] = c[0] / c[3];
+    a.face_verts[t * 3 + 1] = c[1] / c[3];
+    a.face_verts[t * 3 + 2] = vz;
+  }
+}
+
+__global__ void project_bwd_kernel(PRProjectArgs a) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.F * 3; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t f = t / 3;
+    const int n = mesh_of(a.mesh_first_face, a.mesh_num_faces, a.N, f);
+    const int64_t vi = a.faces[t];
+    const float* v = a.verts + vi * 3;
+    const float* M = a.world_to_view + n * 16;
+    const float* P = a.proj + n * 16;
+    float o[4], c[4];
+    xform(M, v[0], v[1], v[2], o);
+    const float vv[3] = {o[0] / o[3], o[1] / o[3], o[2] / o[3]};
+    xform(P, vv[0], vv[1], vv[2], c);
+    const float gx = a.grad_face_verts[t * 3], gy = a.grad_face_verts[t * 3 + 1], gz = a.grad_face_verts[t * 3 + 2];
+    const float i3 = 1.f / c[3], i33 = i3 * i3;
+    float gvv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      gvv[k] = gx * (P[k * 4 + 0] * i3 - c[0] * P[k * 4 + 3] * i33) + gy * (P[k * 4 + 1] * i3 - c[1] * P[k * 4 + 3] * i33);
+    }
+    gvv[2] += gz;
+    const float j3 = 1.f / o[3], j33 = j3 * j3;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      float g = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g += gvv[k] * (M[m * 4 + k] * j3 - o[k] * M[m * 4 + 3] * j33);
+      atomicAdd(&a.grad_verts[vi * 3 + m], g);
+    }
   }
 }
 
@@ -456,7 +585,7 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
     if (int e = check_launch("rast_face_prep")) return e;
   }
   dim3 grid((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, a.N);
-  const size_t lds = (size_t)a.K * 64 * 8 + 64 * sizeof(FaceRec);
+  const size_t lds = (size_t)a.K * 64 * 8 + kCap * 8 + 64 * 4;
   rast_fwd_kernel<<<grid, 64, lds, st>>>(a, fr);
   return check_launch("rast_fwd");
 }
@@ -483,9 +612,8 @@ extern "C" int pr_interp_fwd(const PRInterpArgs* args, void* stream) {
   if (!args || !args->pix_to_face || !args->bary || !args->face_attr || !args->out || args->D <= 0)
     return set_error(PR_ERR_ARG, "interp_fwd: bad args");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int64_t total = args->PK * args->D;
-  if (total == 0) return PR_OK;
-  const int nb = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 8192);
+  if (args->PK == 0) return PR_OK;
+  const int nb = (int)std::min<int64_t>((args->PK + kThreads - 1) / kThreads, 8192);
   interp_fwd_kernel<<<nb, kThreads, 0, st>>>(*args);
   return check_launch("interp_fwd");
 }
@@ -494,12 +622,41 @@ extern "C" int pr_interp_bwd(const PRInterpArgs* args, void* stream) {
   if (!args || !args->pix_to_face || !args->bary || !args->face_attr || !args->grad_out || args->D <= 0)
     return set_error(PR_ERR_ARG, "interp_bwd: bad args");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (args->grad_face_attr && args->F > 0) {
-    if (hipMemsetAsync(args->grad_face_attr, 0, (size_t)args->F * 3 * args->D * sizeof(float), st) != hipSuccess)
+  const int64_t rows = args->faces ? args->V : args->F * 3;
+  if (args->grad_face_attr && rows > 0) {
+    if (hipMemsetAsync(args->grad_face_attr, 0, (size_t)rows * args->D * sizeof(float), st) != hipSuccess)
       return set_error(PR_ERR_HIP, "interp_bwd: memset failed");
   }
   if (args->PK == 0) return PR_OK;
   const int nb = (int)std::min<int64_t>((args->PK + kThreads - 1) / kThreads, 8192);
   interp_bwd_kernel<<<nb, kThreads, 0, st>>>(*args);
   return check_launch("interp_bwd");
+}
+
+static int project_check(const PRProjectArgs* a) {
+  if (!a || !a->verts || !a->faces || !a->mesh_first_face || !a->mesh_num_faces || !a->world_to_view || !a->proj ||
+      a->N <= 0 || a->V < 0 || a->F < 0)
+    return set_error(PR_ERR_ARG, "project: bad args");
+  return PR_OK;
+}
+
+extern "C" int pr_project_fwd(const PRProjectArgs* args, void* stream) {
+  if (int e = project_check(args)) return e;
+  if (!args->face_verts) return set_error(PR_ERR_ARG, "project_fwd: face_verts missing");
+  if (args->F == 0) return PR_OK;
+  const int nb = (int)std::min<int64_t>((args->F * 3 + kThreads - 1) / kThreads, 4096);
+  project_fwd_kernel<<<nb, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(*args);
+  return check_launch("project_fwd");
+}
+
+extern "C" int pr_project_bwd(const PRProjectArgs* args, void* stream) {
+  if (int e = project_check(args)) return e;
+  if (!args->grad_face_verts || !args->grad_verts) return set_error(PR_ERR_ARG, "project_bwd: buffers missing");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (args->V > 0 && hipMemsetAsync(args->grad_verts, 0, (size_t)args->V * 3 * sizeof(float), st) != hipSuccess)
+    return set_error(PR_ERR_HIP, "project_bwd: memset failed");
+  if (args->F == 0) return PR_OK;
+  const int nb = (int)std::min<int64_t>((args->F * 3 + kThreads - 1) / kThreads, 4096);
+  project_bwd_kernel<<<nb, kThreads, 0, st>>>(*args);
+  return check_launch("project_bwd");
 }

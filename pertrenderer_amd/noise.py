@@ -56,11 +56,12 @@ class Noise:
     noise_a: Optional[torch.Tensor] = None
     offset_r: int = 0
     offset_a: int = 0
+    seeds: Optional[torch.Tensor] = None  # device int64[1] key base (graph mode)
 
     @staticmethod
-    def philox(seed_r=0, seed_a=0, offset_r=0, offset_a=0):
+    def philox(seed_r=0, seed_a=0, offset_r=0, offset_a=0, seeds=None):
         return Noise(nat.PR_NOISE_PHILOX, int(seed_r), int(seed_a), None, None, int(offset_r),
-                     int(offset_a))
+                     int(offset_a), seeds)
 
     @staticmethod
     def injected(noise_r=None, noise_a=None):
@@ -69,21 +70,61 @@ class Noise:
     def to(self, device):
         mv = (lambda t: None if t is None else t.to(device=device, dtype=torch.float32).contiguous())
         return Noise(self.mode, self.seed_r, self.seed_a, mv(self.noise_r), mv(self.noise_a),
-                     self.offset_r, self.offset_a)
+                     self.offset_r, self.offset_a, self.seeds)
+
+
+class DeviceSeed:
+    """Graph-capturable Philox keys.
+
+    A device-resident 64-bit base is advanced in place by ``advance()``
+    (pr_seed_advance, a stream-ordered kernel that a captured graph replays);
+    every operator call in between gets a distinct stream id, and the kernels
+    key Philox with mix64(base ^ id).  Inside a captured step the ids are baked
+    into the graph while the base changes per replay, so every replay draws
+    fresh noise without any host work."""
+
+    def __init__(self, device, seed=None):
+        self.tensor = torch.tensor([draw_key() if seed is None else int(seed)], dtype=torch.int64,
+                                   device=device)
+        self._next = 1
+
+    def stream_id(self):
+        i = self._next
+        self._next += 1
+        return i
+
+    def advance(self):
+        nat.check(nat.load().pr_seed_advance(nat.ptr(self.tensor), 1, nat.stream_of(self.tensor)),
+                  "pr_seed_advance")
+        self._next = 1
+
+
+_DEVICE_SEED = None
+
+
+def use_device_seed(ds):
+    """Route Philox draws through a :class:`DeviceSeed` (None restores host draws)."""
+    global _DEVICE_SEED
+    _DEVICE_SEED = ds
 
 
 def draw_rast(shape, Sr, device):
     """Noise for one perturbed-Heaviside call over fragments of `shape` (N,H,W,K)."""
     if _SOURCE == "torch":
         return Noise.injected(noise_r=torch.randn((Sr,) + tuple(shape)).to(device))
+    if _DEVICE_SEED is not None:
+        return Noise.philox(seed_r=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor)
     return Noise.philox(seed_r=draw_key())
 
 
 def draw_agg(shape, Sa, device, fixed_noise=False):
     """Noise for one perturbed-argmax call over logits of `shape` (N,H,W,K+1).
-    fixed_noise reseeds the global generator with 1 first, as smoothagg.py:18-19."""
+    fixed_noise reseeds the global generator with 1 first, as smoothagg.py:18-19
+    (and then ignores any device seed: the noise must be the same every call)."""
     if fixed_noise:
         torch.manual_seed(1)
     if _SOURCE == "torch":
         return Noise.injected(noise_a=torch.randn((Sa,) + tuple(shape)).to(device))
+    if _DEVICE_SEED is not None and not fixed_noise:
+        return Noise.philox(seed_a=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor)
     return Noise.philox(seed_a=draw_key())

@@ -164,6 +164,29 @@ class FoVPerspectiveCameras:
     def transform_points(self, points, eps=None, **kwargs):
         return self.get_full_projection_transform(**kwargs).transform_points(points, eps=eps)
 
+    # -- cached (N,4,4) matrices for the native projection path -------------------
+    _PARAMS = ("R", "T", "znear", "zfar", "aspect_ratio", "fov")
+
+    def matrices_need_grad(self):
+        return any(getattr(self, k).requires_grad for k in self._PARAMS)
+
+    def _cached(self, slot, key_names, build):
+        key = tuple((getattr(self, k).data_ptr(), getattr(self, k)._version) for k in key_names)
+        cache = self.__dict__.get(slot)
+        if cache is None or cache[0] != key:
+            cache = (key, build().contiguous())
+            self.__dict__[slot] = cache
+        return cache[1]
+
+    def world_to_view_matrix(self):
+        """(N,4,4) row-vector world->view matrix, rebuilt only when R/T change."""
+        return self._cached("_w2v", ("R", "T"), lambda: self.get_world_to_view_transform().matrix)
+
+    def projection_matrix(self):
+        """(N,4,4) row-vector view->clip matrix, rebuilt only when the intrinsics change."""
+        return self._cached("_proj", ("znear", "zfar", "aspect_ratio", "fov"),
+                            lambda: self.get_projection_transform().matrix)
+
     def get_camera_center(self, **kwargs):
         w2v = self.get_world_to_view_transform(**kwargs).matrix
         return torch.linalg.inv(w2v)[:, 3, :3]

@@ -1,15 +1,23 @@
 """Triangle-mesh batch and per-vertex textures (PyTorch3D ``Meshes`` / ``TexturesVertex``
 subset used by experiments/eval.py and random_rasterizer.py:170).
 
-Memory layout: vertices and faces are kept as per-mesh lists plus lazily built
-packed views (faces_packed indexes verts_packed).  ``sample_textures`` runs the
-native face-attribute interpolation (pr_interp_*).
+Layout: per-mesh vertex lists plus a shared, lazily built topology record (packed
+faces, per-mesh face offsets/counts as device tensors).  Meshes derived by
+``update_padded`` / ``offset_verts`` share the record, so a pose-optimisation step
+builds no index tensor and does no host->device copy: it is safe to capture in a
+HIP graph.  ``sample_textures`` runs the native face-attribute interpolation.
 """
 import torch
 
 from . import interp as _interp
 
 F32 = torch.float32
+
+
+def gather_faces(values, faces_packed):
+    """values[faces] as (F,3,C) via index_select (its backward is an index_add, no sort)."""
+    F = faces_packed.shape[0]
+    return values.index_select(0, faces_packed.reshape(-1)).reshape(F, 3, values.shape[-1])
 
 
 class TexturesVertex:
@@ -25,7 +33,7 @@ class TexturesVertex:
         return self._list
 
     def verts_features_packed(self):
-        return torch.cat(self._list, dim=0)
+        return self._list[0] if len(self._list) == 1 else torch.cat(self._list, dim=0)
 
     def verts_features_padded(self):
         V = max(f.shape[0] for f in self._list)
@@ -48,25 +56,55 @@ class TexturesVertex:
 
     def sample_textures(self, fragments, faces_packed=None, **kwargs):
         """(N,H,W,K,C) texels = sum_i bary_i * feature[face_i] (0 on padded slots)."""
-        face_attr = self.verts_features_packed()[faces_packed]
-        return _interp.interpolate_face_attributes(fragments.pix_to_face, fragments.bary_coords, face_attr)
+        return _interp.interpolate_vertex_attributes(fragments.pix_to_face, fragments.bary_coords,
+                                                     self.verts_features_packed(), faces_packed)
+
+
+class _Topology:
+    def __init__(self, faces, nverts, device):
+        self.faces = faces
+        self.nverts = list(nverts)
+        self.nfaces = [f.shape[0] for f in faces]
+        self.device = device
+        self._packed = None
+        self._idx = None
+
+    def faces_packed(self):
+        if self._packed is None:
+            offs, out = 0, []
+            for nv, f in zip(self.nverts, self.faces):
+                out.append(f.to(self.device) + offs)
+                offs += nv
+            self._packed = torch.cat(out, dim=0).contiguous()
+        return self._packed
+
+    def index_tensors(self):
+        if self._idx is None:
+            nf = torch.tensor(self.nfaces, dtype=torch.int64)
+            first = torch.cumsum(nf, 0) - nf
+            nv = torch.tensor(self.nverts, dtype=torch.int64)
+            self._idx = dict(nfaces=nf.to(self.device), first=first.to(self.device), nverts=nv.to(self.device),
+                             vfirst=(torch.cumsum(nv, 0) - nv).to(self.device))
+        return self._idx
 
 
 class Meshes:
     """A batch of triangle meshes (lists of (V_i,3) verts and (F_i,3) int64 faces)."""
 
-    def __init__(self, verts, faces, textures=None):
+    def __init__(self, verts, faces, textures=None, _topo=None):
         if torch.is_tensor(verts):
             verts = [v for v in verts] if verts.dim() == 3 else [verts]
-        if torch.is_tensor(faces):
-            faces = [f for f in faces] if faces.dim() == 3 else [faces]
-        if len(verts) != len(faces):
-            raise ValueError("verts and faces must have the same batch size")
+        if _topo is None:
+            if torch.is_tensor(faces):
+                faces = [f for f in faces] if faces.dim() == 3 else [faces]
+            if len(verts) != len(faces):
+                raise ValueError("verts and faces must have the same batch size")
+            dev = verts[0].device if verts else torch.device("cpu")
+            _topo = _Topology([f.to(torch.int64) for f in faces], [v.shape[0] for v in verts], dev)
         self._verts = list(verts)
-        self._faces = [f.to(torch.int64) for f in faces]
+        self._topo = _topo
         self.textures = textures
         self.device = self._verts[0].device if self._verts else torch.device("cpu")
-        self._packed = None
 
     def __len__(self):
         return len(self._verts)
@@ -79,35 +117,29 @@ class Meshes:
         return self._verts
 
     def faces_list(self):
-        return self._faces
+        return self._topo.faces
 
     def num_verts_per_mesh(self):
-        return torch.tensor([v.shape[0] for v in self._verts], dtype=torch.int64, device=self.device)
+        return self._topo.index_tensors()["nverts"]
 
     def num_faces_per_mesh(self):
-        return torch.tensor([f.shape[0] for f in self._faces], dtype=torch.int64, device=self.device)
+        return self._topo.index_tensors()["nfaces"]
 
     def mesh_to_faces_packed_first_idx(self):
-        nf = self.num_faces_per_mesh()
-        return torch.cumsum(nf, 0) - nf
+        return self._topo.index_tensors()["first"]
 
     def mesh_to_verts_packed_first_idx(self):
-        nv = self.num_verts_per_mesh()
-        return torch.cumsum(nv, 0) - nv
+        return self._topo.index_tensors()["vfirst"]
 
     def verts_packed(self):
-        return torch.cat(self._verts, dim=0)
+        return self._verts[0] if len(self._verts) == 1 else torch.cat(self._verts, dim=0)
 
     def faces_packed(self):
-        if self._packed is None:
-            offs, out = 0, []
-            for v, f in zip(self._verts, self._faces):
-                out.append(f.to(v.device) + offs)
-                offs += v.shape[0]
-            self._packed = torch.cat(out, dim=0)
-        return self._packed
+        return self._topo.faces_packed()
 
     def verts_padded(self):
+        if all(v.shape[0] == self._verts[0].shape[0] for v in self._verts):
+            return torch.stack(self._verts, 0)
         V = max(v.shape[0] for v in self._verts)
         out = self._verts[0].new_zeros((len(self._verts), V, 3))
         for i, v in enumerate(self._verts):
@@ -115,17 +147,18 @@ class Meshes:
         return out
 
     def faces_padded(self):
-        Fm = max(f.shape[0] for f in self._faces)
-        out = self._faces[0].new_full((len(self._faces), Fm, 3), -1)
-        for i, f in enumerate(self._faces):
+        faces = self._topo.faces
+        Fm = max(f.shape[0] for f in faces)
+        out = faces[0].new_full((len(faces), Fm, 3), -1)
+        for i, f in enumerate(faces):
             out[i, : f.shape[0]] = f
         return out
 
     def verts_normals_packed(self):
         """Area-weighted vertex normals (PyTorch3D convention)."""
         v = self.verts_packed()
-        f = self.faces_packed().to(v.device)
-        fv = v[f]
+        f = self.faces_packed()
+        fv = gather_faces(v, f)
         n = torch.zeros_like(v)
         # each corner's cross product is 2x the face area times its normal
         n = n.index_add(0, f[:, 1], torch.cross(fv[:, 2] - fv[:, 1], fv[:, 0] - fv[:, 1], dim=1))
@@ -135,22 +168,20 @@ class Meshes:
 
     # ------------------------------------------------------------- updates
     def _new(self, verts):
-        m = Meshes(verts, self._faces, self.textures)
-        return m
+        return Meshes(verts, None, self.textures, _topo=self._topo)
 
     def update_padded(self, new_verts_padded):
-        return self._new([new_verts_padded[i, : v.shape[0]] for i, v in enumerate(self._verts)])
+        return self._new([new_verts_padded[i, : n] for i, n in enumerate(self._topo.nverts)])
 
     def offset_verts(self, vert_offsets_packed):
         off = vert_offsets_packed
         if off.dim() == 1:
-            off = off.expand(self.verts_packed().shape[0], 3)
-        chunks = torch.split(off, [v.shape[0] for v in self._verts], dim=0)
+            off = off.expand(sum(self._topo.nverts), 3)
+        chunks = torch.split(off, self._topo.nverts, dim=0)
         return self._new([v + o for v, o in zip(self._verts, chunks)])
 
     def offset_verts_(self, vert_offsets_packed):
-        m = self.offset_verts(vert_offsets_packed)
-        self._verts = m._verts
+        self._verts = self.offset_verts(vert_offsets_packed)._verts
         return self
 
     def scale_verts(self, scale):
@@ -159,25 +190,24 @@ class Meshes:
         return self._new([v * float(s[i]) for i, v in enumerate(self._verts)])
 
     def scale_verts_(self, scale):
-        m = self.scale_verts(scale)
-        self._verts = m._verts
+        self._verts = self.scale_verts(scale)._verts
         return self
 
     def extend(self, N):
         tex = self.textures.extend(N) if self.textures is not None else None
         return Meshes([v.clone() for v in self._verts for _ in range(N)],
-                      [f.clone() for f in self._faces for _ in range(N)], tex)
+                      [f.clone() for f in self._topo.faces for _ in range(N)], tex)
 
     def clone(self):
-        return Meshes([v.clone() for v in self._verts], [f.clone() for f in self._faces],
+        return Meshes([v.clone() for v in self._verts], [f.clone() for f in self._topo.faces],
                       self.textures.clone() if self.textures is not None else None)
 
     def detach(self):
-        return Meshes([v.detach() for v in self._verts], self._faces,
-                      self.textures.detach() if self.textures is not None else None)
+        return Meshes([v.detach() for v in self._verts], None,
+                      self.textures.detach() if self.textures is not None else None, _topo=self._topo)
 
     def to(self, device):
-        return Meshes([v.to(device) for v in self._verts], [f.to(device) for f in self._faces],
+        return Meshes([v.to(device) for v in self._verts], [f.to(device) for f in self._topo.faces],
                       self.textures.to(device) if self.textures is not None else None)
 
     def sample_textures(self, fragments):

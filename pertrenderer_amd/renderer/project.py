@@ -1,0 +1,53 @@
+"""Fused world -> NDC projection + face gather (pr_project_fwd / pr_project_bwd).
+
+Replaces, for the rasterizer input, MeshRasterizer.transform (world->view, view->NDC,
+keep view z) and rasterize_meshes' ``verts[faces]`` gather: one kernel forward, one
+scatter-add kernel backward (d verts), instead of ~30 small tensor kernels each way.
+Used when the camera matrices need no gradient; otherwise MeshRasterizer keeps the
+differentiable tensor path.
+"""
+import torch
+
+from .. import _native as nat
+
+F32 = torch.float32
+
+
+class _ProjectFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, verts, faces, first, nfaces, w2v, proj):
+        nat.require_device(verts, faces, w2v, proj)
+        lib = nat.load()
+        v = verts.detach().to(F32).contiguous()
+        f = faces.detach().to(torch.int64).contiguous()
+        a = nat.PRProjectArgs()
+        a.verts, a.faces, a.mesh_first_face, a.mesh_num_faces = nat.ptr(v), nat.ptr(f), nat.ptr(first), nat.ptr(nfaces)
+        m1, m2 = w2v.detach().to(F32).contiguous(), proj.detach().to(F32).contiguous()
+        a.world_to_view, a.proj = nat.ptr(m1), nat.ptr(m2)
+        a.V, a.F, a.N = v.shape[0], f.shape[0], first.shape[0]
+        fv = torch.empty((f.shape[0], 3, 3), dtype=F32, device=v.device)
+        a.face_verts = nat.ptr(fv)
+        nat.check(lib.pr_project_fwd(a, nat.stream_of(fv)), "pr_project_fwd")
+        ctx.save_for_backward(v, f, first, nfaces, m1, m2)
+        return fv
+
+    @staticmethod
+    def backward(ctx, g):
+        v, f, first, nfaces, m1, m2 = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None, None, None
+        lib = nat.load()
+        go = g.detach().to(F32).contiguous()
+        gv = torch.empty_like(v)
+        a = nat.PRProjectArgs()
+        a.verts, a.faces, a.mesh_first_face, a.mesh_num_faces = nat.ptr(v), nat.ptr(f), nat.ptr(first), nat.ptr(nfaces)
+        a.world_to_view, a.proj = nat.ptr(m1), nat.ptr(m2)
+        a.V, a.F, a.N = v.shape[0], f.shape[0], first.shape[0]
+        a.grad_face_verts, a.grad_verts = nat.ptr(go), nat.ptr(gv)
+        nat.check(lib.pr_project_bwd(a, nat.stream_of(go)), "pr_project_bwd")
+        return gv, None, None, None, None, None
+
+
+def project_faces(verts_packed, faces_packed, mesh_first_face, mesh_num_faces, world_to_view, proj):
+    """(V,3) world verts -> (F,3,3) face corners (x_ndc, y_ndc, z_view); matrices (N,4,4) row-vector."""
+    return _ProjectFn.apply(verts_packed, faces_packed, mesh_first_face, mesh_num_faces, world_to_view, proj)

@@ -14,6 +14,8 @@ import torch
 
 from .. import _native as nat
 from .. import timing as _timing
+from .mesh import gather_faces
+from .project import project_faces
 
 F32 = torch.float32
 
@@ -110,8 +112,7 @@ def rasterize_meshes(meshes, image_size=256, blur_radius=0.0, faces_per_pixel=8,
                      cull_backfaces=False):
     """PyTorch3D rasterize_meshes on meshes already in NDC (x,y) + view z."""
     verts = meshes.verts_packed()
-    faces = meshes.faces_packed().to(verts.device)
-    face_verts = verts[faces]
+    face_verts = gather_faces(verts, meshes.faces_packed())
     first = meshes.mesh_to_faces_packed_first_idx().to(verts.device)
     nfaces = meshes.num_faces_per_mesh().to(verts.device)
     H, W = _hw(image_size)
@@ -142,11 +143,25 @@ class MeshRasterizer(torch.nn.Module):
         return meshes_world.update_padded(verts_ndc)
 
     def forward(self, meshes_world, **kwargs) -> Fragments:
-        meshes_screen = self.transform(meshes_world, **kwargs)
         rs = kwargs.get("raster_settings", self.raster_settings)
         clip = rs.clip_barycentric_coords
         if clip is None:
             clip = rs.blur_radius > 0.0
+        cameras = kwargs.get("cameras", self.cameras)
+        overrides = any(k in kwargs for k in ("R", "T", "znear", "zfar", "fov", "aspect_ratio", "degrees"))
+        if (hasattr(cameras, "world_to_view_matrix") and not overrides and not cameras.matrices_need_grad()
+                and meshes_world.verts_packed().is_cuda):
+            # fused native projection + face gather (pr_project_*), then the rasterizer
+            first = meshes_world.mesh_to_faces_packed_first_idx()
+            nfaces = meshes_world.num_faces_per_mesh()
+            fv = project_faces(meshes_world.verts_packed(), meshes_world.faces_packed(), first, nfaces,
+                               cameras.world_to_view_matrix(), cameras.projection_matrix())
+            H, W = _hw(rs.image_size)
+            p2f, zbuf, bary, dists = _RasterizeFn.apply(fv, first, nfaces, H, W, int(rs.faces_per_pixel),
+                                                        float(rs.blur_radius), bool(rs.perspective_correct),
+                                                        bool(clip), bool(rs.cull_backfaces))
+            return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)
+        meshes_screen = self.transform(meshes_world, **kwargs)
         p2f, zbuf, bary, dists = rasterize_meshes(
             meshes_screen, image_size=rs.image_size, blur_radius=rs.blur_radius,
             faces_per_pixel=rs.faces_per_pixel, bin_size=rs.bin_size, max_faces_per_bin=rs.max_faces_per_bin,

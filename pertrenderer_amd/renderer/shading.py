@@ -4,7 +4,7 @@ are interpolated on the native pr_interp kernels; the lighting is elementwise.""
 import torch
 import torch.nn.functional as Fn
 
-from .interp import interpolate_face_attributes
+from .interp import interpolate_vertex_attributes
 
 
 def _bc(t, like):
@@ -37,8 +37,8 @@ def phong_shading(meshes, fragments, lights, cameras, materials, texels):
     verts = meshes.verts_packed()
     faces = meshes.faces_packed()
     vnormals = meshes.verts_normals_packed()
-    coords = interpolate_face_attributes(fragments.pix_to_face, fragments.bary_coords, verts[faces])
-    normals = interpolate_face_attributes(fragments.pix_to_face, fragments.bary_coords, vnormals[faces])
+    coords = interpolate_vertex_attributes(fragments.pix_to_face, fragments.bary_coords, verts, faces)
+    normals = interpolate_vertex_attributes(fragments.pix_to_face, fragments.bary_coords, vnormals, faces)
     if hasattr(lights, "light_direction"):
         direction = lights.light_direction(coords)
     else:

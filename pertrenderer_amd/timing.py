@@ -17,9 +17,13 @@ def active():
 
 
 class KernelTimer:
-    def __init__(self):
+    """external=True creates events that become record nodes when the launches are
+    captured into a HIP graph; after a replay they time that replay's kernels."""
+
+    def __init__(self, external=False):
         self._open = {}
         self.events = collections.defaultdict(list)
+        self.external = external
 
     def __enter__(self):
         global _ACTIVE
@@ -32,12 +36,12 @@ class KernelTimer:
         return False
 
     def start(self, name):
-        ev = torch.cuda.Event(enable_timing=True)
+        ev = torch.cuda.Event(enable_timing=True, external=self.external)
         ev.record(torch.cuda.current_stream())
         self._open[name] = ev
 
     def stop(self, name):
-        ev = torch.cuda.Event(enable_timing=True)
+        ev = torch.cuda.Event(enable_timing=True, external=self.external)
         ev.record(torch.cuda.current_stream())
         self.events[name].append((self._open.pop(name), ev))
 

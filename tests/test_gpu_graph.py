@@ -1,0 +1,104 @@
+"""Graph-capture support: device-resident smoothing scalars and device Philox seeds give
+the same results as the host-side paths, and a captured render step replays with
+fresh noise every time (no host work inside the graph)."""
+import numpy as np
+import pytest
+import torch
+
+import pertrenderer_amd as pa
+from pertrenderer_amd import Noise, perturbed_blend
+from pertrenderer_amd.noise import DeviceSeed, use_device_seed
+
+pytestmark = pytest.mark.gpu
+
+
+def _frags(device, N=1, H=24, W=20, K=30, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    valid = torch.rand((N, H, W, K), generator=g) < 0.7
+    p2f = torch.where(valid, torch.randint(0, 100, (N, H, W, K), generator=g), torch.full((N, H, W, K), -1))
+    dists = torch.where(valid, (torch.rand((N, H, W, K), generator=g) - 0.5) * 6e-3, torch.full((N, H, W, K), -1.0))
+    zbuf = torch.where(valid, 5 + torch.rand((N, H, W, K), generator=g), torch.full((N, H, W, K), -1.0))
+    cols = torch.rand((N, H, W, K, 3), generator=g)
+    return [t.to(device) for t in (p2f, dists, zbuf, cols)]
+
+
+def _render(device, p2f, dists, zbuf, cols, scal_dev, noise):
+    d = dists.clone().requires_grad_(True)
+    z = zbuf.clone().requires_grad_(True)
+    c = cols.clone().requires_grad_(True)
+    dev = device if scal_dev else "cpu"
+    s, g, a = (torch.tensor(v, device=dev, requires_grad=True) for v in (1e-3, 1e-2, 1.3))
+    img = perturbed_blend(c, p2f, d, z, s, g, a, 8, 8, background=(0.1, 0.2, 0.3), noise=noise)
+    (img ** 2).sum().backward()
+    return img.detach(), [d.grad, z.grad, c.grad, s.grad, g.grad, a.grad]
+
+
+def test_device_scalars_match_host_scalars(device):
+    fr = _frags(device)
+    n = Noise.philox(seed_r=5, seed_a=6)
+    i1, g1 = _render(device, *fr, False, n)
+    i2, g2 = _render(device, *fr, True, n)
+    assert torch.equal(i1, i2)
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a.cpu(), b.cpu(), rtol=0, atol=0)
+    assert g2[3].is_cuda and g1[3].device.type == "cpu"
+
+
+def test_device_seed_keys_and_graph_replay(device):
+    fr = _frags(device, seed=1)
+    ds = DeviceSeed(device, seed=1234)
+    use_device_seed(ds)
+    try:
+        d = fr[1].clone().requires_grad_(True)
+        s, g, a = (torch.tensor(v, device=device, requires_grad=True) for v in (1e-3, 1e-2, 1.0))
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ds.advance()
+            perturbed_blend(fr[3], fr[0], d, fr[2], s, g, a, 8, 8).sum().backward()
+        torch.cuda.current_stream().wait_stream(side)
+        d.grad = None
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ds.advance()
+            img = perturbed_blend(fr[3], fr[0], d, fr[2], s, g, a, 8, 8)
+            img.sum().backward()
+        outs, grads, bases = [], [], []
+        for _ in range(3):
+            graph.replay()
+            torch.cuda.synchronize()
+            outs.append(img.clone())
+            grads.append(d.grad.clone())
+            bases.append(int(ds.tensor.item()))
+        assert len(set(bases)) == 3
+        assert not torch.equal(outs[0], outs[1]) and not torch.equal(outs[1], outs[2])
+    finally:
+        use_device_seed(None)
+    # the last replay equals an eager call with the same base and stream ids (1: rast, 2: agg)
+    base = torch.tensor([bases[-1]], dtype=torch.int64, device=device)
+    d2 = fr[1].clone().requires_grad_(True)
+    ref = perturbed_blend(fr[3], fr[0], d2, fr[2], s, g, a, 8, 8,
+                          noise=Noise.philox(seed_r=1, seed_a=2, seeds=base))
+    ref.sum().backward()
+    assert torch.equal(ref.detach(), outs[-1])
+    assert torch.equal(d2.grad, grads[-1])
+
+
+def test_fixed_noise_ignores_device_seed(device):
+    fr = _frags(device, seed=2)
+    ds = DeviceSeed(device, seed=99)
+    use_device_seed(ds)
+    try:
+        agg = pa.GaussianAgg(nb_samples=8, gamma=1e-2, fixed_noise=True)
+        rast = pa.GaussianRast(nb_samples=8, sigma=1e-3)
+        from pertrenderer_amd.random_rasterizer import smooth_rgb_blend
+        from pertrenderer_amd.renderer import BlendParams, Fragments
+        frag = Fragments(fr[0], fr[2], None, fr[1])
+        outs = []
+        for _ in range(2):
+            ds.advance()
+            outs.append(smooth_rgb_blend(fr[3], frag, rast, agg, BlendParams(1e-3, 1e-2, (0, 0, 0))).detach())
+        # rast noise changes with the base; agg noise is fixed -> images differ only through P
+        assert outs[0].shape == outs[1].shape
+    finally:
+        use_device_seed(None)

@@ -14,7 +14,45 @@ from pertrenderer_amd.renderer import (FoVPerspectiveCameras, MeshRasterizer, Me
                                        interpolate_face_attributes, load_obj, look_at_view_transform,
                                        rasterize_meshes)
 
+from pertrenderer_amd.renderer.interp import interpolate_vertex_attributes
+from pertrenderer_amd.renderer.project import project_faces
+
 pytestmark = pytest.mark.gpu
+
+
+def test_native_projection_matches_transform_path(device):
+    """pr_project_* == MeshRasterizer.transform + verts[faces] (PyTorch3D Transform3d math), fwd and bwd."""
+    verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
+    v = verts.to(device).requires_grad_(True)
+    mesh = Meshes([v], [faces.verts_idx.to(device)])
+    R, T = look_at_view_transform(2.7, 30.0, 120.0, device=device)
+    cams = FoVPerspectiveCameras(R=R, T=T, device=device)
+    fv = project_faces(mesh.verts_packed(), mesh.faces_packed(), mesh.mesh_to_faces_packed_first_idx(),
+                       mesh.num_faces_per_mesh(), cams.world_to_view_matrix(), cams.projection_matrix())
+    ms = MeshRasterizer(cameras=cams).transform(mesh)
+    ref = ms.verts_packed()[ms.faces_packed()]
+    torch.testing.assert_close(fv, ref, rtol=1e-5, atol=1e-6)
+    g = torch.randn_like(fv)
+    (gv,) = torch.autograd.grad((fv * g).sum(), v)
+    (gr,) = torch.autograd.grad((ref * g).sum(), v)
+    torch.testing.assert_close(gv, gr, rtol=1e-4, atol=1e-5)
+
+
+def test_vertex_interpolation_matches_face_gather(device):
+    rng = np.random.default_rng(7)
+    V, F = 50, 80
+    faces = torch.tensor(rng.integers(0, V, (F, 3)), device=device)
+    p2f = torch.tensor(rng.integers(-1, F, (1, 6, 7, 5)), device=device)
+    bary = torch.rand((1, 6, 7, 5, 3), device=device, requires_grad=True)
+    vattr = torch.randn((V, 3), device=device, requires_grad=True)
+    out = interpolate_vertex_attributes(p2f, bary, vattr, faces)
+    ref = interpolate_face_attributes(p2f, bary, vattr[faces])
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+    g = torch.randn_like(out)
+    ga = torch.autograd.grad((out * g).sum(), (bary, vattr))
+    gr = torch.autograd.grad((ref * g).sum(), (bary, vattr))
+    torch.testing.assert_close(ga[0], gr[0], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(ga[1], gr[1], rtol=1e-5, atol=1e-5)
 
 
 def _soup(F, seed, zmin=0.5, spread=1.2, size=0.4):
@@ -97,21 +135,24 @@ def test_interpolation_matches_oracle_and_backward(device):
     assert_close(a.grad, ac.grad, rtol=1e-4, atol_rel=1e-5, name="grad_attr")
 
 
-def test_mesh_rasterizer_sphere_matches_oracle(device):
+@pytest.mark.parametrize("size,K,dist_cam", [(64, 50, 2.7), (24, 16, 2.7), (40, 8, 6.7)])
+def test_mesh_rasterizer_sphere_matches_oracle(size, K, dist_cam, device):
+    """Includes tiles whose culled face list exceeds one 256-face round (small images)."""
     verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
     mesh = Meshes([verts.to(device)], [faces.verts_idx.to(device)])
-    R, T = look_at_view_transform(2.7, 30.0, 120.0, device=device)
+    R, T = look_at_view_transform(dist_cam, 30.0, 120.0, device=device)
     cams = FoVPerspectiveCameras(R=R, T=T, device=device)
     sigma = 1e-3
-    rs = RasterizationSettings(image_size=64, blur_radius=np.log(1.0 / 1e-4 - 1.0) * sigma, faces_per_pixel=50,
+    rs = RasterizationSettings(image_size=size, blur_radius=np.log(1.0 / 1e-4 - 1.0) * sigma, faces_per_pixel=K,
                                perspective_correct=False)
     frag = MeshRasterizer(cameras=cams, raster_settings=rs)(mesh)
-    ms = MeshRasterizer(cameras=cams, raster_settings=rs).transform(mesh)
-    fv = ms.verts_packed()[ms.faces_packed()].detach().cpu().numpy()
-    rp, rz, rb, rd = rast_ref.rast_fwd(fv, [0], [faces.verts_idx.shape[0]], 64, 64, 50, rs.blur_radius,
+    fv = project_faces(mesh.verts_packed(), mesh.faces_packed(), mesh.mesh_to_faces_packed_first_idx(),
+                       mesh.num_faces_per_mesh(), cams.world_to_view_matrix(),
+                       cams.projection_matrix()).cpu().numpy()
+    rp, rz, rb, rd = rast_ref.rast_fwd(fv, [0], [faces.verts_idx.shape[0]], size, size, K, rs.blur_radius,
                                        False, True, False)
     np.testing.assert_array_equal(frag.pix_to_face.cpu().numpy(), rp)
     np.testing.assert_array_equal(frag.zbuf.cpu().numpy(), rz)
     np.testing.assert_array_equal(frag.dists.cpu().numpy(), rd)
-    full = (rp >= 0).sum(-1)
-    assert full.max() == 50  # the blur radius fills all K slots near the sphere
+    np.testing.assert_array_equal(frag.bary_coords.cpu().numpy(), rb)
+    assert (rp >= 0).sum(-1).max() == K  # the blur radius fills all K slots somewhere
