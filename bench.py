@@ -36,6 +36,7 @@ import pertrenderer_amd as pa  # noqa: E402
 from pertrenderer_amd.renderer import (FoVPerspectiveCameras, MeshRasterizer, MeshRenderer, Meshes,  # noqa: E402
                                        RasterizationSettings, TexturesVertex, load_obj, look_at_view_transform)
 from pertrenderer_amd.renderer.transforms import Rotate, so3_exponential_map  # noqa: E402
+from pertrenderer_amd.parallel import average_gradients  # noqa: E402
 from pertrenderer_amd.timing import KernelTimer  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
@@ -96,17 +97,8 @@ class Workload:
 
 def allreduce_grads(params, world):
     """The single gradient reduction of the data-parallel step: one flattened RCCL
-    all-reduce (sum) of every gradient, then / world."""
-    grads = [p.grad.to("cuda", non_blocking=True).reshape(-1) for p in params if p.grad is not None]
-    flat = torch.cat(grads)
-    dist.all_reduce(flat)
-    flat /= world
-    off = 0
-    for p in params:
-        if p.grad is not None:
-            n = p.grad.numel()
-            p.grad.copy_(flat[off:off + n].reshape(p.grad.shape).to(p.grad.device))
-            off += n
+    all-reduce of every gradient, averaged over ranks (pertrenderer_amd.parallel)."""
+    average_gradients(params)
 
 
 def kernel_bytes(name, P, K, S, F):
