@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 2
+#define PR_ABI_VERSION 3
 
 /* error codes */
 #define PR_OK 0
@@ -89,6 +89,8 @@ typedef struct PRBlendFwdArgs {
   float* image;               /* COLOR out: (N,H,W,4) */
   float* weights;             /* !COLOR out: (N,H,W,K+1) */
   uint8_t* winners;           /* out: (P,Sa) per-sample argmax index, saved for backward */
+  float* rast_cache;          /* RAST, nullable out: (N,H,W,K,2) per-slot (prob, rast score mean);  */
+                              /* handed to pr_blend_bwd it replaces regenerating the rast noise    */
 } PRBlendFwdArgs;
 
 typedef struct PRBlendBwdArgs {
@@ -109,6 +111,7 @@ typedef struct PRBlendBwdArgs {
   float* grad_scalars;        /* out (3,): d sigma, d gamma, d alpha */
   void* workspace;            /* >= pr_blend_bwd_workspace_size(args) bytes */
   size_t workspace_bytes;
+  const float* rast_cache;    /* RAST, nullable: pr_blend_fwd's rast_cache of the same call */
 } PRBlendBwdArgs;
 
 typedef struct PRHeavisideArgs {

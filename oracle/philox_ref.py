@@ -5,6 +5,7 @@ Restates Salmon, Moraes, Dror & Shaw, "Parallel random numbers: as easy as 1, 2,
 and the counter layout the kernels use:
   rast:  counter (pixel, slot, sample // 4, 0x52415354), key = seed_r
   agg:   counter (pixel, slot, sample // 4, 0x41474752), key = seed_a
+Each block gives 4 N(0,1) samples by Box-Muller (pr_common.h:gauss4).
 Known-answer vectors from Random123's kat_vectors pin the generator itself.
 """
 import numpy as np
@@ -46,33 +47,35 @@ def block(seed, pixel, slot, group, tag):
     return philox4x32_10(ctr, np.broadcast_to(key, ctr.shape[:-1] + (2,)))
 
 
-def rast_uniforms(seed, P, K, S, offset=0):
-    """(S, P, K) uniforms of the rast stream (samples offset..offset+S-1)."""
-    s = np.arange(offset, offset + S)
-    pix = np.arange(P)[None, :, None]
-    slot = np.arange(K)[None, None, :]
-    words = block(seed, pix, slot, (s // 4)[:, None, None], TAG_RAST)       # (S,P,K,4)
-    r = np.take_along_axis(words, (s % 4)[:, None, None, None].repeat(P, 1).repeat(K, 2), axis=-1)[..., 0]
-    return u01(r)
-
-
-def agg_normals(seed, P, KP1, S, offset=0):
-    """(S, P, K+1) Box-Muller normals of the agg stream (float64 math; the kernels use
+def _bm4(w):
+    """Box-Muller on one Philox block (...,4) -> 4 normals (float64 math; the kernels use
     the hardware log2/sqrt/sin/cos, so values agree to a few ulp)."""
+    u = u01(w).astype(np.float64)
+    r0 = np.sqrt(-2.0 * np.log(u[..., 0]))
+    r1 = np.sqrt(-2.0 * np.log(u[..., 2]))
+    return [r0 * np.cos(2 * np.pi * u[..., 1]), r0 * np.sin(2 * np.pi * u[..., 1]),
+            r1 * np.cos(2 * np.pi * u[..., 3]), r1 * np.sin(2 * np.pi * u[..., 3])]
+
+
+def _normals(seed, P, J, S, offset, tag):
     s = np.arange(offset, offset + S)
-    groups = np.unique(s // 4)
     pix = np.arange(P)[:, None]
-    slot = np.arange(KP1)[None, :]
-    out = np.empty((S, P, KP1), np.float64)
-    for g in groups:
-        w = block(seed, pix, slot, g, TAG_AGG)                               # (P,K+1,4)
-        u = u01(w).astype(np.float64)
-        r0 = np.sqrt(-2.0 * np.log(u[..., 0]))
-        r1 = np.sqrt(-2.0 * np.log(u[..., 2]))
-        e = [r0 * np.cos(2 * np.pi * u[..., 1]), r0 * np.sin(2 * np.pi * u[..., 1]),
-             r1 * np.cos(2 * np.pi * u[..., 3]), r1 * np.sin(2 * np.pi * u[..., 3])]
+    slot = np.arange(J)[None, :]
+    out = np.empty((S, P, J), np.float64)
+    for g in np.unique(s // 4):
+        e = _bm4(block(seed, pix, slot, g, tag))                              # 4 x (P,J)
         for q in range(4):
             si = 4 * g + q - offset
             if 0 <= si < S:
                 out[si] = e[q]
     return out
+
+
+def rast_normals(seed, P, K, S, offset=0):
+    """(S, P, K) Box-Muller normals of the rast stream (samples offset..offset+S-1)."""
+    return _normals(seed, P, K, S, offset, TAG_RAST)
+
+
+def agg_normals(seed, P, KP1, S, offset=0):
+    """(S, P, K+1) Box-Muller normals of the agg stream."""
+    return _normals(seed, P, KP1, S, offset, TAG_AGG)

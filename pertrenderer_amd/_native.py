@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpertrender.so")
+# PR_NATIVE_LIB selects a diagnostic build (e.g. the -DPR_RAST_PROFILE variant)
+LIB_PATH = os.environ.get("PR_NATIVE_LIB") or os.path.join(_HERE, "libpertrender.so")
 
 PR_NOISE_PHILOX = 0
 PR_NOISE_INJECTED = 1
@@ -34,7 +35,7 @@ class PRBlendParams(C.Structure):
 class PRBlendFwdArgs(C.Structure):
     _fields_ = [("p", PRBlendParams), ("pix_to_face", _vp), ("mask", _vp), ("dists", _vp),
                 ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("image", _vp), ("weights", _vp),
-                ("winners", _vp)]
+                ("winners", _vp), ("rast_cache", _vp)]
 
 
 class PRBlendBwdArgs(C.Structure):
@@ -42,7 +43,7 @@ class PRBlendBwdArgs(C.Structure):
                 ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("winners", _vp),
                 ("grad_image", _vp), ("grad_weights", _vp), ("grad_dists", _vp), ("grad_prob", _vp),
                 ("grad_zbuf", _vp), ("grad_colors", _vp), ("grad_scalars", _vp),
-                ("workspace", _vp), ("workspace_bytes", C.c_size_t)]
+                ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("rast_cache", _vp)]
 
 
 class PRHeavisideArgs(C.Structure):
@@ -95,7 +96,7 @@ EXPORTS = {
     "pr_project_fwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
     "pr_project_bwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
 }
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lib = None
 

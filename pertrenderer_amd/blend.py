@@ -114,6 +114,12 @@ def _timed(name, fn):
 
 
 # ============================================================== fused blend
+# Keep the per-slot (prob, rast score) of the forward for the backward (8 B/slot of
+# HBM) instead of regenerating the rast noise there.  Either way the results are
+# bit-identical (tests/test_gpu_blend.py::test_rast_cache_is_bit_identical).
+RAST_CACHE = True
+
+
 class _FusedBlendFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, dists, zbuf, colors, sigma, gamma, alpha, p2f, znear, zfar, cfg):
@@ -130,19 +136,21 @@ class _FusedBlendFn(torch.autograd.Function):
                     nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR)
         image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
+        # per-slot (prob, rast score) kept for the backward instead of regenerating rast noise
+        cache = torch.empty((N, H, W, K, 2), dtype=F32, device=dev) if RAST_CACHE and any(ctx.needs_input_grad[:6]) else None
         a = nat.PRBlendFwdArgs()
         a.p = p
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
-        a.image, a.winners = nat.ptr(image), nat.ptr(winners)
+        a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
         _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
-        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, sc_dev)
+        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, sc_dev, cache)
         ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
         ctx.refs = (sigma, gamma, alpha)
         return image
 
     @staticmethod
     def backward(ctx, gimg):
-        p2f_c, d_c, z_c, c_c, zn, zf, winners, sc_dev = ctx.saved_tensors
+        p2f_c, d_c, z_c, c_c, zn, zf, winners, sc_dev, cache = ctx.saved_tensors
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
         lib = nat.load()
         N, H, W, K = p2f_c.shape
@@ -155,7 +163,7 @@ class _FusedBlendFn(torch.autograd.Function):
         a = nat.PRBlendBwdArgs()
         a.p = p
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
-        a.winners, a.grad_image = nat.ptr(winners), nat.ptr(g)
+        a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
         a.grad_dists, a.grad_zbuf, a.grad_colors, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gc), nat.ptr(gsc)
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()

@@ -36,32 +36,38 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not _stale():
+def build(force=False, verbose=True, out=None, defines=()):
+    """Compile SOURCES and link the shared library.  `out`/`defines` build a
+    diagnostic variant (e.g. -DPR_RAST_PROFILE) beside the product library."""
+    lib = out or LIB
+    if out is None and not defines and not force and not _stale():
         return LIB
     hipcc = _hipcc()
     objs = []
+    tag = "" if out is None else "_" + os.path.basename(out).replace(".", "_")
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
-        cmd = [hipcc] + FLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(CSRC, src.replace(".hip", tag + ".o"))
+        cmd = [hipcc] + FLAGS + [f"-D{d}" for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [hipcc, "-shared", f"--offload-arch={ARCH}", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--out", help="diagnostic variant path (default: the product library)")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="preprocessor define")
     args = ap.parse_args()
-    print(build(force=args.force))
+    print(build(force=args.force, out=args.out, defines=args.defines))
     sys.exit(0)

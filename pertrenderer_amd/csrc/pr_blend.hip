@@ -19,10 +19,10 @@
 //     group, slot chunk) and merges chunk partials with shuffles.
 // Nothing of size S x P x K is materialised: noise is regenerated from Philox
 // (or read from injected tensors in parity mode).  In Philox mode two exact
-// skips remove RNG work without changing any result: a rast slot whose
-// threshold Phi(d/sigma) lies outside [2^-24, 1-2^-24] has the same outcome for
-// every 24-bit uniform, and an agg logit more than 2*5.8*gamma below the
-// pixel's largest logit can never win (Box-Muller |eps| <= 5.77 for 24-bit u).
+// skips remove RNG work without changing any result (Box-Muller |eps| <= 5.77
+// for 24-bit uniforms): a rast slot with |dist/sigma| > 5.8 has the same outcome
+// for every sample, and an agg logit more than 2*5.8*gamma below the pixel's
+// largest logit can never win.
 #include "pr_common.h"
 
 namespace pr {
@@ -30,8 +30,6 @@ namespace {
 
 constexpr float kNegInf = -__builtin_inff();
 constexpr float kEpsMaxBM = 5.8f;               // > sqrt(-2 ln 2^-24) = 5.7683
-constexpr float kULo = 5.9604644775390625e-08f;  // smallest uniform (2^-24)
-constexpr float kUHi = 1.0f - 5.9604644775390625e-08f;
 
 struct Geo {
   int64_t P, PK;  // pixels, slots
@@ -80,32 +78,43 @@ PR_DEV int image_of(int n0, int rem0, int pl, int HW) {
        i_ += kThreads, pl += (Q), k += (R), (k >= (L) ? (k -= (L), ++pl) : 0))
 
 // ---------------------------------------------------------------- rast noise
-// Count of "inside" samples for one valid slot.  Injected mode is smoothrast.py:32-33
-// literally: H(D + sigma*eps) with H(0)=1, D = -dist.
+// Both noise modes evaluate smoothrast.py:32-33 literally, m_s = H(D + sigma*eps_s)
+// with H(0)=1 and D = -dist; Philox mode draws eps_s by Box-Muller (4 per Philox
+// block, gauss4).  Box-Muller normals from 24-bit uniforms satisfy |eps| <= 5.7683,
+// so a slot with |dist/sigma| > 5.8 has the same outcome for every sample: exact skip.
+PR_DEV float pick4(const float e[4], uint32_t i) {
+  return i == 0 ? e[0] : (i == 1 ? e[1] : (i == 2 ? e[2] : e[3]));
+}
+
+// -1: every sample inside, +1: every sample outside, 0: must draw (NaN included)
+PR_DEV int rast_saturated(float dist, float sigma) {
+  const float x = dist / sigma;
+  return x < -kEpsMaxBM ? -1 : (x > kEpsMaxBM ? 1 : 0);
+}
+
+// Count of "inside" samples for one valid slot.
 template <int NOISE>
 PR_DEV int rast_count(const PRBlendParams& p, const Sc& sc, float dist, uint32_t gp, int k, int64_t gs,
                       int64_t PK) {
   int cnt = 0;
+  const float D = -dist;
   if constexpr (NOISE == PR_NOISE_INJECTED) {
-    const float D = -dist;
     for (int s = 0; s < p.Sr; ++s) cnt += (D + sc.sigma * p.noise_r[(int64_t)s * PK + gs]) >= 0.f ? 1 : 0;
   } else {
-    const float c = rast_threshold(dist, sc.sigma);
-    if (c <= kULo) return p.Sr;   // every uniform is >= c
-    if (c > kUHi) return 0;       // every uniform is < c
-    U4 u{};
+    const int sat = rast_saturated(dist, sc.sigma);
+    if (sat) return sat < 0 ? p.Sr : 0;
+    float e[4];
     for (int s = 0; s < p.Sr; ++s) {
       const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
-      if (s == 0 || (sg & 3u) == 0) u = philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast);
-      cnt += u01(word(u, sg & 3u)) >= c ? 1 : 0;
+      if (s == 0 || (sg & 3u) == 0) gauss4(philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast), e);
+      cnt += (D + sc.sigma * pick4(e, sg & 3u)) >= 0.f ? 1 : 0;
     }
   }
   return cnt;
 }
 
 // Count and the variance-reduced score sum_s ((m_s - vr) * eps_s) / sigma
-// (smoothrast.py:46,53).  Philox mode evaluates eps = Phi^-1(u) only where the
-// sample's decision differs from vr (the term is 0 otherwise).
+// (smoothrast.py:46,53).
 template <int NOISE>
 PR_DEV int rast_count_score(const PRBlendParams& p, const Sc& sc, float dist, uint32_t gp, int k, int64_t gs,
                             int64_t PK, float& gacc) {
@@ -121,17 +130,16 @@ PR_DEV int rast_count_score(const PRBlendParams& p, const Sc& sc, float dist, ui
       gacc += ((m - vr) * e) / sc.sigma;
     }
   } else {
-    const float c = rast_threshold(dist, sc.sigma);
-    if (c <= kULo) return p.Sr;  // all inside: m = vr = 1, no score
-    if (c > kUHi) return 0;      // all outside: m = vr = 0
-    U4 u{};
+    const int sat = rast_saturated(dist, sc.sigma);
+    if (sat) return sat < 0 ? p.Sr : 0;  // m_s = vr for every sample: no score
+    float e[4];
     for (int s = 0; s < p.Sr; ++s) {
       const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
-      if (s == 0 || (sg & 3u) == 0) u = philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast);
-      const float uu = u01(word(u, sg & 3u));
-      const float m = uu >= c ? 1.f : 0.f;
+      if (s == 0 || (sg & 3u) == 0) gauss4(philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast), e);
+      const float ee = pick4(e, sg & 3u);
+      const float m = heaviside1(D + sc.sigma * ee);
       cnt += (int)m;
-      if (m != vr) gacc += ((m - vr) * normcdfinvf(uu)) / sc.sigma;
+      gacc += ((m - vr) * ee) / sc.sigma;
     }
   }
   return cnt;
@@ -183,8 +191,20 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
     const float mf = m ? 1.f : 0.f;
     float prob;
     if constexpr (RAST) {
-      prob = m ? ((float)rast_count<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK) / (float)p.Sr) * mf
-               : 0.f;
+      if (a.rast_cache) {  // also keep the score mean for the backward (same arithmetic as its B1)
+        float gm = 0.f;
+        prob = 0.f;
+        if (m) {
+          float gacc;
+          const int cnt = rast_count_score<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK, gacc);
+          prob = ((float)cnt / (float)p.Sr) * mf;
+          gm = gacc / (float)p.Sr;
+        }
+        reinterpret_cast<float2*>(a.rast_cache)[gs] = make_float2(prob, gm);
+      } else {
+        prob = m ? ((float)rast_count<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK) / (float)p.Sr) * mf
+                 : 0.f;
+      }
     } else {
       prob = a.prob[gs];
     }
@@ -357,7 +377,11 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
       const float mf = m ? 1.f : 0.f;
       float prob, gm = 0.f;
       if constexpr (RAST) {
-        if (m) {
+        if (a.rast_cache) {
+          const float2 c = reinterpret_cast<const float2*>(a.rast_cache)[gs];
+          prob = c.x;
+          gm = c.y;
+        } else if (m) {
           float gacc;
           const int cnt = rast_count_score<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK, gacc);
           prob = ((float)cnt / (float)p.Sr) * mf;

@@ -68,13 +68,6 @@ PR_DEV U4 philox_block(uint64_t seed, uint32_t pixel, uint32_t slot, uint32_t gr
 // --------------------------------------------------------------------- math
 PR_DEV float heaviside1(float x) { return x >= 0.f ? 1.f : 0.f; }  // torch.heaviside(x, 1)
 
-// Rast threshold in Philox mode: the sample is "inside" iff D + sigma*eps >= 0
-// with eps = Phi^-1(u), i.e. iff u >= Phi(-D/sigma) = Phi(dist/sigma).
-PR_DEV float rast_threshold(float dist, float sigma) {
-  const float x = dist / sigma;
-  if (x != x) return 0.f;  // 0/0: D + sigma*eps = 0 -> H(0) = 1
-  return normcdff(x);
-}
 
 template <typename T>
 PR_DEV T ld(const T* p) { return *p; }

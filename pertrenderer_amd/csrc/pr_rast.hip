@@ -17,6 +17,8 @@
 // contributions in an LDS hash table keyed by face id before one global
 // atomic per (face, component), so hot faces shared by neighbouring pixels
 // do not serialise on global atomics.
+#include <type_traits>
+
 #include "pr_common.h"
 
 namespace pr {
@@ -80,11 +82,18 @@ PR_DEV float ndc(int i, int S1, int S2) {
   return -off + (range * (float)i + off) / (float)S1;
 }
 
-struct FaceRec {  // 64 B, staged through LDS
+// Per-face record for the forward traversal (96 B).  Besides the vertices it holds
+// the edge deltas and the (area + eps) that bary_fwd / seg_dist2 would compute:
+// the same IEEE operations on the same operands, so every per-pixel value below is
+// bit-identical to the straightforward formulas (and to oracle/rast_oracle.c).
+// Invalid faces get an empty bbox (+inf / -inf) so every cull rejects them.
+struct FaceRec {
   float4 a;  // v0.x v0.y v0.z v1.x
   float4 b;  // v1.y v1.z v2.x v2.y
   float4 c;  // v2.z xmin xmax ymin   (bbox grown by sqrt(blur))
-  float4 d;  // ymax valid - -
+  float4 d;  // ymax area+eps l2_01 l2_12
+  float4 e;  // D01.x D01.y D12.x D12.y   (D01 = v1 - v0, D12 = v2 - v1)
+  float4 f;  // D20.x D20.y l2_20 z_min   (D20 = v0 - v2)
 };
 
 __global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cull_backfaces, FaceRec* out) {
@@ -92,44 +101,92 @@ __global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cul
     const float* v = fv + f * 9;
     const float x0 = v[0], y0 = v[1], z0 = v[2], x1 = v[3], y1 = v[4], z1 = v[5], x2 = v[6], y2 = v[7], z2 = v[8];
     const float r = sqrtf(blur);
-    const float xmin = fminf(x0, fminf(x1, x2)) - r, xmax = fmaxf(x0, fmaxf(x1, x2)) + r;
-    const float ymin = fminf(y0, fminf(y1, y2)) - r, ymax = fmaxf(y0, fmaxf(y1, y2)) + r;
+    float xmin = fminf(x0, fminf(x1, x2)) - r, xmax = fmaxf(x0, fmaxf(x1, x2)) + r;
+    float ymin = fminf(y0, fminf(y1, y2)) - r, ymax = fmaxf(y0, fmaxf(y1, y2)) + r;
     const float zmax = fmaxf(z0, fmaxf(z1, z2));
     const float area = edge_fn(V2{x0, y0}, V2{x1, y1}, V2{x2, y2});
     const bool back = area < 0.f;
     const bool zero_area = area <= kEps && area >= -kEps;
     const bool valid = !(zmax < 0.f || (cull_backfaces && back) || zero_area);
+    if (!valid) { xmin = ymin = __builtin_inff(); xmax = ymax = -__builtin_inff(); }
+    const float d01x = x1 - x0, d01y = y1 - y0, d12x = x2 - x1, d12y = y2 - y1, d20x = x0 - x2, d20y = y0 - y2;
     FaceRec rec;
     rec.a = make_float4(x0, y0, z0, x1);
     rec.b = make_float4(y1, z1, x2, y2);
     rec.c = make_float4(z2, xmin, xmax, ymin);
-    rec.d = make_float4(ymax, valid ? 1.f : 0.f, 0.f, 0.f);
+    rec.d = make_float4(ymax, edge_fn(V2{x2, y2}, V2{x0, y0}, V2{x1, y1}) + kEps, d01x * d01x + d01y * d01y,
+                        d12x * d12x + d12y * d12y);
+    rec.e = make_float4(d01x, d01y, d12x, d12y);
+    rec.f = make_float4(d20x, d20y, d20x * d20x + d20y * d20y, fminf(z0, fminf(z1, z2)));
     out[f] = rec;
   }
 }
 
 PR_DEV bool key_less(float za, int fa, float zb, int fb) { return za < zb || (za == zb && fa < fb); }
 
-// full per-pixel test of one face; returns true and pz if the face is a candidate
-PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, bool persp, bool clip, float& pz) {
-  if (p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x) return false;
-  const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
-  const float z0 = r.a.z, z1 = r.b.y, z2 = r.c.x;
-  float b0[3], b[3], bc[3];
-  bary_fwd(p, v0, v1, v2, b0);
-  if (persp) persp_fwd(b0, z0, z1, z2, b); else { b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; }
-  if (clip) clip_fwd(b, bc); else { bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2]; }
-  pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
-  if (pz < 0.f) return false;
-  const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
-  if (inside) return true;
-  const float d = tri_dist2(p, v0, v1, v2);
-  return d < blur;
+// seg_dist2 with the segment delta (b - a) and its squared length precomputed
+PR_DEV float seg_dist2_d(V2 p, V2 a, float bax, float bay, float l2, V2 b) {
+  if (l2 <= kEps) {
+    const float dx = p.x - b.x, dy = p.y - b.y;
+    return dx * dx + dy * dy;
+  }
+  float t = (bax * (p.x - a.x) + bay * (p.y - a.y)) / l2;
+  t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+  const float qx = a.x + t * bax, qy = a.y + t * bay;
+  const float dx = p.x - qx, dy = p.y - qy;
+  return dx * dx + dy * dy;
 }
 
-constexpr int kCap = 256;  // per-round tile face list (faces beyond it are handled in later rounds)
+// Full per-pixel test of one face, branch-free so that several faces' division
+// chains interleave (one wave per SIMD: ILP is the latency hiding).  Same decisions
+// as PyTorch3D's per-face body: in bbox -> bary -> perspective -> clip -> pz >= 0 ->
+// inside or dist < blur.  `persp` / `clip` / the degenerate-edge tests are uniform.
+PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, bool persp, bool clip, float& pz) {
+  const bool inbox = !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
+  const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
+  const float z0 = r.a.z, z1 = r.b.y, z2 = r.c.x;
+  const float area = r.d.y;
+  // edge functions E(p,v1,v2), E(p,v2,v0), E(p,v0,v1) with the precomputed deltas
+  const float e0 = (p.x - v1.x) * r.e.w - (p.y - v1.y) * r.e.z;
+  const float e1 = (p.x - v2.x) * r.f.y - (p.y - v2.y) * r.f.x;
+  const float e2 = (p.x - v0.x) * r.e.y - (p.y - v0.y) * r.e.x;
+  float b[3] = {e0 / area, e1 / area, e2 / area};
+  if (persp) {
+    const float t0 = b[0] * z1 * z2, t1 = z0 * b[1] * z2, t2 = z0 * z1 * b[2];
+    float d = t0 + t1 + t2;
+    d = d > kEps ? d : kEps;
+    b[0] = t0 / d; b[1] = t1 / d; b[2] = t2 / d;
+  }
+  if (clip) {
+    float bc[3];
+    clip_fwd(b, bc);
+    pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
+  } else {
+    pz = b[0] * z0 + b[1] * z1 + b[2] * z2;
+  }
+  const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
+  const float d01 = seg_dist2_d(p, v0, r.e.x, r.e.y, r.d.z, v1);
+  const float d02 = seg_dist2_d(p, v0, -r.f.x, -r.f.y, r.f.z, v2);
+  const float d12 = seg_dist2_d(p, v1, r.e.z, r.e.w, r.d.w, v2);
+  float d = d01 < d02 ? d01 : d02;
+  d = d < d12 ? d : d12;
+  return inbox && !(pz < 0.f) && (inside || d < blur);
+}
 
-PR_DEV float zmin3(const FaceRec& r) { return fminf(r.a.z, fminf(r.b.y, r.c.x)); }
+PR_DEV bool in_bbox(const FaceRec& r, V2 p) {
+  return !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
+}
+
+#ifdef PR_RAST_PROFILE
+#define PR_STAMP(i) (stamp[i] += (long long)__builtin_amdgcn_s_memtime() - t_, t_ = __builtin_amdgcn_s_memtime())
+#else
+#define PR_STAMP(i) ((void)0)
+#endif
+
+constexpr int kCap = 512;    // per-round tile face list (faces beyond it are handled in later rounds)
+static_assert(kCap <= 8 * 64, "suffix-min pass holds kCap / 64 <= 8 entries per lane");
+constexpr int kCullU = 4;    // 64-face cull chunks whose loads are in flight together
+constexpr int kGroup = 4;    // faces tested together (independent chains)
 
 // Bitonic sort (ascending key) of n2 (power of two) LDS entries by one wave.
 PR_DEV void bitonic_sort(float* key, int* val, int n2, int lane) {
@@ -151,13 +208,25 @@ PR_DEV void bitonic_sort(float* key, int* val, int n2, int lane) {
   }
 }
 
+// Forward, pass 1: per-pixel K nearest (z, face) keys -> pix_to_face, zbuf.
+// One wave per 8x8 tile, one lane per pixel.  Per round: cull the mesh's faces
+// against the tile (ballot compaction into LDS, kCullU chunks of loads in flight),
+// bitonic-sort the survivors by z_min, then walk them in 64-face chunks staged in
+// LDS; the wave tests kGroup faces at once (broadcast LDS reads, independent
+// chains) and inserts the candidates in order.  The lane's K-queue is an LDS
+// column sorted by (z, face id), exactly PyTorch3D's order (the final queue is the
+// K smallest keys, independent of insertion order).  Barycentrics / distances of
+// the winners come from rast_frag_kernel, fully parallel over slots.
 __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces) {
   extern __shared__ float smem[];
   const int K = a.K;
-  float2* q = reinterpret_cast<float2*>(smem);             // [K][64] (z, face id bits), sorted per lane
-  int* lfid = reinterpret_cast<int*>(q + K * 64);           // [kCap] tile face list
-  float* lkey = reinterpret_cast<float*>(lfid + kCap);      // [kCap] its z_min (sort key)
-  int* qsz = reinterpret_cast<int*>(lkey + kCap);           // [64] queue sizes
+  FaceRec* lrec = reinterpret_cast<FaceRec*>(smem);          // [64] staged face records of a chunk
+  float2* q = reinterpret_cast<float2*>(lrec + 64);          // [K][64] (z, face id bits), sorted per lane
+  int* lfid = reinterpret_cast<int*>(q + K * 64);            // [kCap] tile face list (cull order)
+  float* lkey = reinterpret_cast<float*>(lfid + kCap);       // [kCap] sort key (depth near the tile centre),
+  float* lsuf = lkey;                                        //   then suffix min of z_min in sorted order
+  int* lidx = reinterpret_cast<int*>(lkey + kCap);           // [kCap] sorted -> cull order
+  int* qsz = lidx + kCap;                                    // [64] queue sizes
   const int lane = threadIdx.x;
   const int n = blockIdx.z;
   const int H = a.H, W = a.W;
@@ -169,74 +238,202 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
   const int c1 = min(col0 + kTile - 1, W - 1), r1 = min(row0 + kTile - 1, H - 1);
   const float txmax = ndc(W - 1 - col0, W, H), txmin = ndc(W - 1 - c1, W, H);
   const float tymax = ndc(H - 1 - row0, H, W), tymin = ndc(H - 1 - r1, H, W);
+  const float tcx = 0.5f * (txmin + txmax), tcy = 0.5f * (tymin + tymax);
   const int64_t fb = a.mesh_first_face[n], fe = fb + a.mesh_num_faces[n];
   const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
+  const float blur = a.blur_radius;
   int qs = 0;
   float qlast_z = __builtin_inff();
   int qlast_f = 0x7fffffff;
-  bool done = !inimg;
   int64_t base = fb;
+#ifdef PR_RAST_PROFILE
+  long long stamp[7] = {0, 0, 0, 0, 0, 0, 0}, t_ = __builtin_amdgcn_s_memtime(), u_ = 0;
+  int ntest = 0, nins = 0, nlist = 0;
+#endif
   while (base < fe) {
     // ---- gather this round's culled faces (expanded bbox overlaps the tile)
     int nl = 0;
-    while (base < fe && nl <= kCap - 64) {
-      const int64_t f = base + lane;
-      bool keep = false;
-      float zk = 0.f;
-      if (f < fe) {
-        const FaceRec r = faces[f];
-        keep = r.d.y != 0.f && !(r.c.y > txmax || r.c.z < txmin || r.c.w > tymax || r.d.x < tymin);
-        zk = zmin3(r);
+    while (base < fe && nl <= kCap - 64 * kCullU) {
+      float4 cc[kCullU], dd[kCullU];
+#pragma unroll
+      for (int u = 0; u < kCullU; ++u) {
+        const int64_t f = base + u * 64 + lane;
+        const int64_t fl = f < fe ? f : fe - 1;
+        cc[u] = faces[fl].c; dd[u] = faces[fl].d;
       }
-      const uint64_t bal = __ballot(keep);
-      if (keep) {
-        const int idx = nl + __popcll(bal & ((1ull << lane) - 1ull));
-        lfid[idx] = (int)f;
-        lkey[idx] = zk;
+#pragma unroll
+      for (int u = 0; u < kCullU; ++u) {
+        const int64_t f = base + u * 64 + lane;
+        const bool keep = f < fe && !(cc[u].y > txmax || cc[u].z < txmin || cc[u].w > tymax || dd[u].x < tymin);
+        const uint64_t bal = __ballot(keep);
+        if (keep) lfid[nl + __popcll(bal & ((1ull << lane) - 1ull))] = (int)f;
+        nl += __popcll(bal);
       }
-      nl += __popcll(bal);
-      base += 64;
+      base += 64 * kCullU;
     }
+    PR_STAMP(0);
+#ifdef PR_RAST_PROFILE
+    nlist += nl;
+#endif
     if (nl == 0) continue;
-    done = !inimg;  // the early exit below is only valid inside one z-sorted round
-    // ---- sort by z_min: near faces first, so inserts are mostly appends and lanes
-    //      whose K-queue is full can stop early (pz >= z_min when barycentrics are clipped)
+    bool done = !inimg;  // the early exit below is only valid inside one sorted round
+    // ---- sort key: the face plane's depth at the tile centre, clamped to the face's
+    //      z range (an ordering heuristic only: it makes the per-pixel inserts mostly
+    //      appends).  Exactness does not depend on it; the early exit uses z_min.
     int n2 = 1;
     while (n2 < nl) n2 <<= 1;
-    for (int i = nl + lane; i < n2; i += 64) { lkey[i] = __builtin_inff(); lfid[i] = 0x7fffffff; }
     __syncthreads();
-    bitonic_sort(lkey, lfid, n2, lane);
-    for (int i = 0; i < nl; ++i) {
-      const float zk = lkey[i];
-      // clipped barycentrics make pz a convex combination of the vertex depths, so
-      // pz >= z_min (up to rounding: keep a 1e-6 relative margin)
-      if (clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
-      if (__ballot(!done) == 0) break;
-      if (done) continue;
-      const int fid = __builtin_amdgcn_readfirstlane(lfid[i]);
-      const FaceRec rr = faces[fid];
-      float pz;
-      if (!face_test(rr, p, a.blur_radius, persp, clip, pz)) continue;
-      if (qs == K && !key_less(pz, fid, qlast_z, qlast_f)) continue;
-      int pos = qs < K ? qs : K - 1;
-      if (qs < K) ++qs;
-      while (pos > 0) {
-        const float2 prev = q[(pos - 1) * 64 + lane];
-        if (!key_less(pz, fid, prev.x, __float_as_int(prev.y))) break;
-        q[pos * 64 + lane] = prev;
-        --pos;
+    for (int i = lane; i < n2; i += 64) {
+      float key = __builtin_inff();
+      if (i < nl) {
+        const FaceRec& r = faces[lfid[i]];
+        const float4 ra = r.a, rb = r.b, re = r.e, rf = r.f;
+        const float z2 = r.c.x, area = r.d.y;
+        const float e0 = (tcx - ra.w) * re.w - (tcy - rb.x) * re.z;
+        const float e1 = (tcx - rb.z) * rf.y - (tcy - rb.w) * rf.x;
+        const float e2 = (tcx - ra.x) * re.y - (tcy - ra.y) * re.x;
+        const float ia = 1.f / area;
+        const float zc = (e0 * ia) * ra.z + (e1 * ia) * rb.y + (e2 * ia) * z2;
+        const float zmx = fmaxf(ra.z, fmaxf(rb.y, z2));
+        key = fminf(fmaxf(zc, rf.w), zmx);
+        if (key != key) key = rf.w;
+        key = fminf(key, 3.0e38f);  // real faces sort before the +inf padding
+        if (key != key) key = 0.f;
       }
-      q[pos * 64 + lane] = make_float2(pz, __int_as_float(fid));
-      if (qs == K) {
-        const float2 last = q[(K - 1) * 64 + lane];
-        qlast_z = last.x;
-        qlast_f = __float_as_int(last.y);
+      lkey[i] = key;
+      lidx[i] = i < nl ? i : 0x7fffffff;
+    }
+    __syncthreads();
+    bitonic_sort(lkey, lidx, n2, lane);
+    // suffix minimum of z_min along the sorted order (faces after position i cannot
+    // produce pz below lsuf[i] when barycentrics are clipped)
+    {
+      const int per = (nl + 63) / 64;  // contiguous run of sorted positions per lane
+      const int i0 = lane * per, i1 = min(nl, i0 + per);
+      float zl[8];  // z_min of this lane's run (per <= kCap / 64)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) zl[u] = i0 + u < i1 ? faces[lfid[lidx[i0 + u]]].f.w : __builtin_inff();
+      float m = __builtin_inff();
+#pragma unroll
+      for (int u = 0; u < 8; ++u) m = fminf(m, zl[u]);
+      // exclusive suffix-min across lanes (lanes above this one)
+      float ex = m;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_down(ex, o);
+        if (lane + o < 64) ex = fminf(ex, t);
+      }
+      float run = __shfl_down(ex, 1);
+      if (lane == 63) run = __builtin_inff();
+      __syncthreads();  // lsuf aliases lkey: every lane is past its sorted reads
+#pragma unroll
+      for (int u = 7; u >= 0; --u) {
+        run = fminf(run, zl[u]);
+        if (i0 + u < i1) lsuf[i0 + u] = run;
       }
     }
     __syncthreads();
+    PR_STAMP(1);
+    for (int c0 = 0; c0 < nl && __ballot(!done) != 0; c0 += 64) {
+      const int cnt = min(64, nl - c0);
+      __syncthreads();
+      // lane i holds chunk entry i's face id and suffix-min z (read back with readlane)
+      const int cfid = lfid[lidx[c0 + min(lane, cnt - 1)]];
+      const float csuf = lsuf[c0 + min(lane, cnt - 1)];
+      if (lane < cnt) lrec[lane] = faces[cfid];
+      __syncthreads();
+      for (int t = 0; t < cnt; t += kGroup) {
+        bool cand[kGroup];
+        float pzv[kGroup];
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+          const int tt = min(t + j, cnt - 1);
+          any |= t + j < cnt && __ballot(in_bbox(lrec[tt], p)) != 0;
+        }
+        if (!any) continue;
+#ifdef PR_RAST_PROFILE
+        u_ = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+          const int tt = min(t + j, cnt - 1);
+          const FaceRec rr = lrec[tt];
+          cand[j] = face_test(rr, p, blur, persp, clip, pzv[j]) && t + j < cnt;
+        }
+#ifdef PR_RAST_PROFILE
+        if (__ballot(cand[0] || cand[1] || cand[2] || cand[3]) == ~0ull) stamp[6] += 0;
+        stamp[5] += __builtin_amdgcn_s_memtime() - u_;
+        u_ = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+          if (t + j >= cnt) break;
+          // clipped barycentrics make pz a convex combination of the vertex depths, so
+          // pz >= z_min for this and every later face (up to rounding: 1e-6 margin)
+          const float zk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, csuf), t + j));
+          if (clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
+          if (done || !cand[j]) continue;
+          const int fid = __builtin_amdgcn_readlane(cfid, t + j);
+          const float pz = pzv[j];
+#ifdef PR_RAST_PROFILE
+          ++nins;
+#endif
+          // (qlast_z, qlast_f) = the queue's last (largest) key, kept in registers
+          if (qs == K && !key_less(pz, fid, qlast_z, qlast_f)) continue;
+          if (qs == 0 || key_less(qlast_z, qlast_f, pz, fid)) {
+            // append (the common case: faces arrive roughly in depth order)
+            if (qs < K) {
+              q[qs * 64 + lane] = make_float2(pz, __int_as_float(fid));
+              ++qs;
+            } else {
+              q[(K - 1) * 64 + lane] = make_float2(pz, __int_as_float(fid));
+            }
+            qlast_z = pz;
+            qlast_f = fid;
+            continue;
+          }
+          int pos = qs < K ? qs : K - 1;
+          if (qs < K) ++qs;
+          // shift the entries greater than the key up by one, reading up to four of
+          // them per LDS round trip
+          while (pos > 0) {
+            float2 e[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) e[i] = q[max(pos - 1 - i, 0) * 64 + lane];
+            int sh = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if (sh == i && pos - 1 - i >= 0 && key_less(pz, fid, e[i].x, __float_as_int(e[i].y))) {
+                q[(pos - i) * 64 + lane] = e[i];
+                sh = i + 1;
+              }
+            }
+            pos -= sh;
+            if (sh < 4) break;
+          }
+          q[pos * 64 + lane] = make_float2(pz, __int_as_float(fid));
+          {
+            const float2 last = q[(qs - 1) * 64 + lane];
+            qlast_z = last.x;
+            qlast_f = __float_as_int(last.y);
+          }
+        }
+#ifdef PR_RAST_PROFILE
+        ntest += kGroup;
+        stamp[6] += __builtin_amdgcn_s_memtime() - u_;
+#endif
+        if (__ballot(!done) == 0) break;
+      }
+    }
+    __syncthreads();
+    PR_STAMP(2);
   }
   qsz[lane] = inimg ? qs : 0;
   __syncthreads();
+#ifdef PR_RAST_PROFILE
+  PR_STAMP(3);
+#endif
   // ---- coalesced output: each tile row's 8 pixels own a contiguous 8*K slot range
   const int q64 = 64 / K, r64 = 64 % K;
   for (int r = 0; r < kTile; ++r) {
@@ -245,38 +442,52 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
     const int ncols = min(kTile, W - col0);
     const int total = ncols * K;
     const int64_t obase = (((int64_t)n * H + prow) * W + col0) * K;
-    const float py = ndc(H - 1 - prow, H, W);
     for (int i = lane, c = lane / K, k = lane - (lane / K) * K; i < total;
          i += 64, c += q64, k += r64, (k >= K ? (k -= K, ++c) : 0)) {
       const int tl = r * kTile + c;
       const int64_t o = obase + i;
-      if (k < qsz[tl]) {
-        const float2 e = q[k * 64 + tl];
-        const int fid = __float_as_int(e.y);
-        const V2 pp{ndc(W - 1 - (col0 + c), W, H), py};
-        const float* v = a.face_verts + (int64_t)fid * 9;
-        const V2 v0{v[0], v[1]}, v1{v[3], v[4]}, v2{v[6], v[7]};
-        float b0[3], b[3], bc[3];
-        bary_fwd(pp, v0, v1, v2, b0);
-        if (persp) persp_fwd(b0, v[2], v[5], v[8], b); else { b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; }
-        if (clip) clip_fwd(b, bc); else { bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2]; }
-        const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
-        const float d = tri_dist2(pp, v0, v1, v2);
-        a.pix_to_face[o] = fid;
-        a.zbuf[o] = e.x;
-        a.dists[o] = inside ? -d : d;
-        a.bary[o * 3 + 0] = bc[0];
-        a.bary[o * 3 + 1] = bc[1];
-        a.bary[o * 3 + 2] = bc[2];
-      } else {
-        a.pix_to_face[o] = -1;
-        a.zbuf[o] = -1.f;
-        a.dists[o] = -1.f;
-        a.bary[o * 3 + 0] = -1.f;
-        a.bary[o * 3 + 1] = -1.f;
-        a.bary[o * 3 + 2] = -1.f;
-      }
+      const float2 e = q[k * 64 + tl];  // read with the size (stale beyond it, unused)
+      const bool valid = k < qsz[tl];
+      a.pix_to_face[o] = valid ? (int64_t)__float_as_int(e.y) : (int64_t)-1;
+      a.zbuf[o] = valid ? e.x : -1.f;
     }
+  }
+#ifdef PR_RAST_PROFILE
+  PR_STAMP(4);
+  if (lane == 0 && nlist >= 90)
+    printf("tile %d,%d list %d tests(lane0) %d ins %d | cull %lld sort %lld test %lld tail %lld out %lld | tcomp %lld tins %lld\n",
+           blockIdx.x, blockIdx.y, nlist, ntest, nins, stamp[0], stamp[1], stamp[2], stamp[3], stamp[4], stamp[5], stamp[6]);
+#endif
+}
+
+// Forward, pass 2: barycentrics (perspective-corrected, clipped) and signed squared
+// distances of every slot, one lane per slot.
+template <bool WIDE>
+__global__ void __launch_bounds__(kThreads) rast_frag_kernel(PRRastArgs a, int64_t total) {
+  using idx_t = typename std::conditional<WIDE, int64_t, uint32_t>::type;
+  const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
+  for (int64_t oo = (int64_t)blockIdx.x * kThreads + threadIdx.x; oo < total; oo += (int64_t)gridDim.x * kThreads) {
+    const idx_t o = (idx_t)oo;
+    const int64_t fid = a.pix_to_face[o];
+    float bc[3] = {-1.f, -1.f, -1.f}, dist = -1.f;
+    if (fid >= 0) {
+      const idx_t pix = o / (idx_t)a.K;
+      const int col = (int)(pix % (idx_t)a.W), row = (int)((pix / (idx_t)a.W) % (idx_t)a.H);
+      const V2 pp{ndc(a.W - 1 - col, a.W, a.H), ndc(a.H - 1 - row, a.H, a.W)};
+      const float* v = a.face_verts + fid * 9;
+      const V2 v0{v[0], v[1]}, v1{v[3], v[4]}, v2{v[6], v[7]};
+      float b0[3], b[3];
+      bary_fwd(pp, v0, v1, v2, b0);
+      if (persp) persp_fwd(b0, v[2], v[5], v[8], b); else { b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; }
+      if (clip) clip_fwd(b, bc); else { bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2]; }
+      const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
+      const float d = tri_dist2(pp, v0, v1, v2);
+      dist = inside ? -d : d;
+    }
+    a.dists[o] = dist;
+    a.bary[o * 3 + 0] = bc[0];
+    a.bary[o * 3 + 1] = bc[1];
+    a.bary[o * 3 + 2] = bc[2];
   }
 }
 
@@ -585,9 +796,15 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
     if (int e = check_launch("rast_face_prep")) return e;
   }
   dim3 grid((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, a.N);
-  const size_t lds = (size_t)a.K * 64 * 8 + kCap * 8 + 64 * 4;
+  const size_t lds = 64 * sizeof(FaceRec) + (size_t)a.K * 64 * 8 + kCap * 12 + 64 * 4;
+  if (lds > 160 * 1024) return set_error(PR_ERR_ARG, "rast_fwd: faces_per_pixel too large for the LDS queue (max 300)");
   rast_fwd_kernel<<<grid, 64, lds, st>>>(a, fr);
-  return check_launch("rast_fwd");
+  if (int e = check_launch("rast_fwd")) return e;
+  const int64_t total = (int64_t)a.N * a.H * a.W * a.K;
+  const int nb = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 1 << 20);
+  if (total * 3 < (int64_t(1) << 32)) rast_frag_kernel<false><<<nb, kThreads, 0, st>>>(a, total);
+  else rast_frag_kernel<true><<<nb, kThreads, 0, st>>>(a, total);
+  return check_launch("rast_frag");
 }
 
 extern "C" size_t pr_rast_bwd_workspace_size(const PRRastArgs*) { return 0; }

@@ -135,9 +135,9 @@ def test_interpolation_matches_oracle_and_backward(device):
     assert_close(a.grad, ac.grad, rtol=1e-4, atol_rel=1e-5, name="grad_attr")
 
 
-@pytest.mark.parametrize("size,K,dist_cam", [(64, 50, 2.7), (24, 16, 2.7), (40, 8, 6.7)])
+@pytest.mark.parametrize("size,K,dist_cam", [(64, 50, 2.7), (24, 16, 2.7), (40, 8, 6.7), (16, 150, 2.7)])
 def test_mesh_rasterizer_sphere_matches_oracle(size, K, dist_cam, device):
-    """Includes tiles whose culled face list exceeds one 256-face round (small images)."""
+    """Includes tiles whose culled face list exceeds one 512-face round (small images) and K=150 (cfg 4)."""
     verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
     mesh = Meshes([verts.to(device)], [faces.verts_idx.to(device)])
     R, T = look_at_view_transform(dist_cam, 30.0, 120.0, device=device)
@@ -155,4 +155,4 @@ def test_mesh_rasterizer_sphere_matches_oracle(size, K, dist_cam, device):
     np.testing.assert_array_equal(frag.zbuf.cpu().numpy(), rz)
     np.testing.assert_array_equal(frag.dists.cpu().numpy(), rd)
     np.testing.assert_array_equal(frag.bary_coords.cpu().numpy(), rb)
-    assert (rp >= 0).sum(-1).max() == K  # the blur radius fills all K slots somewhere
+    assert (rp >= 0).sum(-1).max() == min(K, 56)  # the blur radius fills all K slots somewhere (<= 56 here)

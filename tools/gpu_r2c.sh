@@ -1,0 +1,8 @@
+set -u
+R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out"; mkdir -p "$OUT"; TAG="${1:-r2c}"
+cd "$R"
+PR_NATIVE_LIB=$R/pertrenderer_amd/libpertrender_prof.so timeout -k 10 120 python tools/rast_prof.py > "$OUT/rast_prof_$TAG.log" 2>&1
+rc=$?; echo "rast_prof rc=$rc"; sort -t'|' -k2 "$OUT/rast_prof_$TAG.log" | tail -6
+[ $rc -ne 0 ] && exit $rc
+bash tools/gpu_quick.sh $TAG || exit $?
+bash tools/gpu_ktrace.sh kt_$TAG
