@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 3
+#define PR_ABI_VERSION 4
 
 /* error codes */
 #define PR_OK 0
@@ -182,6 +182,35 @@ typedef struct PRProjectArgs {
 
 int pr_project_fwd(const PRProjectArgs* args, void* stream);
 int pr_project_bwd(const PRProjectArgs* args, void* stream);
+
+/* Pose of the pose-optimisation loop (experiments/eval.py:343-346; PyTorch3D 0.4.0
+ * so3_exponential_map and Rotate(R).transform_points):
+ *   R[n] = I + sin(t)/t hat(w) + (1-cos t)/t^2 hat(w)^2,  t = sqrt(max(|w|^2, eps))
+ *   out[n,p] = points[n,p] @ R[n or 0]                   (row-vector convention)   */
+typedef struct PRSO3Args {
+  int32_t N;
+  float eps;
+  const float* log_rot;        /* (N,3) */
+  float* R;                    /* fwd out (N,3,3) */
+  const float* grad_R;         /* bwd in (N,3,3) */
+  float* grad_log_rot;         /* bwd out (N,3) */
+} PRSO3Args;
+
+typedef struct PRRotateArgs {
+  int32_t N, P;                /* point batches x points per batch */
+  int32_t R_batched;           /* 1: R is (N,3,3); 0: one (3,3) shared by every batch */
+  const float* points;         /* (N,P,3) */
+  const float* R;
+  float* out;                  /* fwd out (N,P,3) */
+  const float* grad_out;       /* bwd in (N,P,3) */
+  float* grad_points;          /* bwd out (N,P,3), nullable */
+  float* grad_R;               /* bwd out, R's shape, nullable (deterministic block reduction) */
+} PRRotateArgs;
+
+int pr_so3_exp_fwd(const PRSO3Args* args, void* stream);
+int pr_so3_exp_bwd(const PRSO3Args* args, void* stream);
+int pr_rotate_fwd(const PRRotateArgs* args, void* stream);
+int pr_rotate_bwd(const PRRotateArgs* args, void* stream);
 
 int pr_abi_version(void);
 const char* pr_last_error(void);

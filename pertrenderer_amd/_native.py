@@ -76,6 +76,16 @@ class PRProjectArgs(C.Structure):
                 ("face_verts", _vp), ("grad_face_verts", _vp), ("grad_verts", _vp)]
 
 
+class PRSO3Args(C.Structure):
+    _fields_ = [("N", C.c_int32), ("eps", C.c_float), ("log_rot", _vp), ("R", _vp), ("grad_R", _vp),
+                ("grad_log_rot", _vp)]
+
+
+class PRRotateArgs(C.Structure):
+    _fields_ = [("N", C.c_int32), ("P", C.c_int32), ("R_batched", C.c_int32), ("points", _vp), ("R", _vp),
+                ("out", _vp), ("grad_out", _vp), ("grad_points", _vp), ("grad_R", _vp)]
+
+
 # every symbol include/pertrender.h declares, with its argument struct (None = no args)
 EXPORTS = {
     "pr_abi_version": (C.c_int, []),
@@ -95,8 +105,12 @@ EXPORTS = {
     "pr_seed_advance": (C.c_int, [_vp, C.c_int32, _vp]),
     "pr_project_fwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
     "pr_project_bwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
+    "pr_so3_exp_fwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
+    "pr_so3_exp_bwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
+    "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
+    "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
 }
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 

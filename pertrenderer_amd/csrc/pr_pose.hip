@@ -1,0 +1,168 @@
+// Pose ops of the pose-optimisation loop: SO(3) exponential map and the row-vector
+// rotation of a point set, forward and backward (PyTorch3D 0.4.0 so3_exponential_map
+// and Rotate.transform_points as used at experiments/eval.py:343-346).
+//
+// They are tiny (one 3-vector, a few thousand points), so the point of a native op
+// is launch count: the torch composition is ~60 kernels per fwd+bwd step (hat
+// assembly, bmm, elementwise, their autograd), each a separate graph node.  Here it
+// is one kernel per direction; the R-gradient reduction is a fixed-order block
+// reduction (deterministic).
+#include "pr_common.h"
+
+namespace pr {
+namespace {
+
+PR_DEV void hat3(const float w[3], float S[9]) {
+  S[0] = 0.f;   S[1] = -w[2]; S[2] = w[1];
+  S[3] = w[2];  S[4] = 0.f;   S[5] = -w[0];
+  S[6] = -w[1]; S[7] = w[0];  S[8] = 0.f;
+}
+
+PR_DEV void mm3(const float A[9], const float B[9], float C[9]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) C[i * 3 + j] = (A[i * 3] * B[j] + A[i * 3 + 1] * B[3 + j]) + A[i * 3 + 2] * B[6 + j];
+}
+
+struct SO3Fac {
+  float nrms, angle, inv, sn, cs, fac1, fac2;
+};
+
+PR_DEV SO3Fac so3_fac(const float w[3], float eps) {
+  SO3Fac f;
+  f.nrms = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
+  f.angle = sqrtf(f.nrms > eps ? f.nrms : eps);
+  f.inv = 1.f / f.angle;
+  f.sn = sinf(f.angle);
+  f.cs = cosf(f.angle);
+  f.fac1 = f.inv * f.sn;
+  f.fac2 = f.inv * f.inv * (1.f - f.cs);
+  return f;
+}
+
+__global__ void so3_exp_fwd_kernel(PRSO3Args a) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= a.N) return;
+  const float w[3] = {a.log_rot[n * 3], a.log_rot[n * 3 + 1], a.log_rot[n * 3 + 2]};
+  const SO3Fac f = so3_fac(w, a.eps);
+  float S[9], S2[9];
+  hat3(w, S);
+  mm3(S, S, S2);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) a.R[n * 9 + i] = (f.fac1 * S[i] + f.fac2 * S2[i]) + ((i % 4) == 0 ? 1.f : 0.f);
+}
+
+// autograd of the forward expression, term by term
+__global__ void so3_exp_bwd_kernel(PRSO3Args a) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= a.N) return;
+  const float w[3] = {a.log_rot[n * 3], a.log_rot[n * 3 + 1], a.log_rot[n * 3 + 2]};
+  const SO3Fac f = so3_fac(w, a.eps);
+  float S[9], S2[9], G[9];
+  hat3(w, S);
+  mm3(S, S, S2);
+  for (int i = 0; i < 9; ++i) G[i] = a.grad_R[n * 9 + i];
+  float dfac1 = 0.f, dfac2 = 0.f;
+  for (int i = 0; i < 9; ++i) { dfac1 += G[i] * S[i]; dfac2 += G[i] * S2[i]; }
+  // S2 = S @ S: dS = G2 S^T + S^T G2 with G2 = fac2 * G
+  float G2[9], St[9], A[9], B[9], dS[9];
+  for (int i = 0; i < 9; ++i) G2[i] = f.fac2 * G[i];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) St[i * 3 + j] = S[j * 3 + i];
+  mm3(G2, St, A);
+  mm3(St, G2, B);
+  for (int i = 0; i < 9; ++i) dS[i] = f.fac1 * G[i] + (A[i] + B[i]);
+  const float dinv = dfac1 * f.sn + dfac2 * (2.f * f.inv * (1.f - f.cs));
+  const float dang = dfac1 * f.inv * f.cs + dfac2 * f.inv * f.inv * f.sn - dinv * f.inv * f.inv;
+  const float dc = dang * 0.5f / f.angle;
+  const float dn = f.nrms >= a.eps ? dc : 0.f;  // clamp(min=eps) passes the gradient where nrms >= eps
+  a.grad_log_rot[n * 3 + 0] = 2.f * w[0] * dn + (dS[7] - dS[5]);
+  a.grad_log_rot[n * 3 + 1] = 2.f * w[1] * dn + (dS[2] - dS[6]);
+  a.grad_log_rot[n * 3 + 2] = 2.f * w[2] * dn + (dS[3] - dS[1]);
+}
+
+__global__ void __launch_bounds__(kThreads) rotate_fwd_kernel(PRRotateArgs a) {
+  const int64_t total = (int64_t)a.N * a.P;
+  for (int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x; t < total; t += (int64_t)gridDim.x * kThreads) {
+    const int n = (int)(t / a.P);
+    const float* R = a.R + (a.R_batched ? n * 9 : 0);
+    const float x = a.points[t * 3], y = a.points[t * 3 + 1], z = a.points[t * 3 + 2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) a.out[t * 3 + j] = (x * R[j] + y * R[3 + j]) + z * R[6 + j];
+  }
+}
+
+// One workgroup per R (per batch if R_batched, else one for all): d R = sum_p p^T g,
+// reduced in a fixed order; d points = g @ R^T alongside.
+__global__ void __launch_bounds__(kThreads) rotate_bwd_kernel(PRRotateArgs a) {
+  __shared__ float red[kThreads * 9];
+  const int tid = threadIdx.x;
+  const int r = blockIdx.x;
+  const int n0 = a.R_batched ? r : 0, n1 = a.R_batched ? r + 1 : a.N;
+  const float* R = a.R + (a.R_batched ? r * 9 : 0);
+  float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t lo = (int64_t)n0 * a.P, hi = (int64_t)n1 * a.P;
+  for (int64_t t = lo + tid; t < hi; t += kThreads) {
+    const float x = a.points[t * 3], y = a.points[t * 3 + 1], z = a.points[t * 3 + 2];
+    const float g0 = a.grad_out[t * 3], g1 = a.grad_out[t * 3 + 1], g2 = a.grad_out[t * 3 + 2];
+    if (a.grad_R) {
+      acc[0] += x * g0; acc[1] += x * g1; acc[2] += x * g2;
+      acc[3] += y * g0; acc[4] += y * g1; acc[5] += y * g2;
+      acc[6] += z * g0; acc[7] += z * g1; acc[8] += z * g2;
+    }
+    if (a.grad_points) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) a.grad_points[t * 3 + i] = (g0 * R[i * 3] + g1 * R[i * 3 + 1]) + g2 * R[i * 3 + 2];
+    }
+  }
+  if (!a.grad_R) return;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) red[i * kThreads + tid] = acc[i];
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) red[i * kThreads + tid] += red[i * kThreads + tid + s];
+    }
+    __syncthreads();
+  }
+  if (tid < 9) a.grad_R[r * 9 + tid] = red[tid * kThreads];
+}
+
+}  // namespace
+}  // namespace pr
+
+using namespace pr;
+
+extern "C" int pr_so3_exp_fwd(const PRSO3Args* a, void* stream) {
+  if (!a || a->N < 0 || (a->N > 0 && (!a->log_rot || !a->R))) return set_error(PR_ERR_ARG, "so3_exp_fwd: bad args");
+  if (a->N == 0) return PR_OK;
+  so3_exp_fwd_kernel<<<(a->N + 63) / 64, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(*a);
+  return check_launch("so3_exp_fwd");
+}
+
+extern "C" int pr_so3_exp_bwd(const PRSO3Args* a, void* stream) {
+  if (!a || a->N < 0 || (a->N > 0 && (!a->log_rot || !a->grad_R || !a->grad_log_rot)))
+    return set_error(PR_ERR_ARG, "so3_exp_bwd: bad args");
+  if (a->N == 0) return PR_OK;
+  so3_exp_bwd_kernel<<<(a->N + 63) / 64, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(*a);
+  return check_launch("so3_exp_bwd");
+}
+
+extern "C" int pr_rotate_fwd(const PRRotateArgs* a, void* stream) {
+  if (!a || a->N < 0 || a->P < 0 || !a->R || ((int64_t)a->N * a->P > 0 && (!a->points || !a->out)))
+    return set_error(PR_ERR_ARG, "rotate_fwd: bad args");
+  const int64_t total = (int64_t)a->N * a->P;
+  if (total == 0) return PR_OK;
+  const int nb = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 4096);
+  rotate_fwd_kernel<<<nb, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(*a);
+  return check_launch("rotate_fwd");
+}
+
+extern "C" int pr_rotate_bwd(const PRRotateArgs* a, void* stream) {
+  if (!a || a->N <= 0 || a->P < 0 || !a->R || !a->points || !a->grad_out) return set_error(PR_ERR_ARG, "rotate_bwd: bad args");
+  if (!a->grad_R && !a->grad_points) return PR_OK;
+  rotate_bwd_kernel<<<a->R_batched ? a->N : 1, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(*a);
+  return check_launch("rotate_bwd");
+}

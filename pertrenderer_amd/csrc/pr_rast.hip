@@ -31,6 +31,15 @@ struct V2 {
   float x, y;
 };
 
+// a / b: IEEE division (FAST = false: every forward value and every decision that
+// must agree with the forward) or reciprocal-multiply (FAST: backward arithmetic,
+// ~1 ulp, compared with a tolerance)
+template <bool FAST = false>
+PR_DEV float dv(float a, float b) {
+  if constexpr (FAST) return a * __builtin_amdgcn_rcpf(b);
+  else return a / b;
+}
+
 PR_DEV float edge_fn(V2 p, V2 a, V2 b) { return (p.x - a.x) * (b.y - a.y) - (p.y - a.y) * (b.x - a.x); }
 
 PR_DEV void bary_fwd(V2 p, V2 v0, V2 v1, V2 v2, float w[3]) {
@@ -40,18 +49,20 @@ PR_DEV void bary_fwd(V2 p, V2 v0, V2 v1, V2 v2, float w[3]) {
   w[2] = edge_fn(p, v0, v1) / area;
 }
 
+template <bool FAST = false>
 PR_DEV void persp_fwd(const float b[3], float z0, float z1, float z2, float o[3]) {
   const float t0 = b[0] * z1 * z2, t1 = z0 * b[1] * z2, t2 = z0 * z1 * b[2];
   float d = t0 + t1 + t2;
   d = d > kEps ? d : kEps;
-  o[0] = t0 / d; o[1] = t1 / d; o[2] = t2 / d;
+  o[0] = dv<FAST>(t0, d); o[1] = dv<FAST>(t1, d); o[2] = dv<FAST>(t2, d);
 }
 
+template <bool FAST = false>
 PR_DEV void clip_fwd(const float b[3], float o[3]) {
   const float w0 = b[0] > 0.f ? b[0] : 0.f, w1 = b[1] > 0.f ? b[1] : 0.f, w2 = b[2] > 0.f ? b[2] : 0.f;
   float s = w0 + w1 + w2;
   s = s > 1e-5f ? s : 1e-5f;
-  o[0] = w0 / s; o[1] = w1 / s; o[2] = w2 / s;
+  o[0] = dv<FAST>(w0, s); o[1] = dv<FAST>(w1, s); o[2] = dv<FAST>(w2, s);
 }
 
 // squared distance from p to segment ab
@@ -499,7 +510,7 @@ PR_DEV void seg_dist2_bwd(V2 p, V2 a, V2 b, float g, V2& ga, V2& gb) {
   float t;
   if (l2 <= kEps) t = 1.f;
   else {
-    t = (bax * (p.x - a.x) + bay * (p.y - a.y)) / l2;
+    t = dv<true>(bax * (p.x - a.x) + bay * (p.y - a.y), l2);
     t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
   }
   const float qx = (1.f - t) * a.x + t * b.x, qy = (1.f - t) * a.y + t * b.y;
@@ -528,8 +539,9 @@ PR_DEV void edge_bwd(V2 p, V2 a, V2 b, float g, V2& ga, V2& gb) {
 PR_DEV void bary_bwd(V2 p, V2 v0, V2 v1, V2 v2, const float gb[3], V2 gv[3]) {
   const float area = edge_fn(v2, v0, v1) + kEps;
   const float e0 = edge_fn(p, v1, v2), e1 = edge_fn(p, v2, v0), e2 = edge_fn(p, v0, v1);
-  const float de0 = gb[0] / area, de1 = gb[1] / area, de2 = gb[2] / area;
-  const float darea = -(gb[0] * e0 + gb[1] * e1 + gb[2] * e2) / (area * area);
+  const float ia = __builtin_amdgcn_rcpf(area);
+  const float de0 = gb[0] * ia, de1 = gb[1] * ia, de2 = gb[2] * ia;
+  const float darea = -(gb[0] * e0 + gb[1] * e1 + gb[2] * e2) * (ia * ia);
   V2 g0{0.f, 0.f}, g1{0.f, 0.f}, g2{0.f, 0.f};
   edge_bwd(p, v1, v2, de0, g1, g2);
   edge_bwd(p, v2, v0, de1, g2, g0);
@@ -550,10 +562,11 @@ PR_DEV void persp_bwd(const float b[3], float z0, float z1, float z2, const floa
   const float s = t0 + t1 + t2;
   float gt[3];
   if (s > kEps) {
-    const float dot = (go[0] * t0 + go[1] * t1 + go[2] * t2) / (s * s);
-    gt[0] = go[0] / s - dot; gt[1] = go[1] / s - dot; gt[2] = go[2] / s - dot;
+    const float is = __builtin_amdgcn_rcpf(s);
+    const float dot = (go[0] * t0 + go[1] * t1 + go[2] * t2) * (is * is);
+    gt[0] = go[0] * is - dot; gt[1] = go[1] * is - dot; gt[2] = go[2] * is - dot;
   } else {
-    gt[0] = go[0] / kEps; gt[1] = go[1] / kEps; gt[2] = go[2] / kEps;
+    gt[0] = go[0] * 1e8f; gt[1] = go[1] * 1e8f; gt[2] = go[2] * 1e8f;
   }
   gb[0] = gt[0] * z1 * z2; gb[1] = gt[1] * z0 * z2; gb[2] = gt[2] * z0 * z1;
   gz[0] = gt[1] * b[1] * z2 + gt[2] * z1 * b[2];
@@ -567,10 +580,11 @@ PR_DEV void clip_bwd(const float b[3], const float go[3], float gb[3]) {
   const float s = w0 + w1 + w2;
   float gw[3];
   if (s > 1e-5f) {
-    const float dot = (go[0] * w0 + go[1] * w1 + go[2] * w2) / (s * s);
-    gw[0] = go[0] / s - dot; gw[1] = go[1] / s - dot; gw[2] = go[2] / s - dot;
+    const float is = __builtin_amdgcn_rcpf(s);
+    const float dot = (go[0] * w0 + go[1] * w1 + go[2] * w2) * (is * is);
+    gw[0] = go[0] * is - dot; gw[1] = go[1] * is - dot; gw[2] = go[2] * is - dot;
   } else {
-    gw[0] = go[0] / 1e-5f; gw[1] = go[1] / 1e-5f; gw[2] = go[2] / 1e-5f;
+    gw[0] = go[0] * 1e5f; gw[1] = go[1] * 1e5f; gw[2] = go[2] * 1e5f;
   }
   gb[0] = b[0] > 0.f ? gw[0] : 0.f;
   gb[1] = b[1] > 0.f ? gw[1] : 0.f;
@@ -587,8 +601,10 @@ PR_DEV void slot_grad(const PRRastArgs& a, V2 p, const float* v, int64_t o, floa
   if (a.grad_bary) { gbu[0] = a.grad_bary[o * 3]; gbu[1] = a.grad_bary[o * 3 + 1]; gbu[2] = a.grad_bary[o * 3 + 2]; }
   float bw[3], bp[3], bc[3];
   bary_fwd(p, v0, v1, v2, bw);
-  if (persp) persp_fwd(bw, z0, z1, z2, bp); else { bp[0] = bw[0]; bp[1] = bw[1]; bp[2] = bw[2]; }
-  if (clip) clip_fwd(bp, bc); else { bc[0] = bp[0]; bc[1] = bp[1]; bc[2] = bp[2]; }
+  // bw is exact (its signs decide inside / clip masks as in the forward); the rest
+  // only feeds gradient arithmetic
+  if (persp) persp_fwd<true>(bw, z0, z1, z2, bp); else { bp[0] = bw[0]; bp[1] = bw[1]; bp[2] = bw[2]; }
+  if (clip) clip_fwd<true>(bp, bc); else { bc[0] = bp[0]; bc[1] = bp[1]; bc[2] = bp[2]; }
   const bool inside = bp[0] > 0.f && bp[1] > 0.f && bp[2] > 0.f;
   V2 gdv[3];
   tri_dist2_bwd(p, v0, v1, v2, inside ? -gd : gd, gdv);
@@ -606,9 +622,12 @@ PR_DEV void slot_grad(const PRRastArgs& a, V2 p, const float* v, int64_t o, floa
   g[6] = gbv[2].x + gdv[2].x; g[7] = gbv[2].y + gdv[2].y; g[8] = gzb * bc[2] + gz[2];
 }
 
-constexpr int kHash = 1024;  // LDS table entries per workgroup
-constexpr int kBwdPix = 32;  // pixels per workgroup
+constexpr int kHash = 512;  // LDS table entries per workgroup (distinct faces of one tile)
 
+// One workgroup per 8x8 pixel tile (the forward's tiling): the tile's slots share
+// few faces, so an LDS hash keyed by face id pre-reduces the 9 vertex-gradient
+// components before one global float atomic per (face, component).  Rows of the
+// tile are contiguous 8*K slot ranges: coalesced reads.
 __global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a) {
   __shared__ int hkey[kHash];
   __shared__ float hval[kHash * 9];
@@ -616,27 +635,29 @@ __global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a) {
   for (int i = tid; i < kHash; i += kThreads) hkey[i] = -1;
   for (int i = tid; i < kHash * 9; i += kThreads) hval[i] = 0.f;
   __syncthreads();
-  const int64_t P = (int64_t)a.N * a.H * a.W;
-  const int64_t pix0 = (int64_t)blockIdx.x * kBwdPix;
-  const int npix = (int)min((int64_t)kBwdPix, P - pix0);
-  const int K = a.K;
-  for (int i = tid; i < npix * K; i += kThreads) {
-    const int64_t o = pix0 * K + i;
+  const int K = a.K, H = a.H, W = a.W;
+  const int n = blockIdx.z, row0 = blockIdx.y * kTile, col0 = blockIdx.x * kTile;
+  const int ncols = min(kTile, W - col0), nrows = min(kTile, H - row0);
+  const int per_row = ncols * K;
+  const int total = nrows * per_row;
+  for (int i = tid; i < total; i += kThreads) {
+    const int r = i / per_row, rem = i - r * per_row;
+    const int c = rem / K;
+    const int row = row0 + r, col = col0 + c;
+    const int64_t o = (((int64_t)n * H + row) * W + col0) * K + rem;
     const int64_t f = a.pix_to_face[o];
     if (f < 0) continue;
-    const int64_t pix = o / K;
-    const int col = (int)(pix % a.W), row = (int)((pix / a.W) % a.H);
-    const V2 p{ndc(a.W - 1 - col, a.W, a.H), ndc(a.H - 1 - row, a.H, a.W)};
+    const V2 p{ndc(W - 1 - col, W, H), ndc(H - 1 - row, H, W)};
     float g[9];
     slot_grad(a, p, a.face_verts + f * 9, o, g);
-    // LDS hash pre-reduction
+    // LDS hash pre-reduction (linear probing; overflow goes straight to global)
     uint32_t h = ((uint32_t)f * 2654435761u) & (kHash - 1);
     bool done = false;
     for (int probe = 0; probe < 32 && !done; ++probe) {
       const int cur = atomicCAS(&hkey[h], -1, (int)f);
       if (cur == -1 || cur == (int)f) {
 #pragma unroll
-        for (int c = 0; c < 9; ++c) atomicAdd(&hval[h * 9 + c], g[c]);
+        for (int cc = 0; cc < 9; ++cc) atomicAdd(&hval[h * 9 + cc], g[cc]);
         done = true;
       } else {
         h = (h + 1) & (kHash - 1);
@@ -644,14 +665,15 @@ __global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a) {
     }
     if (!done) {
 #pragma unroll
-      for (int c = 0; c < 9; ++c) atomicAdd(&a.grad_face_verts[f * 9 + c], g[c]);
+      for (int cc = 0; cc < 9; ++cc) atomicAdd(&a.grad_face_verts[f * 9 + cc], g[cc]);
     }
   }
   __syncthreads();
-  for (int i = tid; i < kHash * 9; i += kThreads) {
-    const int e = i / 9;
+  for (int e = tid; e < kHash; e += kThreads) {
     const int f = hkey[e];
-    if (f >= 0) atomicAdd(&a.grad_face_verts[(int64_t)f * 9 + (i - e * 9)], hval[i]);
+    if (f < 0) continue;
+#pragma unroll
+    for (int cc = 0; cc < 9; ++cc) atomicAdd(&a.grad_face_verts[(int64_t)f * 9 + cc], hval[e * 9 + cc]);
   }
 }
 
@@ -819,9 +841,8 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
     if (hipMemsetAsync(a.grad_face_verts, 0, (size_t)a.F * 9 * sizeof(float), st) != hipSuccess)
       return set_error(PR_ERR_HIP, "rast_bwd: memset failed");
   }
-  const int64_t P = (int64_t)a.N * a.H * a.W;
-  const int64_t nb = (P + kBwdPix - 1) / kBwdPix;
-  rast_bwd_kernel<<<(int)nb, kThreads, 0, st>>>(a);
+  dim3 grid((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, a.N);
+  rast_bwd_kernel<<<grid, kThreads, 0, st>>>(a);
   return check_launch("rast_bwd");
 }
 

@@ -138,6 +138,8 @@ class Meshes:
         return self._topo.faces_packed()
 
     def verts_padded(self):
+        if len(self._verts) == 1:
+            return self._verts[0][None]  # a view: no copy kernel
         if all(v.shape[0] == self._verts[0].shape[0] for v in self._verts):
             return torch.stack(self._verts, 0)
         V = max(v.shape[0] for v in self._verts)

@@ -1,10 +1,71 @@
 """SO(3) helpers and Rotate with PyTorch3D conventions (experiments/eval.py:49-55, 343-346,
-428-430): row-vector rotation points @ R, so3_exponential_map = Rodrigues' formula."""
+428-430): row-vector rotation points @ R, so3_exponential_map = Rodrigues' formula.
+
+On the GPU, so3_exponential_map and Rotate.transform_points run as single native
+kernels (pr_so3_exp_*, pr_rotate_*: one launch per direction instead of the ~60
+small kernels of the torch composition); CPU tensors use the torch formulas below.
+"""
 import math
 
 import torch
 
+from .. import _native as nat
+
 F32 = torch.float32
+
+
+class _SO3ExpFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, log_rot, eps):
+        lib = nat.load()
+        w = log_rot.detach().to(F32).contiguous()
+        R = torch.empty((w.shape[0], 3, 3), dtype=F32, device=w.device)
+        a = nat.PRSO3Args()
+        a.N, a.eps, a.log_rot, a.R = w.shape[0], float(eps), nat.ptr(w), nat.ptr(R)
+        nat.check(lib.pr_so3_exp_fwd(a, nat.stream_of(R)), "pr_so3_exp_fwd")
+        ctx.save_for_backward(w)
+        ctx.eps = eps
+        return R
+
+    @staticmethod
+    def backward(ctx, gR):
+        (w,) = ctx.saved_tensors
+        lib = nat.load()
+        g = gR.detach().to(F32).contiguous()
+        gw = torch.empty_like(w)
+        a = nat.PRSO3Args()
+        a.N, a.eps, a.log_rot, a.grad_R, a.grad_log_rot = w.shape[0], float(ctx.eps), nat.ptr(w), nat.ptr(g), nat.ptr(gw)
+        nat.check(lib.pr_so3_exp_bwd(a, nat.stream_of(gw)), "pr_so3_exp_bwd")
+        return gw, None
+
+
+class _RotateFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, points, R):
+        lib = nat.load()
+        p = points.detach().to(F32).contiguous()
+        r = R.detach().to(F32).contiguous()
+        out = torch.empty_like(p)
+        a = nat.PRRotateArgs()
+        a.N, a.P, a.R_batched = p.shape[0], p.shape[1], int(r.shape[0] > 1)
+        a.points, a.R, a.out = nat.ptr(p), nat.ptr(r), nat.ptr(out)
+        nat.check(lib.pr_rotate_fwd(a, nat.stream_of(out)), "pr_rotate_fwd")
+        ctx.save_for_backward(p, r)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        p, r = ctx.saved_tensors
+        lib = nat.load()
+        g = gout.detach().to(F32).contiguous()
+        need_p, need_r = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        gp = torch.empty_like(p) if need_p else None
+        gr = torch.empty_like(r) if need_r else None
+        a = nat.PRRotateArgs()
+        a.N, a.P, a.R_batched = p.shape[0], p.shape[1], int(r.shape[0] > 1)
+        a.points, a.R, a.grad_out, a.grad_points, a.grad_R = nat.ptr(p), nat.ptr(r), nat.ptr(g), nat.ptr(gp), nat.ptr(gr)
+        nat.check(lib.pr_rotate_bwd(a, nat.stream_of(g)), "pr_rotate_bwd")
+        return gp, gr
 
 
 def hat(v):
@@ -18,6 +79,8 @@ def hat(v):
 
 
 def so3_exponential_map(log_rot, eps=0.0001):
+    if log_rot.is_cuda:
+        return _SO3ExpFn.apply(log_rot, eps)
     nrms = (log_rot * log_rot).sum(1)
     angles = torch.clamp(nrms, eps).sqrt()
     inv = 1.0 / angles
@@ -79,7 +142,11 @@ class Rotate:
 
     def transform_points(self, points):
         pts = points if points.dim() == 3 else points[None]
-        out = torch.bmm(pts, self.R.to(pts.device).expand(pts.shape[0], 3, 3))
+        R = self.R.to(pts.device)
+        if pts.is_cuda and R.shape[0] in (1, pts.shape[0]):
+            out = _RotateFn.apply(pts, R)
+        else:
+            out = torch.bmm(pts, R.expand(pts.shape[0], 3, 3))
         return out if points.dim() == 3 else out[0]
 
     def get_matrix(self):

@@ -47,7 +47,8 @@ def test_argument_validation_without_gpu():
 STRUCTS = {
     "PRBlendParams": nat.PRBlendParams, "PRBlendFwdArgs": nat.PRBlendFwdArgs,
     "PRBlendBwdArgs": nat.PRBlendBwdArgs, "PRHeavisideArgs": nat.PRHeavisideArgs,
-    "PRRastArgs": nat.PRRastArgs, "PRInterpArgs": nat.PRInterpArgs,
+    "PRRastArgs": nat.PRRastArgs, "PRInterpArgs": nat.PRInterpArgs, "PRProjectArgs": nat.PRProjectArgs,
+    "PRSO3Args": nat.PRSO3Args, "PRRotateArgs": nat.PRRotateArgs,
 }
 
 
