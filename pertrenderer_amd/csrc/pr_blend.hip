@@ -23,6 +23,8 @@
 // for 24-bit uniforms): a rast slot with |dist/sigma| > 5.8 has the same outcome
 // for every sample, and an agg logit more than 2*5.8*gamma below the pixel's
 // largest logit can never win.
+#include <cstdlib>
+
 #include "pr_common.h"
 
 namespace pr {
@@ -716,12 +718,21 @@ size_t bwd_lds(int PB, int KP1, int Sa) {
   const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + 8 * PB) * sizeof(float);
   return b < 16 * sizeof(float) ? 16 * sizeof(float) : b;
 }
-constexpr size_t kLdsBudget = 48 * 1024;  // >= 3 workgroups (12 waves) per CU
+constexpr size_t kLdsBudget = 48 * 1024;  // forward: >= 3 workgroups (12 waves) per CU
+constexpr size_t kLdsBudgetBwd = 32 * 1024;  // backward: PB=16 at K=50 -> 7 workgroups per CU (measured best)
+
+// PR_BLEND_LDS_KB_FWD / _BWD override the per-workgroup LDS budget (tuning sweeps)
+size_t lds_budget(bool bwd) {
+  const char* e = getenv(bwd ? "PR_BLEND_LDS_KB_BWD" : "PR_BLEND_LDS_KB_FWD");
+  const long v = e ? atol(e) : 0;
+  return v > 0 ? (size_t)v * 1024 : (bwd ? kLdsBudgetBwd : kLdsBudget);
+}
 
 int pick_pb(int KP1, int Sa, bool bwd) {
+  const size_t budget = lds_budget(bwd);
   for (int PB = 32; PB >= 1; PB >>= 1) {
     const size_t b = bwd ? bwd_lds(PB, KP1, Sa) : fwd_lds(PB, KP1);
-    if (b <= kLdsBudget || PB == 1) return PB;
+    if (b <= budget || PB == 1) return PB;
   }
   return 1;
 }

@@ -17,6 +17,7 @@
 // contributions in an LDS hash table keyed by face id before one global
 // atomic per (face, component), so hot faces shared by neighbouring pixels
 // do not serialise on global atomics.
+#include <cstdlib>
 #include <type_traits>
 
 #include "pr_common.h"
@@ -135,24 +136,26 @@ __global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cul
 
 PR_DEV bool key_less(float za, int fa, float zb, int fb) { return za < zb || (za == zb && fa < fb); }
 
-// seg_dist2 with the segment delta (b - a) and its squared length precomputed
+// seg_dist2 with the segment delta (b - a) and its squared length precomputed;
+// branch-free (the degenerate-segment case is a select) so that several faces'
+// tests form one straight-line block the scheduler can interleave
 PR_DEV float seg_dist2_d(V2 p, V2 a, float bax, float bay, float l2, V2 b) {
-  if (l2 <= kEps) {
-    const float dx = p.x - b.x, dy = p.y - b.y;
-    return dx * dx + dy * dy;
-  }
+  const float bx = p.x - b.x, by = p.y - b.y;
+  const float db = bx * bx + by * by;
   float t = (bax * (p.x - a.x) + bay * (p.y - a.y)) / l2;
   t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
   const float qx = a.x + t * bax, qy = a.y + t * bay;
   const float dx = p.x - qx, dy = p.y - qy;
-  return dx * dx + dy * dy;
+  const float ds = dx * dx + dy * dy;
+  return l2 <= kEps ? db : ds;
 }
 
 // Full per-pixel test of one face, branch-free so that several faces' division
 // chains interleave (one wave per SIMD: ILP is the latency hiding).  Same decisions
 // as PyTorch3D's per-face body: in bbox -> bary -> perspective -> clip -> pz >= 0 ->
-// inside or dist < blur.  `persp` / `clip` / the degenerate-edge tests are uniform.
-PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, bool persp, bool clip, float& pz) {
+// inside or dist < blur.  Perspective correction / clipping are compile-time.
+template <bool PERSP, bool CLIP>
+PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, float& pz) {
   const bool inbox = !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
   const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
   const float z0 = r.a.z, z1 = r.b.y, z2 = r.c.x;
@@ -162,13 +165,13 @@ PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, bool persp, bool clip,
   const float e1 = (p.x - v2.x) * r.f.y - (p.y - v2.y) * r.f.x;
   const float e2 = (p.x - v0.x) * r.e.y - (p.y - v0.y) * r.e.x;
   float b[3] = {e0 / area, e1 / area, e2 / area};
-  if (persp) {
+  if constexpr (PERSP) {
     const float t0 = b[0] * z1 * z2, t1 = z0 * b[1] * z2, t2 = z0 * z1 * b[2];
     float d = t0 + t1 + t2;
     d = d > kEps ? d : kEps;
     b[0] = t0 / d; b[1] = t1 / d; b[2] = t2 / d;
   }
-  if (clip) {
+  if constexpr (CLIP) {
     float bc[3];
     clip_fwd(b, bc);
     pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
@@ -188,22 +191,17 @@ PR_DEV bool in_bbox(const FaceRec& r, V2 p) {
   return !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
 }
 
-#ifdef PR_RAST_PROFILE
-#define PR_STAMP(i) (stamp[i] += (long long)__builtin_amdgcn_s_memtime() - t_, t_ = __builtin_amdgcn_s_memtime())
-#else
-#define PR_STAMP(i) ((void)0)
-#endif
-
 constexpr int kCap = 512;    // per-round tile face list (faces beyond it are handled in later rounds)
 static_assert(kCap <= 8 * 64, "suffix-min pass holds kCap / 64 <= 8 entries per lane");
-constexpr int kCullU = 4;    // 64-face cull chunks whose loads are in flight together
+constexpr int kCullU = 4;    // 64-face cull chunks whose loads are in flight together (per wave)
 constexpr int kGroup = 4;    // faces tested together (independent chains)
 
-// Bitonic sort (ascending key) of n2 (power of two) LDS entries by one wave.
-PR_DEV void bitonic_sort(float* key, int* val, int n2, int lane) {
+// Bitonic sort (ascending key) of n2 (power of two) LDS entries by NT threads.
+template <int NT>
+PR_DEV void bitonic_sort(float* key, int* val, int n2, int tid) {
   for (int k = 2; k <= n2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = lane; i < n2; i += 64) {
+      for (int i = tid; i < n2; i += NT) {
         const int ixj = i ^ j;
         if (ixj > i) {
           const bool up = (i & k) == 0;
@@ -219,26 +217,67 @@ PR_DEV void bitonic_sort(float* key, int* val, int n2, int lane) {
   }
 }
 
+PR_DEV bool ekey_less(float2 x, float2 y) { return key_less(x.x, __float_as_int(x.y), y.x, __float_as_int(y.y)); }
+
+// In-place merge of the lane's sorted columns A (a entries) and B (b entries), keys
+// all distinct: A[0..m) becomes the m = min(K, a+b) smallest, ascending.  Runs from
+// the back (writes land at or above A's read cursor); the a+b-m largest are dropped.
+PR_DEV int merge_columns(float2* A, const float2* B, int a, int b, int K, int lane) {
+  const int m = min(K, a + b);
+  int i = a - 1, j = b - 1;
+  float2 ea = i >= 0 ? A[i * 64 + lane] : make_float2(0.f, 0.f);
+  float2 eb = j >= 0 ? B[j * 64 + lane] : make_float2(0.f, 0.f);
+  for (int skip = a + b - m; skip > 0; --skip) {
+    if (j < 0 || (i >= 0 && ekey_less(eb, ea))) { --i; if (i >= 0) ea = A[i * 64 + lane]; }
+    else { --j; if (j >= 0) eb = B[j * 64 + lane]; }
+  }
+  for (int pos = m - 1; j >= 0; --pos) {  // once B is exhausted A[0..i] is already in place
+    if (i >= 0 && ekey_less(eb, ea)) {
+      A[pos * 64 + lane] = ea;
+      --i;
+      if (i >= 0) ea = A[i * 64 + lane];
+    } else {
+      A[pos * 64 + lane] = eb;
+      --j;
+      if (j >= 0) eb = B[j * 64 + lane];
+    }
+  }
+  return m;
+}
+
+template <bool PERSP, bool CLIP>
+void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, dim3 grid, int wv, size_t lds, hipStream_t st);
+
+size_t rast_fwd_lds(int K, int WV) {
+  return (size_t)WV * 64 * sizeof(FaceRec) + (size_t)WV * K * 64 * 8 + (size_t)kCap * 12 + (size_t)WV * 64 * 4 + 16;
+}
+
 // Forward, pass 1: per-pixel K nearest (z, face) keys -> pix_to_face, zbuf.
-// One wave per 8x8 tile, one lane per pixel.  Per round: cull the mesh's faces
-// against the tile (ballot compaction into LDS, kCullU chunks of loads in flight),
-// bitonic-sort the survivors by z_min, then walk them in 64-face chunks staged in
-// LDS; the wave tests kGroup faces at once (broadcast LDS reads, independent
-// chains) and inserts the candidates in order.  The lane's K-queue is an LDS
-// column sorted by (z, face id), exactly PyTorch3D's order (the final queue is the
-// K smallest keys, independent of insertion order).  Barycentrics / distances of
-// the winners come from rast_frag_kernel, fully parallel over slots.
-__global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces) {
+// One workgroup of WV waves per 8x8 tile, one lane per pixel.  Per round: the waves
+// cull the mesh's faces against the tile (ballot compaction, LDS append), sort the
+// survivors by their depth near the tile centre, then wave w walks sorted positions
+// w, w+WV, ... in 64-face chunks staged in its own LDS slice, testing kGroup faces
+// at once (broadcast reads, independent chains) into its own per-pixel K-queue (an
+// LDS column sorted by (z, face id), PyTorch3D's order).  The WV queues are then
+// merged per pixel.  The final queue is the K smallest keys of all candidates, so
+// it does not depend on WV or on the traversal order.  WV > 1 spreads a heavy
+// tile over several SIMDs and lets the dispatcher balance light and heavy tiles.
+// Barycentrics / distances of the winners come from rast_frag_kernel.
+template <int WV, bool PERSP, bool CLIP>
+__global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces) {
   extern __shared__ float smem[];
+  constexpr int NT = 64 * WV;
   const int K = a.K;
-  FaceRec* lrec = reinterpret_cast<FaceRec*>(smem);          // [64] staged face records of a chunk
-  float2* q = reinterpret_cast<float2*>(lrec + 64);          // [K][64] (z, face id bits), sorted per lane
-  int* lfid = reinterpret_cast<int*>(q + K * 64);            // [kCap] tile face list (cull order)
-  float* lkey = reinterpret_cast<float*>(lfid + kCap);       // [kCap] sort key (depth near the tile centre),
-  float* lsuf = lkey;                                        //   then suffix min of z_min in sorted order
-  int* lidx = reinterpret_cast<int*>(lkey + kCap);           // [kCap] sorted -> cull order
-  int* qsz = lidx + kCap;                                    // [64] queue sizes
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  FaceRec* lrec = reinterpret_cast<FaceRec*>(smem) + wv * 64;        // [WV][64] staged chunk per wave
+  float2* qall = reinterpret_cast<float2*>(reinterpret_cast<FaceRec*>(smem) + WV * 64);
+  float2* q = qall + (size_t)wv * K * 64;                              // [WV][K][64] per-wave queues
+  int* lfid = reinterpret_cast<int*>(qall + (size_t)WV * K * 64);      // [kCap] tile face list (cull order)
+  float* lkey = reinterpret_cast<float*>(lfid + kCap);                 // [kCap] sort key, then
+  float* lsuf = lkey;                                                  //   suffix min of z_min
+  int* lidx = reinterpret_cast<int*>(lkey + kCap);                     // [kCap] sorted -> cull order
+  int* qsz = lidx + kCap;                                              // [WV][64] queue sizes
+  int* lcount = qsz + WV * 64;                                         // cull append counter
   const int n = blockIdx.z;
   const int H = a.H, W = a.W;
   const int row0 = blockIdx.y * kTile, col0 = blockIdx.x * kTile;
@@ -251,41 +290,42 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
   const float tymax = ndc(H - 1 - row0, H, W), tymin = ndc(H - 1 - r1, H, W);
   const float tcx = 0.5f * (txmin + txmax), tcy = 0.5f * (tymin + tymax);
   const int64_t fb = a.mesh_first_face[n], fe = fb + a.mesh_num_faces[n];
-  const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
+  constexpr bool clip = CLIP;
   const float blur = a.blur_radius;
   int qs = 0;
   float qlast_z = __builtin_inff();
   int qlast_f = 0x7fffffff;
   int64_t base = fb;
-#ifdef PR_RAST_PROFILE
-  long long stamp[7] = {0, 0, 0, 0, 0, 0, 0}, t_ = __builtin_amdgcn_s_memtime(), u_ = 0;
-  int ntest = 0, nins = 0, nlist = 0;
-#endif
   while (base < fe) {
     // ---- gather this round's culled faces (expanded bbox overlaps the tile)
+    if (tid == 0) *lcount = 0;
+    __syncthreads();
     int nl = 0;
-    while (base < fe && nl <= kCap - 64 * kCullU) {
-      float4 cc[kCullU], dd[kCullU];
+    constexpr int U = kCullU / WV > 0 ? kCullU / WV : 1;  // chunks per wave: 64*kCullU faces per pass
+    while (base < fe && nl <= kCap - 64 * U * WV) {
+      float4 cc[U], dd[U];
 #pragma unroll
-      for (int u = 0; u < kCullU; ++u) {
-        const int64_t f = base + u * 64 + lane;
+      for (int u = 0; u < U; ++u) {
+        const int64_t f = base + (wv * U + u) * 64 + lane;
         const int64_t fl = f < fe ? f : fe - 1;
         cc[u] = faces[fl].c; dd[u] = faces[fl].d;
       }
 #pragma unroll
-      for (int u = 0; u < kCullU; ++u) {
-        const int64_t f = base + u * 64 + lane;
+      for (int u = 0; u < U; ++u) {
+        const int64_t f = base + (wv * U + u) * 64 + lane;
         const bool keep = f < fe && !(cc[u].y > txmax || cc[u].z < txmin || cc[u].w > tymax || dd[u].x < tymin);
         const uint64_t bal = __ballot(keep);
-        if (keep) lfid[nl + __popcll(bal & ((1ull << lane) - 1ull))] = (int)f;
-        nl += __popcll(bal);
+        if (bal == 0) continue;
+        int off = 0;
+        if (lane == 0) off = atomicAdd(lcount, __popcll(bal));
+        off = __shfl(off, 0);
+        if (keep) lfid[off + __popcll(bal & ((1ull << lane) - 1ull))] = (int)f;
       }
-      base += 64 * kCullU;
+      base += 64 * U * WV;
+      __syncthreads();
+      nl = *lcount;
+      __syncthreads();
     }
-    PR_STAMP(0);
-#ifdef PR_RAST_PROFILE
-    nlist += nl;
-#endif
     if (nl == 0) continue;
     bool done = !inimg;  // the early exit below is only valid inside one sorted round
     // ---- sort key: the face plane's depth at the tile centre, clamped to the face's
@@ -293,8 +333,7 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
     //      appends).  Exactness does not depend on it; the early exit uses z_min.
     int n2 = 1;
     while (n2 < nl) n2 <<= 1;
-    __syncthreads();
-    for (int i = lane; i < n2; i += 64) {
+    for (int i = tid; i < n2; i += NT) {
       float key = __builtin_inff();
       if (i < nl) {
         const FaceRec& r = faces[lfid[i]];
@@ -315,44 +354,52 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
       lidx[i] = i < nl ? i : 0x7fffffff;
     }
     __syncthreads();
-    bitonic_sort(lkey, lidx, n2, lane);
+    bitonic_sort<NT>(lkey, lidx, n2, tid);
     // suffix minimum of z_min along the sorted order (faces after position i cannot
-    // produce pz below lsuf[i] when barycentrics are clipped)
+    // produce pz below lsuf[i] when barycentrics are clipped); wave 0 computes it
     {
       const int per = (nl + 63) / 64;  // contiguous run of sorted positions per lane
       const int i0 = lane * per, i1 = min(nl, i0 + per);
       float zl[8];  // z_min of this lane's run (per <= kCap / 64)
+      float run = __builtin_inff();
+      if (wv == 0) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) zl[u] = i0 + u < i1 ? faces[lfid[lidx[i0 + u]]].f.w : __builtin_inff();
-      float m = __builtin_inff();
+        for (int u = 0; u < 8; ++u) zl[u] = i0 + u < i1 ? faces[lfid[lidx[i0 + u]]].f.w : __builtin_inff();
+        float m = __builtin_inff();
 #pragma unroll
-      for (int u = 0; u < 8; ++u) m = fminf(m, zl[u]);
-      // exclusive suffix-min across lanes (lanes above this one)
-      float ex = m;
+        for (int u = 0; u < 8; ++u) m = fminf(m, zl[u]);
+        // exclusive suffix-min across lanes (lanes above this one)
+        float ex = m;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const float t = __shfl_down(ex, o);
-        if (lane + o < 64) ex = fminf(ex, t);
+        for (int o = 1; o < 64; o <<= 1) {
+          const float t = __shfl_down(ex, o);
+          if (lane + o < 64) ex = fminf(ex, t);
+        }
+        run = __shfl_down(ex, 1);
+        if (lane == 63) run = __builtin_inff();
       }
-      float run = __shfl_down(ex, 1);
-      if (lane == 63) run = __builtin_inff();
-      __syncthreads();  // lsuf aliases lkey: every lane is past its sorted reads
+      __syncthreads();  // lsuf aliases lkey: every thread is past its sorted reads
+      if (wv == 0) {
 #pragma unroll
-      for (int u = 7; u >= 0; --u) {
-        run = fminf(run, zl[u]);
-        if (i0 + u < i1) lsuf[i0 + u] = run;
+        for (int u = 7; u >= 0; --u) {
+          run = fminf(run, zl[u]);
+          if (i0 + u < i1) lsuf[i0 + u] = run;
+        }
       }
     }
     __syncthreads();
-    PR_STAMP(1);
-    for (int c0 = 0; c0 < nl && __ballot(!done) != 0; c0 += 64) {
-      const int cnt = min(64, nl - c0);
-      __syncthreads();
+    // ---- traversal: this wave's sorted positions wv, wv+WV, ... in chunks of 64
+    const int nmine = nl > wv ? (nl - wv + WV - 1) / WV : 0;
+    for (int c0 = 0; c0 < nmine && __ballot(!done) != 0; c0 += 64) {
+      const int cnt = min(64, nmine - c0);
+      const int sp = wv + WV * (c0 + min(lane, cnt - 1));  // sorted position held by this lane
       // lane i holds chunk entry i's face id and suffix-min z (read back with readlane)
-      const int cfid = lfid[lidx[c0 + min(lane, cnt - 1)]];
-      const float csuf = lsuf[c0 + min(lane, cnt - 1)];
+      const int cfid = lfid[lidx[sp]];
+      const float csuf = lsuf[sp];
+      __builtin_amdgcn_wave_barrier();
       if (lane < cnt) lrec[lane] = faces[cfid];
-      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       for (int t = 0; t < cnt; t += kGroup) {
         bool cand[kGroup];
         float pzv[kGroup];
@@ -363,20 +410,12 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
           any |= t + j < cnt && __ballot(in_bbox(lrec[tt], p)) != 0;
         }
         if (!any) continue;
-#ifdef PR_RAST_PROFILE
-        u_ = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           const int tt = min(t + j, cnt - 1);
           const FaceRec rr = lrec[tt];
-          cand[j] = face_test(rr, p, blur, persp, clip, pzv[j]) && t + j < cnt;
+          cand[j] = face_test<PERSP, CLIP>(rr, p, blur, pzv[j]) && t + j < cnt;
         }
-#ifdef PR_RAST_PROFILE
-        if (__ballot(cand[0] || cand[1] || cand[2] || cand[3]) == ~0ull) stamp[6] += 0;
-        stamp[5] += __builtin_amdgcn_s_memtime() - u_;
-        u_ = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           if (t + j >= cnt) break;
@@ -387,19 +426,12 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
           if (done || !cand[j]) continue;
           const int fid = __builtin_amdgcn_readlane(cfid, t + j);
           const float pz = pzv[j];
-#ifdef PR_RAST_PROFILE
-          ++nins;
-#endif
           // (qlast_z, qlast_f) = the queue's last (largest) key, kept in registers
           if (qs == K && !key_less(pz, fid, qlast_z, qlast_f)) continue;
           if (qs == 0 || key_less(qlast_z, qlast_f, pz, fid)) {
             // append (the common case: faces arrive roughly in depth order)
-            if (qs < K) {
-              q[qs * 64 + lane] = make_float2(pz, __int_as_float(fid));
-              ++qs;
-            } else {
-              q[(K - 1) * 64 + lane] = make_float2(pz, __int_as_float(fid));
-            }
+            q[qs * 64 + lane] = make_float2(pz, __int_as_float(fid));
+            ++qs;
             qlast_z = pz;
             qlast_f = fid;
             continue;
@@ -424,30 +456,33 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
             if (sh < 4) break;
           }
           q[pos * 64 + lane] = make_float2(pz, __int_as_float(fid));
-          {
-            const float2 last = q[(qs - 1) * 64 + lane];
-            qlast_z = last.x;
-            qlast_f = __float_as_int(last.y);
-          }
+          const float2 last = q[(qs - 1) * 64 + lane];
+          qlast_z = last.x;
+          qlast_f = __float_as_int(last.y);
         }
-#ifdef PR_RAST_PROFILE
-        ntest += kGroup;
-        stamp[6] += __builtin_amdgcn_s_memtime() - u_;
-#endif
         if (__ballot(!done) == 0) break;
       }
     }
     __syncthreads();
-    PR_STAMP(2);
   }
-  qsz[lane] = inimg ? qs : 0;
+  qsz[wv * 64 + lane] = inimg ? qs : 0;
   __syncthreads();
-#ifdef PR_RAST_PROFILE
-  PR_STAMP(3);
-#endif
+  // ---- merge the WV per-wave queues into wave 0's (pairwise, from the back)
+  if constexpr (WV >= 2) {
+#pragma unroll
+    for (int step = 1; step < WV; step <<= 1) {
+      if ((wv & (2 * step - 1)) == 0) {
+        const int other = wv + step;
+        qsz[wv * 64 + lane] = merge_columns(q, qall + (size_t)other * K * 64, qsz[wv * 64 + lane],
+                                            qsz[other * 64 + lane], K, lane);
+      }
+      __syncthreads();
+    }
+  }
   // ---- coalesced output: each tile row's 8 pixels own a contiguous 8*K slot range
+  const float2* q0 = qall;
   const int q64 = 64 / K, r64 = 64 % K;
-  for (int r = 0; r < kTile; ++r) {
+  for (int r = wv; r < kTile; r += WV) {
     const int prow = row0 + r;
     if (prow >= H) break;
     const int ncols = min(kTile, W - col0);
@@ -457,18 +492,27 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
          i += 64, c += q64, k += r64, (k >= K ? (k -= K, ++c) : 0)) {
       const int tl = r * kTile + c;
       const int64_t o = obase + i;
-      const float2 e = q[k * 64 + tl];  // read with the size (stale beyond it, unused)
+      const float2 e = q0[k * 64 + tl];  // read with the size (stale beyond it, unused)
       const bool valid = k < qsz[tl];
       a.pix_to_face[o] = valid ? (int64_t)__float_as_int(e.y) : (int64_t)-1;
       a.zbuf[o] = valid ? e.x : -1.f;
     }
   }
-#ifdef PR_RAST_PROFILE
-  PR_STAMP(4);
-  if (lane == 0 && nlist >= 90)
-    printf("tile %d,%d list %d tests(lane0) %d ins %d | cull %lld sort %lld test %lld tail %lld out %lld | tcomp %lld tins %lld\n",
-           blockIdx.x, blockIdx.y, nlist, ntest, nins, stamp[0], stamp[1], stamp[2], stamp[3], stamp[4], stamp[5], stamp[6]);
-#endif
+}
+
+template <bool PERSP, bool CLIP>
+void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, dim3 grid, int wv, size_t lds, hipStream_t st) {
+  if (wv == 4) rast_fwd_kernel<4, PERSP, CLIP><<<grid, 256, lds, st>>>(a, fr);
+  else if (wv == 2) rast_fwd_kernel<2, PERSP, CLIP><<<grid, 128, lds, st>>>(a, fr);
+  else rast_fwd_kernel<1, PERSP, CLIP><<<grid, 64, lds, st>>>(a, fr);
+}
+
+void launch_rast_fwd(const PRRastArgs& a, const FaceRec* fr, dim3 grid, int wv, size_t lds, hipStream_t st) {
+  const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
+  if (persp && clip) launch_rast_fwd_pc<true, true>(a, fr, grid, wv, lds, st);
+  else if (persp) launch_rast_fwd_pc<true, false>(a, fr, grid, wv, lds, st);
+  else if (clip) launch_rast_fwd_pc<false, true>(a, fr, grid, wv, lds, st);
+  else launch_rast_fwd_pc<false, false>(a, fr, grid, wv, lds, st);
 }
 
 // Forward, pass 2: barycentrics (perspective-corrected, clipped) and signed squared
@@ -628,16 +672,23 @@ constexpr int kHash = 512;  // LDS table entries per workgroup (distinct faces o
 // few faces, so an LDS hash keyed by face id pre-reduces the 9 vertex-gradient
 // components before one global float atomic per (face, component).  Rows of the
 // tile are contiguous 8*K slot ranges: coalesced reads.
-__global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a) {
+__global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a, int tile_rows) {
   __shared__ int hkey[kHash];
   __shared__ float hval[kHash * 9];
   const int tid = threadIdx.x;
+#ifdef PR_RAST_PROFILE
+  long long t0 = __builtin_amdgcn_s_memtime(), t1 = 0, t2 = 0, tg = 0, th = 0;
+  int nv = 0;
+#endif
   for (int i = tid; i < kHash; i += kThreads) hkey[i] = -1;
   for (int i = tid; i < kHash * 9; i += kThreads) hval[i] = 0.f;
   __syncthreads();
+#ifdef PR_RAST_PROFILE
+  t1 = __builtin_amdgcn_s_memtime();
+#endif
   const int K = a.K, H = a.H, W = a.W;
-  const int n = blockIdx.z, row0 = blockIdx.y * kTile, col0 = blockIdx.x * kTile;
-  const int ncols = min(kTile, W - col0), nrows = min(kTile, H - row0);
+  const int n = blockIdx.z, row0 = blockIdx.y * tile_rows, col0 = blockIdx.x * kTile;
+  const int ncols = min(kTile, W - col0), nrows = min(tile_rows, H - row0);
   const int per_row = ncols * K;
   const int total = nrows * per_row;
   for (int i = tid; i < total; i += kThreads) {
@@ -649,7 +700,16 @@ __global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a) {
     if (f < 0) continue;
     const V2 p{ndc(W - 1 - col, W, H), ndc(H - 1 - row, H, W)};
     float g[9];
+#ifdef PR_RAST_PROFILE
+    long long u0 = __builtin_amdgcn_s_memtime();
+    ++nv;
+#endif
     slot_grad(a, p, a.face_verts + f * 9, o, g);
+#ifdef PR_RAST_PROFILE
+    for (int cc = 0; cc < 9; ++cc) if (g[cc] == 12345.f) tg += 1;  // keep g live before the stamp
+    long long u1 = __builtin_amdgcn_s_memtime();
+    tg += u1 - u0;
+#endif
     // LDS hash pre-reduction (linear probing; overflow goes straight to global)
     uint32_t h = ((uint32_t)f * 2654435761u) & (kHash - 1);
     bool done = false;
@@ -667,14 +727,27 @@ __global__ void __launch_bounds__(kThreads) rast_bwd_kernel(PRRastArgs a) {
 #pragma unroll
       for (int cc = 0; cc < 9; ++cc) atomicAdd(&a.grad_face_verts[f * 9 + cc], g[cc]);
     }
+#ifdef PR_RAST_PROFILE
+    th += __builtin_amdgcn_s_memtime() - u1;
+#endif
   }
   __syncthreads();
+#ifdef PR_RAST_PROFILE
+  t2 = __builtin_amdgcn_s_memtime();
+#endif
   for (int e = tid; e < kHash; e += kThreads) {
     const int f = hkey[e];
     if (f < 0) continue;
 #pragma unroll
     for (int cc = 0; cc < 9; ++cc) atomicAdd(&a.grad_face_verts[(int64_t)f * 9 + cc], hval[e * 9 + cc]);
   }
+#ifdef PR_RAST_PROFILE
+  __syncthreads();
+  const long long t3 = __builtin_amdgcn_s_memtime();
+  if (tid == 0 && nv >= 8)
+    printf("bwd tile %d,%d nvalid(t0) %d | init %lld main %lld flush %lld | grad %lld hash %lld\n", blockIdx.x,
+           blockIdx.y, nv, t1 - t0, t2 - t1, t3 - t2, tg, th);
+#endif
 }
 
 // ------------------------------------------------------------ interpolation
@@ -788,7 +861,7 @@ int rast_check(const PRRastArgs& a) {
   if (!a.face_verts && a.F > 0) return set_error(PR_ERR_ARG, "rast: face_verts missing");
   if (!a.mesh_first_face || !a.mesh_num_faces) return set_error(PR_ERR_ARG, "rast: mesh index missing");
   if (a.K > 512) return set_error(PR_ERR_ARG, "rast: faces_per_pixel must be <= 512");
-  if ((int64_t)a.H > 65535 * kTile || (int64_t)a.W > 65535 * kTile || a.N > 65535)
+  if ((int64_t)a.H > 65535 || (int64_t)a.W > 65535 * kTile || a.N > 65535)
     return set_error(PR_ERR_ARG, "rast: image too large");
   return PR_OK;
 }
@@ -818,9 +891,18 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
     if (int e = check_launch("rast_face_prep")) return e;
   }
   dim3 grid((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, a.N);
-  const size_t lds = 64 * sizeof(FaceRec) + (size_t)a.K * 64 * 8 + kCap * 12 + 64 * 4;
+  // waves per tile: 1 measured fastest on the bench frame (256^2, 1024 tiles: the
+  // split's per-tile cull/sort/merge overhead outweighs the shorter traversal);
+  // PR_RAST_WAVES=2|4 selects the split variant (sweeps, few-tile heavy meshes)
+  int wv = 1;
+  if (const char* ew = getenv("PR_RAST_WAVES")) {
+    const int v = atoi(ew);
+    if (v == 1 || v == 2 || v == 4) wv = v;
+  }
+  while (wv > 1 && rast_fwd_lds(a.K, wv) > 160 * 1024) wv >>= 1;
+  const size_t lds = rast_fwd_lds(a.K, wv);
   if (lds > 160 * 1024) return set_error(PR_ERR_ARG, "rast_fwd: faces_per_pixel too large for the LDS queue (max 300)");
-  rast_fwd_kernel<<<grid, 64, lds, st>>>(a, fr);
+  launch_rast_fwd(a, fr, grid, wv, lds, st);
   if (int e = check_launch("rast_fwd")) return e;
   const int64_t total = (int64_t)a.N * a.H * a.W * a.K;
   const int nb = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 1 << 20);
@@ -841,8 +923,11 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
     if (hipMemsetAsync(a.grad_face_verts, 0, (size_t)a.F * 9 * sizeof(float), st) != hipSuccess)
       return set_error(PR_ERR_HIP, "rast_bwd: memset failed");
   }
-  dim3 grid((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, a.N);
-  rast_bwd_kernel<<<grid, kThreads, 0, st>>>(a);
+  // rows per workgroup tile (8 = the forward's tiles); PR_RAST_BWD_ROWS overrides (sweeps)
+  const char* er = getenv("PR_RAST_BWD_ROWS");
+  const int rows = er && atoi(er) > 0 && atoi(er) <= 64 ? atoi(er) : kTile;
+  dim3 grid((a.W + kTile - 1) / kTile, (a.H + rows - 1) / rows, a.N);
+  rast_bwd_kernel<<<grid, kThreads, 0, st>>>(a, rows);
   return check_launch("rast_bwd");
 }
 
