@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 4
+#define PR_ABI_VERSION 5
 
 /* error codes */
 #define PR_OK 0
@@ -50,12 +50,20 @@ extern "C" {
 #define PR_ERR_WORKSPACE -3
 
 /* noise sources */
-#define PR_NOISE_PHILOX 0   /* in-kernel Philox4x32-10 keyed by (seed, pixel, slot, sample) */
+#define PR_NOISE_PHILOX 0   /* in-kernel Philox4x32-10 keyed by (seed, pixel, slot, sample); */
+                            /* N(0,1) by Box-Muller, Cauchy by tan(pi (u - 1/2))             */
 #define PR_NOISE_INJECTED 1 /* caller-provided N(0,1) tensors (reference-parity mode) */
 
 /* pr_blend flags */
 #define PR_BLEND_RAST 1  /* probabilities from dists via the perturbed Heaviside (else `prob` input) */
 #define PR_BLEND_COLOR 2 /* colour mix + alpha -> image (else weights (N,H,W,K+1) out) */
+#define PR_BLEND_VERTEX 4 /* with COLOR: slot colours interpolated on demand from per-vertex    */
+                          /* colours (TexturesVertex.sample_textures fused; no texel tensor)    */
+/* noise variants; also valid in PRHeavisideArgs.flags (RAST bits) */
+#define PR_BLEND_RAST_CAUCHY 8  /* ArctanRast: Cauchy rast noise, score 2e/(1+e^2) (smoothrast.py:162-173) */
+#define PR_BLEND_AGG_CAUCHY 16  /* CauchyAgg: Cauchy agg noise (smoothagg.py:230-250)                    */
+#define PR_BLEND_RAST_WOVR 32   /* GaussianRast_wovr: score without the vr baseline (smoothrast.py:61-108) */
+#define PR_BLEND_AGG_WOVR 64    /* GaussianAgg_wovr: a_s = <g, w_s> (smoothagg.py:75-141; Cauchy keeps vr) */
 
 typedef struct PRBlendParams {
   int32_t N, H, W, K;        /* fragment shape */
@@ -91,6 +99,10 @@ typedef struct PRBlendFwdArgs {
   uint8_t* winners;           /* out: (P,Sa) per-sample argmax index, saved for backward */
   float* rast_cache;          /* RAST, nullable out: (N,H,W,K,2) per-slot (prob, rast score mean);  */
                               /* handed to pr_blend_bwd it replaces regenerating the rast noise    */
+  /* VERTEX: colour of slot (p,k) = sum_i bary[p,k,i] * vert_colors[faces[p2f[p,k],i]] (0 if p2f<0) */
+  const float* bary;          /* (N,H,W,K,3) */
+  const int64_t* faces;       /* (F,3) packed vertex indices */
+  const float* vert_colors;   /* (V,3) packed per-vertex colours */
 } PRBlendFwdArgs;
 
 typedef struct PRBlendBwdArgs {
@@ -112,6 +124,11 @@ typedef struct PRBlendBwdArgs {
   void* workspace;            /* >= pr_blend_bwd_workspace_size(args) bytes */
   size_t workspace_bytes;
   const float* rast_cache;    /* RAST, nullable: pr_blend_fwd's rast_cache of the same call */
+  const float* bary;          /* VERTEX: as in PRBlendFwdArgs */
+  const int64_t* faces;
+  const float* vert_colors;
+  float* grad_bary;           /* VERTEX out (N,H,W,K,3) (replaces grad_colors) */
+  float* grad_vert_colors;    /* VERTEX out (V,3), nullable, accumulated (caller zeroes) */
 } PRBlendBwdArgs;
 
 typedef struct PRHeavisideArgs {
@@ -128,6 +145,7 @@ typedef struct PRHeavisideArgs {
   size_t workspace_bytes;
   const float* sigma_dev;     /* nullable device sigma (overrides `sigma`) */
   const uint64_t* seeds;      /* nullable device seed base (see PRBlendParams.seeds) */
+  int32_t flags;              /* PR_BLEND_RAST_CAUCHY | PR_BLEND_RAST_WOVR */
 } PRHeavisideArgs;
 
 typedef struct PRRastArgs {

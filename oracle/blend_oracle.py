@@ -6,8 +6,11 @@ leg may import this module.  The product (``pertrenderer_amd``) never calls it.
 A closed-form restatement, in float32 torch-CPU tensor arithmetic with INJECTED
 noise, of the reference's perturbed soft rasterizer + perturbed aggregation:
 
-* ``smoothrast.py:12-59``   randomHeaviside  (Gaussian noise, variance-reduced score)
-* ``smoothagg.py:10-73``    randomArgmax     (Gaussian noise, variance-reduced score)
+* ``smoothrast.py:12-59``   randomHeaviside  (Gaussian / Cauchy noise, variance-reduced score)
+* ``smoothrast.py:61-108``  randomHeaviside_wovr (no variance reduction)
+* ``smoothagg.py:10-73``    randomArgmax     (Gaussian / Cauchy noise, variance-reduced score)
+* ``smoothagg.py:75-141``   randomArgmax_wovr (Gaussian without variance reduction; its
+  Cauchy branch keeps w - vr, as the reference does)
 * ``smoothagg.py:185-205``  GaussianAgg.aggregate  (logit assembly incl. background)
 * ``smoothagg.py:292-337``  log_corrected / prod_corrected  (inf/nan-safe backward)
 * ``random_rasterizer.py:34-56``  smooth_rgb_blend  (mask, alpha product, colour mix)
@@ -38,12 +41,19 @@ def heaviside_fwd(D, noise_r, sigma):
     return maps.mean(dim=0), maps, vr
 
 
-def heaviside_bwd(maps, vr, noise_r, sigma, gP):
-    """smoothrast.py:45-58 (gaussian branch): gmaps = mean_s((maps-vr)*eps/sigma);
-    d D = gmaps*gP ; d sigma = sum(gmaps*gP)  (the quirk at :57-58 overwrites the
-    sigma score of :47 with this sum)."""
+def score(noise, kind):
+    """d/d eps of -log density: eps (Gaussian, smoothrast.py:46) or 2 eps / (1 + eps^2)
+    (Cauchy, smoothrast.py:49, smoothagg.py:60)."""
+    return noise if kind == "gaussian" else (2 * noise) / (1 + torch.square(noise))
+
+
+def heaviside_bwd(maps, vr, noise_r, sigma, gP, kind="gaussian", use_vr=True):
+    """smoothrast.py:45-58 / :94-107: gmaps = mean_s(base*score/sigma) with base = maps-vr
+    (variance-reduced) or maps (_wovr); d D = gmaps*gP ; d sigma = sum(gmaps*gP) (the
+    quirk at :57-58 overwrites the sigma score of :47 with this sum)."""
     sigma = _t(sigma)
-    gmaps = ((maps - vr) * noise_r / sigma).mean(dim=0)
+    base = (maps - vr) if use_vr else maps
+    gmaps = (base * score(noise_r, kind) / sigma).mean(dim=0)
     gD = gmaps * gP
     return gD, gD.sum()
 
@@ -77,15 +87,21 @@ def argmax_fwd(z, noise_a, gamma):
     return w.mean(dim=0), w, vr
 
 
-def argmax_bwd(w, vr, noise_a, gamma, gW):
-    """smoothagg.py:50-56,71-72: a_s = <gW, w_s - vr'> ; dz = mean_s(a_s*eps_s/gamma) ;
-    d gamma = mean_s sum_{pix,j} gW*(w_s-vr')*(|eps_s|^2 - 1)/gamma
-    (|eps_s|^2 over all K+1 logits, masked slots included)."""
+def argmax_bwd(w, vr, noise_a, gamma, gW, kind="gaussian", use_vr=True):
+    """smoothagg.py:50-56,71-72 (and :118-124 wovr): a_s = <gW, diff_s> with diff = w_s - vr'
+    (variance-reduced, and always for Cauchy) or w_s (Gaussian _wovr);
+    dz = mean_s(a_s*score(eps_s)/gamma) ;
+    d gamma = mean_s sum_{pix,j} gW*diff_s*(n_s - 1)/gamma with n_s = |eps_s|^2 (Gaussian) or
+    sum_j score(eps_sj)*eps_sj (Cauchy), over all K+1 logits, masked slots included."""
     gamma = _t(gamma)
-    diff = w - vr.unsqueeze(0)
+    diff = (w - vr.unsqueeze(0)) if (use_vr or kind == "cauchy") else w
     a = (gW.unsqueeze(0) * diff).sum(-1, keepdim=True)
-    dz = (a * noise_a / gamma).mean(dim=0)
-    n2 = torch.square(torch.norm(noise_a, dim=-1, keepdim=True))
+    sc = score(noise_a, kind)
+    dz = (a * sc / gamma).mean(dim=0)
+    if kind == "gaussian":
+        n2 = torch.square(torch.norm(noise_a, dim=-1, keepdim=True))
+    else:
+        n2 = (sc * noise_a).sum(-1, keepdim=True)
     gg = (gW.unsqueeze(0) * (diff * (n2 - 1.0) / gamma)).sum(dim=(1, 2, 3, 4)).mean(dim=0)
     return dz, gg
 
@@ -127,7 +143,8 @@ def _prod_backward(x, g):
 
 # ---------------------------------------------------------------------------- blend
 def blend_forward(p2f, dists, zbuf, colors, noise_r, noise_a, sigma, gamma, alpha, eps,
-                  background, znear, zfar):
+                  background, znear, zfar, rast_kind="gaussian", rast_vr=True, agg_kind="gaussian",
+                  agg_vr=True):
     """random_rasterizer.py:34-56 with GaussianRast/GaussianAgg, injected noise.
 
     znear/zfar: (N,1,1,1) float32 tensors (random_rasterizer.py:172-173).
@@ -148,7 +165,8 @@ def blend_forward(p2f, dists, zbuf, colors, noise_r, noise_a, sigma, gamma, alph
     img[..., 3] = 1.0 - alpha_chan                                     # :54
     saved = dict(mask=mask, maps=maps, vr=vr, prob=prob, one_minus=one_minus, aux=aux, w=w,
                  vra=vra, W=Wt, colors=colors, bg=bg, zfar=zfar, znear=znear, noise_r=noise_r,
-                 noise_a=noise_a, sigma=sigma, gamma=gamma, alpha=alpha, eps=eps, P=P)
+                 noise_a=noise_a, sigma=sigma, gamma=gamma, alpha=alpha, eps=eps, P=P,
+                 kinds=(rast_kind, rast_vr, agg_kind, agg_vr))
     return img, saved
 
 
@@ -161,31 +179,35 @@ def blend_backward(gimg, s):
     dW = torch.cat(((g_rgb[..., None, :] * s["colors"]).sum(-1),
                     (g_rgb * s["bg"]).sum(-1, keepdim=True)), dim=-1)
     dcolors = s["W"][..., :-1, None] * g_rgb[..., None, :]
-    dz, dg1 = argmax_bwd(s["w"], s["vra"], s["noise_a"], s["gamma"], dW)
+    rk, rvr, ak, avr = s.get("kinds", ("gaussian", True, "gaussian", True))
+    dz, dg1 = argmax_bwd(s["w"], s["vra"], s["noise_a"], s["gamma"], dW, ak, avr)
     dzbuf, dprob_l, dg2, dalpha = logits_bwd(dz, s["prob"], s["mask"], s["zfar"], s["znear"],
                                              s["gamma"], s["alpha"], s["eps"], s["aux"])
     # alpha channel: A = 1 - prod(1 - prob)  (:48,:54)
     dprob_a = -_prod_backward(s["one_minus"], -g_a)
     dprob = dprob_a + dprob_l
     dP = dprob * s["mask"]                                             # :47
-    dD, dsigma = heaviside_bwd(s["maps"], s["vr"], s["noise_r"], s["sigma"], dP)
+    dD, dsigma = heaviside_bwd(s["maps"], s["vr"], s["noise_r"], s["sigma"], dP, rk, rvr)
     return dict(dists=-dD, zbuf=dzbuf, colors=dcolors, sigma=dsigma, gamma=dg1 + dg2,
                 alpha=dalpha)
 
 
 # --------------------------------------------------------------- standalone methods
-def rasterize_forward_backward(dists, noise_r, sigma, gP):
-    """GaussianRast.rasterize (smoothrast.py:144-147) and its backward."""
+def rasterize_forward_backward(dists, noise_r, sigma, gP, kind="gaussian", use_vr=True):
+    """GaussianRast / ArctanRast / GaussianRast_wovr .rasterize (smoothrast.py:144-173) and
+    the backward."""
     P, maps, vr = heaviside_fwd(-dists, noise_r, sigma)
-    dD, dsigma = heaviside_bwd(maps, vr, noise_r, sigma, gP)
+    dD, dsigma = heaviside_bwd(maps, vr, noise_r, sigma, gP, kind, use_vr)
     return P, -dD, dsigma
 
 
-def aggregate_forward_backward(zbuf, zfar, znear, prob, mask, noise_a, gamma, alpha, eps, gW):
-    """GaussianAgg.aggregate (smoothagg.py:196-205) and its backward."""
+def aggregate_forward_backward(zbuf, zfar, znear, prob, mask, noise_a, gamma, alpha, eps, gW,
+                               kind="gaussian", use_vr=True):
+    """GaussianAgg / CauchyAgg / GaussianAgg_wovr .aggregate (smoothagg.py:196-250) and the
+    backward."""
     z, aux = logits(zbuf, zfar, znear, prob, mask, gamma, alpha, eps)
     Wt, w, vra = argmax_fwd(z, noise_a, gamma)
-    dz, dg1 = argmax_bwd(w, vra, noise_a, gamma, gW)
+    dz, dg1 = argmax_bwd(w, vra, noise_a, gamma, gW, kind, use_vr)
     dzbuf, dprob, dg2, dalpha = logits_bwd(dz, prob, mask, zfar, znear, gamma, alpha, eps, aux)
     return Wt, dzbuf, dprob, dg1 + dg2, dalpha
 

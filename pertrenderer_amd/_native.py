@@ -17,6 +17,11 @@ PR_NOISE_PHILOX = 0
 PR_NOISE_INJECTED = 1
 PR_BLEND_RAST = 1
 PR_BLEND_COLOR = 2
+PR_BLEND_VERTEX = 4
+PR_BLEND_RAST_CAUCHY = 8
+PR_BLEND_AGG_CAUCHY = 16
+PR_BLEND_RAST_WOVR = 32
+PR_BLEND_AGG_WOVR = 64
 
 _vp = C.c_void_p
 
@@ -35,7 +40,7 @@ class PRBlendParams(C.Structure):
 class PRBlendFwdArgs(C.Structure):
     _fields_ = [("p", PRBlendParams), ("pix_to_face", _vp), ("mask", _vp), ("dists", _vp),
                 ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("image", _vp), ("weights", _vp),
-                ("winners", _vp), ("rast_cache", _vp)]
+                ("winners", _vp), ("rast_cache", _vp), ("bary", _vp), ("faces", _vp), ("vert_colors", _vp)]
 
 
 class PRBlendBwdArgs(C.Structure):
@@ -43,7 +48,8 @@ class PRBlendBwdArgs(C.Structure):
                 ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("winners", _vp),
                 ("grad_image", _vp), ("grad_weights", _vp), ("grad_dists", _vp), ("grad_prob", _vp),
                 ("grad_zbuf", _vp), ("grad_colors", _vp), ("grad_scalars", _vp),
-                ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("rast_cache", _vp)]
+                ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("rast_cache", _vp), ("bary", _vp),
+                ("faces", _vp), ("vert_colors", _vp), ("grad_bary", _vp), ("grad_vert_colors", _vp)]
 
 
 class PRHeavisideArgs(C.Structure):
@@ -51,7 +57,8 @@ class PRHeavisideArgs(C.Structure):
                 ("Sr", C.c_int32), ("sample_offset_r", C.c_int32), ("noise_mode", C.c_int32),
                 ("sigma", C.c_float), ("seed_r", C.c_uint64), ("noise_r", _vp), ("dists", _vp),
                 ("prob", _vp), ("grad_prob", _vp), ("grad_dists", _vp), ("grad_sigma", _vp),
-                ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("sigma_dev", _vp), ("seeds", _vp)]
+                ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("sigma_dev", _vp), ("seeds", _vp),
+                ("flags", C.c_int32)]
 
 
 class PRRastArgs(C.Structure):
@@ -110,7 +117,7 @@ EXPORTS = {
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
 }
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib = None
 

@@ -58,6 +58,23 @@ def _scalars(vals, device):
     return tuple(float(v.detach().cpu()) if torch.is_tensor(v) else float(v) for v in vals), None
 
 
+KINDS = ("gaussian", "cauchy")
+
+
+def variant_flags(rast_kind="gaussian", rast_vr=True, agg_kind="gaussian", agg_vr=True):
+    """PR_BLEND_* noise-variant bits: ArctanRast (Cauchy rast), GaussianRast_wovr, CauchyAgg,
+    GaussianAgg_wovr."""
+    for k in (rast_kind, agg_kind):
+        if k not in KINDS:
+            raise NotImplementedError(f"noise type {k!r} not implemented (gaussian, cauchy)")
+    f = 0
+    f |= nat.PR_BLEND_RAST_CAUCHY if rast_kind == "cauchy" else 0
+    f |= nat.PR_BLEND_AGG_CAUCHY if agg_kind == "cauchy" else 0
+    f |= 0 if rast_vr else nat.PR_BLEND_RAST_WOVR
+    f |= 0 if agg_vr else nat.PR_BLEND_AGG_WOVR
+    return f
+
+
 def _params(shape, Sr, Sa, sc, sc_dev, eps, bg, noise, znear, zfar, flags):
     N, H, W, K = shape
     p = nat.PRBlendParams()
@@ -133,7 +150,7 @@ class _FusedBlendFn(torch.autograd.Function):
         noise = cfg["noise"].to(dev)
         sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
         p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf,
-                    nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR)
+                    nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | cfg["vflags"])
         image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
         # per-slot (prob, rast score) kept for the backward instead of regenerating rast noise
@@ -156,7 +173,7 @@ class _FusedBlendFn(torch.autograd.Function):
         N, H, W, K = p2f_c.shape
         dev = p2f_c.device
         p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf,
-                    nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR)
+                    nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | cfg["vflags"])
         g = gimg.detach().to(F32).contiguous()
         gd, gz, gc = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(c_c)
         gsc = torch.empty(3, dtype=F32, device=dev)
@@ -174,10 +191,100 @@ class _FusedBlendFn(torch.autograd.Function):
                 s_g, g_g, a_g, None, None, None, None)
 
 
+class _FusedVertexBlendFn(torch.autograd.Function):
+    """perturbed_blend with TexturesVertex sampling fused in: slot colours are
+    interpolated from per-vertex colours on demand (PR_BLEND_VERTEX); gradients go
+    to bary (-> rasterizer backward) and the vertex colours instead of a texel tensor."""
+
+    @staticmethod
+    def forward(ctx, dists, zbuf, bary, vert_colors, sigma, gamma, alpha, p2f, faces, znear, zfar, cfg):
+        nat.require_device(dists, zbuf, bary, vert_colors, p2f, faces)
+        lib = nat.load()
+        N, H, W, K = p2f.shape
+        dev = p2f.device
+        p2f_c = p2f.detach().to(torch.int64).contiguous()
+        f_c = faces.detach().to(torch.int64).contiguous()
+        d_c, z_c, b_c, v_c = _contig(dists), _contig(zbuf), _contig(bary), _contig(vert_colors)
+        zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
+        noise = cfg["noise"].to(dev)
+        sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
+        flags = nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | nat.PR_BLEND_VERTEX | cfg["vflags"]
+        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf, flags)
+        image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
+        winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
+        need = ctx.needs_input_grad
+        cache = torch.empty((N, H, W, K, 2), dtype=F32, device=dev) if RAST_CACHE and any(need[:7]) else None
+        a = nat.PRBlendFwdArgs()
+        a.p = p
+        a.pix_to_face, a.dists, a.zbuf = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c)
+        a.bary, a.faces, a.vert_colors = nat.ptr(b_c), nat.ptr(f_c), nat.ptr(v_c)
+        a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
+        _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
+        ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, sc_dev, cache)
+        ctx.cfg, ctx.noise, ctx.sc, ctx.flags = cfg, noise, sc, flags
+        ctx.refs = (sigma, gamma, alpha)
+        return image
+
+    @staticmethod
+    def backward(ctx, gimg):
+        p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, sc_dev, cache = ctx.saved_tensors
+        cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
+        lib = nat.load()
+        N, H, W, K = p2f_c.shape
+        dev = p2f_c.device
+        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf, ctx.flags)
+        need = ctx.needs_input_grad
+        g = gimg.detach().to(F32).contiguous()
+        gd, gz, gb = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(b_c)
+        gv = torch.zeros_like(v_c) if need[3] else None
+        gsc = torch.empty(3, dtype=F32, device=dev)
+        a = nat.PRBlendBwdArgs()
+        a.p = p
+        a.pix_to_face, a.dists, a.zbuf = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c)
+        a.bary, a.faces, a.vert_colors = nat.ptr(b_c), nat.ptr(f_c), nat.ptr(v_c)
+        a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
+        a.grad_dists, a.grad_zbuf, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gsc)
+        a.grad_bary, a.grad_vert_colors = nat.ptr(gb), nat.ptr(gv)
+        ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
+        _timed("blend_bwd", lambda: nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd"))
+        s_g, g_g, a_g = _scalar_grads(gsc, need[4:7], ctx.refs)
+        return (gd if need[0] else None, gz if need[1] else None, gb if need[2] else None, gv,
+                s_g, g_g, a_g, None, None, None, None, None)
+
+
+def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, sigma, gamma, alpha,
+                           nb_samples_rast, nb_samples_agg, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0,
+                           zfar=100.0, noise=None, fixed_noise=False, rast_kind="gaussian", rast_vr=True,
+                           agg_kind="gaussian", agg_vr=True):
+    """perturbed_blend(TexturesVertex(vert_colors).sample_textures(fragments), ...) as one native op:
+    colours are interpolated only where a slot wins a Monte-Carlo sample (no texel tensor).
+    vert_colors (V,3) and faces (F,3) are the packed mesh tensors; gradients flow to
+    dists, zbuf, bary, vert_colors and the smoothing scalars."""
+    shape = tuple(pix_to_face.shape)
+    N, H, W, K = shape
+    if tuple(bary.shape) != shape + (3,) or vert_colors.dim() != 2 or vert_colors.shape[-1] != 3:
+        raise ValueError("bary must be (N,H,W,K,3) and vert_colors (V,3)")
+    if tuple(dists.shape) != shape or tuple(zbuf.shape) != shape:
+        raise ValueError("dists / zbuf must match pix_to_face's shape")
+    vflags = variant_flags(rast_kind, rast_vr, agg_kind, agg_vr)
+    if noise is None:
+        nr = noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device, rast_kind)
+        na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind)
+        noise = _merge(nr, na)
+    _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
+    cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
+               bg=_background(background), noise=noise, vflags=vflags)
+    return _FusedVertexBlendFn.apply(dists, zbuf, bary, vert_colors, sigma, gamma, alpha, pix_to_face, faces,
+                                     znear, zfar, cfg)
+
+
 def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_samples_rast,
                     nb_samples_agg, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0, zfar=100.0,
-                    noise=None, fixed_noise=False):
-    """smooth_rgb_blend(colors, fragments, GaussianRast, GaussianAgg, ...) as one native op.
+                    noise=None, fixed_noise=False, rast_kind="gaussian", rast_vr=True, agg_kind="gaussian",
+                    agg_vr=True):
+    """smooth_rgb_blend(colors, fragments, <Rast>, <Agg>, ...) as one native op, for the
+    Gaussian / Cauchy, with / without variance reduction operator pairs.
 
     Returns the (N,H,W,4) image; differentiable w.r.t. dists, zbuf, colors and the
     0-d smoothing tensors sigma, gamma, alpha."""
@@ -187,20 +294,22 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
         raise ValueError(f"colors must be (N,H,W,K,3) = {shape + (3,)}, got {tuple(colors.shape)}")
     if tuple(dists.shape) != shape or tuple(zbuf.shape) != shape:
         raise ValueError("dists / zbuf must match pix_to_face's shape")
+    vflags = variant_flags(rast_kind, rast_vr, agg_kind, agg_vr)
     if noise is None:
-        nr = noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device)
-        na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise)
+        nr = noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device, rast_kind)
+        na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind)
         noise = _merge(nr, na)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
-               bg=_background(background), noise=noise)
+               bg=_background(background), noise=noise, vflags=vflags)
     return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, pix_to_face, znear, zfar, cfg)
 
 
 # ==================================================== standalone heaviside
-def _heaviside_args(shape, Sr, noise, sigma_val, sigma_dev, d_c):
+def _heaviside_args(shape, Sr, noise, sigma_val, sigma_dev, d_c, flags=0):
     N, H, W, K = shape
     a = nat.PRHeavisideArgs()
+    a.flags = flags
     a.N, a.H, a.W, a.K, a.Sr = N, H, W, K, int(Sr)
     a.sample_offset_r, a.noise_mode, a.sigma = noise.offset_r, noise.mode, sigma_val
     a.seed_r, a.noise_r, a.dists = noise.seed_r & (2 ** 64 - 1), nat.ptr(noise.noise_r), nat.ptr(d_c)
@@ -210,25 +319,25 @@ def _heaviside_args(shape, Sr, noise, sigma_val, sigma_dev, d_c):
 
 class _HeavisideFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, dists, sigma, Sr, noise):
+    def forward(ctx, dists, sigma, Sr, noise, flags):
         nat.require_device(dists)
         lib = nat.load()
         d_c = _contig(dists)
         noise = noise.to(d_c.device)
         (sv,), sdev = _scalars((sigma,), d_c.device)
-        a = _heaviside_args(tuple(d_c.shape), Sr, noise, sv, sdev, d_c)
+        a = _heaviside_args(tuple(d_c.shape), Sr, noise, sv, sdev, d_c, flags)
         prob = torch.empty_like(d_c)
         a.prob = nat.ptr(prob)
         nat.check(lib.pr_heaviside_fwd(a, nat.stream_of(prob)), "pr_heaviside_fwd")
         ctx.save_for_backward(d_c, sdev)
-        ctx.noise, ctx.Sr, ctx.sv, ctx.sigma_ref = noise, int(Sr), sv, sigma
+        ctx.noise, ctx.Sr, ctx.sv, ctx.sigma_ref, ctx.flags = noise, int(Sr), sv, sigma, flags
         return prob
 
     @staticmethod
     def backward(ctx, gP):
         d_c, sdev = ctx.saved_tensors
         lib = nat.load()
-        a = _heaviside_args(tuple(d_c.shape), ctx.Sr, ctx.noise, ctx.sv, sdev, d_c)
+        a = _heaviside_args(tuple(d_c.shape), ctx.Sr, ctx.noise, ctx.sv, sdev, d_c, ctx.flags)
         g = gP.detach().to(F32).contiguous()
         gd = torch.empty_like(d_c)
         gs = torch.empty(1, dtype=F32, device=d_c.device)
@@ -239,17 +348,19 @@ class _HeavisideFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         ref = ctx.sigma_ref
         sg = gs[0].to(ref.dtype) if (need[1] and torch.is_tensor(ref)) else None
-        return (gd if need[0] else None), sg, None, None
+        return (gd if need[0] else None), sg, None, None, None
 
 
-def perturbed_heaviside(dists, sigma, nb_samples, noise=None):
-    """GaussianRast.rasterize(dists): P = mean_s H(-dists + sigma*eps_s) (smoothrast.py:144-147)."""
+def perturbed_heaviside(dists, sigma, nb_samples, noise=None, kind="gaussian", variance_reduction=True):
+    """GaussianRast / ArctanRast (kind="cauchy") / GaussianRast_wovr (variance_reduction=False)
+    .rasterize(dists): P = mean_s H(-dists + sigma*eps_s) (smoothrast.py:144-173)."""
     if dists.dim() != 4:
         raise ValueError("dists must be (N,H,W,K)")
+    flags = variant_flags(rast_kind=kind, rast_vr=variance_reduction)
     if noise is None:
-        noise = noise_mod.draw_rast(tuple(dists.shape), nb_samples, dists.device)
+        noise = noise_mod.draw_rast(tuple(dists.shape), nb_samples, dists.device, kind)
     _check_injected(noise, nb_samples, 0, tuple(dists.shape), True, False)
-    return _HeavisideFn.apply(dists, sigma, int(nb_samples), noise)
+    return _HeavisideFn.apply(dists, sigma, int(nb_samples), noise, flags)
 
 
 # ==================================================== standalone aggregate
@@ -266,7 +377,8 @@ class _AggregateFn(torch.autograd.Function):
         noise = cfg["noise"].to(dev)
         one = torch.ones((), dtype=F32, device=dev) if (torch.is_tensor(gamma) and gamma.is_cuda) else 1.0
         sc, sc_dev = _scalars((one, gamma, alpha), dev)
-        p = _params((N, H, W, K), 1, cfg["Sa"], sc, sc_dev, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf, 0)
+        p = _params((N, H, W, K), 1, cfg["Sa"], sc, sc_dev, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf,
+                    cfg["vflags"])
         weights = torch.empty((N, H, W, K + 1), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
         a = nat.PRBlendFwdArgs()
@@ -285,7 +397,8 @@ class _AggregateFn(torch.autograd.Function):
         lib = nat.load()
         N, H, W, K = z_c.shape
         dev = z_c.device
-        p = _params((N, H, W, K), 1, cfg["Sa"], sc, sc_dev, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf, 0)
+        p = _params((N, H, W, K), 1, cfg["Sa"], sc, sc_dev, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf,
+                    cfg["vflags"])
         g = gW.detach().to(F32).contiguous()
         gz, gp = torch.empty_like(z_c), torch.empty_like(p_c)
         gsc = torch.empty(3, dtype=F32, device=dev)
@@ -302,13 +415,15 @@ class _AggregateFn(torch.autograd.Function):
 
 
 def perturbed_aggregate(zbuf, zfar, znear, prob_map, mask, gamma, alpha, nb_samples, eps=1e-10,
-                        noise=None, fixed_noise=False):
-    """GaussianAgg.aggregate(zbuf, zfar, znear, prob_map, mask) -> (N,H,W,K+1) weights."""
+                        noise=None, fixed_noise=False, kind="gaussian", variance_reduction=True):
+    """GaussianAgg / CauchyAgg (kind="cauchy") / GaussianAgg_wovr (variance_reduction=False)
+    .aggregate(zbuf, zfar, znear, prob_map, mask) -> (N,H,W,K+1) weights (smoothagg.py:196-250)."""
     N, H, W, K = zbuf.shape
+    vflags = variant_flags(agg_kind=kind, agg_vr=variance_reduction)
     if noise is None:
-        noise = noise_mod.draw_agg((N, H, W, K + 1), nb_samples, zbuf.device, fixed_noise)
+        noise = noise_mod.draw_agg((N, H, W, K + 1), nb_samples, zbuf.device, fixed_noise, kind)
     _check_injected(noise, 0, nb_samples, (N, H, W, K), False, True)
     mask = mask.expand(N, H, W, K) if mask.shape != zbuf.shape else mask
     prob_map = prob_map.expand(N, H, W, K) if prob_map.shape != zbuf.shape else prob_map
-    cfg = dict(Sa=int(nb_samples), eps=float(eps), noise=noise)
+    cfg = dict(Sa=int(nb_samples), eps=float(eps), noise=noise, vflags=vflags)
     return _AggregateFn.apply(zbuf, prob_map, gamma, alpha, mask, znear, zfar, cfg)

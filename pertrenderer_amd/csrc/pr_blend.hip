@@ -82,8 +82,9 @@ PR_DEV int image_of(int n0, int rem0, int pl, int HW) {
 // ---------------------------------------------------------------- rast noise
 // Both noise modes evaluate smoothrast.py:32-33 literally, m_s = H(D + sigma*eps_s)
 // with H(0)=1 and D = -dist; Philox mode draws eps_s by Box-Muller (4 per Philox
-// block, gauss4).  Box-Muller normals from 24-bit uniforms satisfy |eps| <= 5.7683,
-// so a slot with |dist/sigma| > 5.8 has the same outcome for every sample: exact skip.
+// block, gauss4) or, for ArctanRast, as Cauchy samples (cauchy4).  Box-Muller normals
+// from 24-bit uniforms satisfy |eps| <= 5.7683, so with Gaussian noise a slot with
+// |dist/sigma| > 5.8 has the same outcome for every sample: exact skip.
 PR_DEV float pick4(const float e[4], uint32_t i) {
   return i == 0 ? e[0] : (i == 1 ? e[1] : (i == 2 ? e[2] : e[3]));
 }
@@ -103,20 +104,26 @@ PR_DEV int rast_count(const PRBlendParams& p, const Sc& sc, float dist, uint32_t
   if constexpr (NOISE == PR_NOISE_INJECTED) {
     for (int s = 0; s < p.Sr; ++s) cnt += (D + sc.sigma * p.noise_r[(int64_t)s * PK + gs]) >= 0.f ? 1 : 0;
   } else {
-    const int sat = rast_saturated(dist, sc.sigma);
-    if (sat) return sat < 0 ? p.Sr : 0;
+    const bool cauchy = p.flags & PR_BLEND_RAST_CAUCHY;
+    if (!cauchy) {
+      const int sat = rast_saturated(dist, sc.sigma);
+      if (sat) return sat < 0 ? p.Sr : 0;
+    }
     float e[4];
     for (int s = 0; s < p.Sr; ++s) {
       const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
-      if (s == 0 || (sg & 3u) == 0) gauss4(philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast), e);
+      if (s == 0 || (sg & 3u) == 0) {
+        const U4 u = philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast);
+        if (cauchy) cauchy4(u, e); else gauss4(u, e);
+      }
       cnt += (D + sc.sigma * pick4(e, sg & 3u)) >= 0.f ? 1 : 0;
     }
   }
   return cnt;
 }
 
-// Count and the variance-reduced score sum_s ((m_s - vr) * eps_s) / sigma
-// (smoothrast.py:46,53).
+// Count and the score sum_s (base_s * score(eps_s)) / sigma with base = m_s - vr
+// (smoothrast.py:46,49,53) or m_s (_wovr, :95,98), score = eps or 2 eps / (1 + eps^2).
 template <int NOISE>
 PR_DEV int rast_count_score(const PRBlendParams& p, const Sc& sc, float dist, uint32_t gp, int k, int64_t gs,
                             int64_t PK, float& gacc) {
@@ -124,24 +131,30 @@ PR_DEV int rast_count_score(const PRBlendParams& p, const Sc& sc, float dist, ui
   const float D = -dist;
   const float vr = heaviside1(D);
   gacc = 0.f;
+  const bool cauchy = p.flags & PR_BLEND_RAST_CAUCHY, wovr = p.flags & PR_BLEND_RAST_WOVR;
   if constexpr (NOISE == PR_NOISE_INJECTED) {
     for (int s = 0; s < p.Sr; ++s) {
       const float e = p.noise_r[(int64_t)s * PK + gs];
       const float m = heaviside1(D + sc.sigma * e);
       cnt += (int)m;
-      gacc += ((m - vr) * e) / sc.sigma;
+      gacc += ((wovr ? m : m - vr) * noise_score(e, cauchy)) / sc.sigma;
     }
   } else {
-    const int sat = rast_saturated(dist, sc.sigma);
-    if (sat) return sat < 0 ? p.Sr : 0;  // m_s = vr for every sample: no score
+    if (!cauchy && !wovr) {
+      const int sat = rast_saturated(dist, sc.sigma);
+      if (sat) return sat < 0 ? p.Sr : 0;  // m_s = vr for every sample: no score
+    }
     float e[4];
     for (int s = 0; s < p.Sr; ++s) {
       const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
-      if (s == 0 || (sg & 3u) == 0) gauss4(philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast), e);
+      if (s == 0 || (sg & 3u) == 0) {
+        const U4 u = philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast);
+        if (cauchy) cauchy4(u, e); else gauss4(u, e);
+      }
       const float ee = pick4(e, sg & 3u);
       const float m = heaviside1(D + sc.sigma * ee);
       cnt += (int)m;
-      gacc += ((m - vr) * ee) / sc.sigma;
+      gacc += ((wovr ? m : m - vr) * noise_score(ee, cauchy)) / sc.sigma;
     }
   }
   return cnt;
@@ -161,7 +174,8 @@ PR_DEV void agg_noise4(const PRBlendParams& p, const Sc& sc, uint32_t gp, int j,
       e[i] = s < p.Sa ? p.noise_a[(int64_t)s * PKa + (int64_t)gp * KP1 + j] : 0.f;
     }
   } else {
-    gauss4(philox_block(sc.ka, gp, (uint32_t)j, g, kTagAgg), e);
+    const U4 u = philox_block(sc.ka, gp, (uint32_t)j, g, kTagAgg);
+    if (p.flags & PR_BLEND_AGG_CAUCHY) cauchy4(u, e); else gauss4(u, e);
   }
 }
 
@@ -170,8 +184,28 @@ PR_DEV int agg_num_groups(const PRBlendParams& p) {
   return ((p.sample_offset_a + p.Sa - 1) >> 2) - (p.sample_offset_a >> 2) + 1;
 }
 
+// Colour of slot gs: texel tensor (CM 1) or interpolated on demand from per-vertex
+// colours (CM 2; the same operation order as interp_fwd_kernel, so the result is
+// bit-identical to sampling the texels first).
+template <int CM, typename A>
+PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
+  if constexpr (CM == 2) {
+    const int64_t f = a.pix_to_face[gs];
+    if (f < 0) { c[0] = c[1] = c[2] = 0.f; return; }
+    const float w0 = a.bary[gs * 3], w1 = a.bary[gs * 3 + 1], w2 = a.bary[gs * 3 + 2];
+    const float* r0 = a.vert_colors + a.faces[f * 3] * 3;
+    const float* r1 = a.vert_colors + a.faces[f * 3 + 1] * 3;
+    const float* r2 = a.vert_colors + a.faces[f * 3 + 2] * 3;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) c[d] = (w0 * r0[d] + w1 * r1[d]) + w2 * r2[d];
+  } else {
+    c[0] = a.colors[gs * 3]; c[1] = a.colors[gs * 3 + 1]; c[2] = a.colors[gs * 3 + 2];
+  }
+}
+
 // ================================================================== forward
-template <int NOISE, bool RAST, bool COLOR>
+// CM: colour mode, 0 = weights out (no colour), 1 = texel colours, 2 = vertex colours
+template <int NOISE, bool RAST, int CM>
 __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, Geo g, int NC) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
@@ -258,7 +292,9 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
     const int ng = agg_num_groups(p), g0 = agg_first_group(p);
     const int CS = (KP1 + NC - 1) / NC;
     const int npairs = npix * ng * NC;
-    const float skipm = NOISE == PR_NOISE_PHILOX ? 2.f * kEpsMaxBM * sc.gamma : __builtin_inff();
+    // bounded (Box-Muller) noise only: a logit this far below the best can never win
+    const float skipm = NOISE == PR_NOISE_PHILOX && !(p.flags & PR_BLEND_AGG_CAUCHY) ? 2.f * kEpsMaxBM * sc.gamma
+                                                                                    : __builtin_inff();
     for (int base = 0; base < npairs; base += kThreads) {
       const int t = base + tid;
       const bool act = t < npairs;
@@ -309,19 +345,20 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
 
   // ---- 4: outputs
   const float fSa = (float)p.Sa;
-  if constexpr (COLOR) {
-    // 8 lanes per pixel sweep the pixel's contiguous K*3 colours (8 slots = 96 B per step)
+  if constexpr (CM != 0) {
+    // 8 lanes per pixel sweep the pixel's slots; only slots that won a sample are read
     const int pl = tid >> 3, l = tid & 7;
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
     if (pl < npix) {
-      const float* col = a.colors + (pix0 + pl) * K * 3;
       for (int k = l; k < K; k += 8) {
         const int cw = CNT[pl * KP1 + k];
         if (cw == 0) continue;
         const float w = (float)cw / fSa;
-        acc0 += w * col[k * 3 + 0];
-        acc1 += w * col[k * 3 + 1];
-        acc2 += w * col[k * 3 + 2];
+        float c[3];
+        slot_color<CM>(a, (pix0 + pl) * K + k, c);
+        acc0 += w * c[0];
+        acc1 += w * c[1];
+        acc2 += w * c[2];
       }
     }
 #pragma unroll
@@ -347,7 +384,7 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
 }
 
 // ================================================================= backward
-template <int NOISE, bool RAST, bool COLOR>
+template <int NOISE, bool RAST, int CM>
 __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
@@ -399,18 +436,18 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
       PR[pl * KP1 + k] = prob;
       ZZ[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
       GM[pl * KP1 + k] = gm;
-      float dw;
-      if constexpr (COLOR) {
+      float dw = 0.f;  // CM 2: computed on demand in B5 (only winners and j0 need it)
+      if constexpr (CM == 1) {
         const float* gi = a.grad_image + gp * 4;
         const float* c = a.colors + gs * 3;
         dw = (gi[0] * c[0] + gi[1] * c[1]) + gi[2] * c[2];
-      } else {
+      } else if constexpr (CM == 0) {
         dw = a.grad_weights[gp * KP1 + k];
       }
       DW[pl * KP1 + k] = dw;
     } else {
       float dw;
-      if constexpr (COLOR) {
+      if constexpr (CM != 0) {
         const float* gi = a.grad_image + gp * 4;
         dw = (gi[0] * p.background[0] + gi[1] * p.background[1]) + gi[2] * p.background[2];
       } else {
@@ -443,7 +480,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     }
     if (km == (1 << 30)) km = 0;
     const float zmax = zm < p.eps ? p.eps : zm;
-    if constexpr (COLOR) {
+    if constexpr (CM != 0) {
       // exclusive products across the 8 lane chunks, then within the chunk
       float pre = 1.f, suf = 1.f;
       const int lane8 = (tid & 63) & ~7;
@@ -491,16 +528,38 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     const int64_t gp = pix0 + pl;
     const int jw = a.winners[gp * Sa + s];
     const int j0 = (int)PX[pl * 8 + 3];
-    const float as = DW[pl * KP1 + jw] - DW[pl * KP1 + j0];
+    // GaussianAgg_wovr: a_s = <g, w_s> (smoothagg.py:118); else <g, w_s - vr'>
+    const bool nobase = (p.flags & PR_BLEND_AGG_WOVR) && !(p.flags & PR_BLEND_AGG_CAUCHY);
+    float as;
+    if constexpr (CM == 2) {  // dW_j = g_rgb . colour_j for the two slots involved
+      const float* gi = a.grad_image + gp * 4;
+      float dw2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = e == 0 ? jw : j0;
+        if (j == K) {
+          dw2[e] = DW[pl * KP1 + K];
+        } else {
+          float c[3];
+          slot_color<CM>(a, gp * K + j, c);
+          dw2[e] = (gi[0] * c[0] + gi[1] * c[1]) + gi[2] * c[2];
+        }
+      }
+      as = nobase ? dw2[0] : dw2[0] - dw2[1];
+    } else {
+      as = nobase ? DW[pl * KP1 + jw] : DW[pl * KP1 + jw] - DW[pl * KP1 + j0];
+    }
     AS[pl * Sa + s] = as;
     part_a += as;
     atomicAdd(&CN[pl * KP1 + jw], 1);
   }
   __syncthreads();
 
-  // ---- B6: dz_j = mean_s(a_s * eps_sj / gamma) and sum_s a_s * eps_sj^2 (d gamma)
+  // ---- B6: dz_j = mean_s(a_s * score(eps_sj) / gamma) and sum_s a_s * eps_sj * score(eps_sj)
+  //          (d gamma; score = eps for Gaussian noise, 2 eps / (1 + eps^2) for Cauchy)
   {
     const int ng = agg_num_groups(p), g0 = agg_first_group(p);
+    const bool cauchy = p.flags & PR_BLEND_AGG_CAUCHY;
     PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
       const int j = k;
       const int64_t gp = pix0 + pl;
@@ -522,8 +581,9 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           if (av[r] != 0.f) {
-            dz += (av[r] * e[r]) / sc.gamma;
-            q += av[r] * (e[r] * e[r]);
+            const float scr = noise_score(e[r], cauchy);
+            dz += (av[r] * scr) / sc.gamma;
+            q += av[r] * (e[r] * scr);
           }
         }
       }
@@ -569,7 +629,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     float r = 1.f / prob;
     if (__builtin_isinf(r)) r = 0.f;
     float dprob = r * dL;
-    if constexpr (COLOR) {
+    if constexpr (CM != 0) {
       const float ga = a.grad_image[gp * 4 + 3];
       dprob = -((-ga) * EX[pl * KP1 + k]) + dprob;
     }
@@ -580,13 +640,36 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     } else {
       a.grad_prob[gs] = dprob;
     }
-    if constexpr (COLOR) {
+    if constexpr (CM == 1) {
       const float w = (float)CN[pl * KP1 + k] / (float)Sa;
       const float* gi = a.grad_image + gp * 4;
       float* dc = a.grad_colors + gs * 3;
       dc[0] = w * gi[0];
       dc[1] = w * gi[1];
       dc[2] = w * gi[2];
+    } else if constexpr (CM == 2) {
+      // d colour = w * g_rgb, pushed through the interpolation (interp_bwd_kernel's order)
+      const int cnt = CN[pl * KP1 + k];
+      float gb[3] = {0.f, 0.f, 0.f};
+      const int64_t f = m ? a.pix_to_face[gs] : -1;
+      if (cnt != 0 && f >= 0) {
+        const float w = (float)cnt / (float)Sa;
+        const float* gi = a.grad_image + gp * 4;
+        const float dc[3] = {w * gi[0], w * gi[1], w * gi[2]};
+        const int64_t v[3] = {a.faces[f * 3], a.faces[f * 3 + 1], a.faces[f * 3 + 2]};
+        const float bw[3] = {a.bary[gs * 3], a.bary[gs * 3 + 1], a.bary[gs * 3 + 2]};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            gb[i] += dc[d] * a.vert_colors[v[i] * 3 + d];
+            if (a.grad_vert_colors && dc[d] != 0.f) atomicAdd(&a.grad_vert_colors[v[i] * 3 + d], bw[i] * dc[d]);
+          }
+        }
+      }
+      a.grad_bary[gs * 3] = gb[0];
+      a.grad_bary[gs * 3 + 1] = gb[1];
+      a.grad_bary[gs * 3 + 2] = gb[2];
     }
   }
 
@@ -650,6 +733,7 @@ PR_DEV PRBlendParams heaviside_params(const PRHeavisideArgs& a) {
   p.Sr = a.Sr; p.sample_offset_r = a.sample_offset_r; p.sigma = a.sigma;
   p.seed_r = a.seed_r; p.noise_r = a.noise_r;
   p.seeds = a.seeds;
+  p.flags = a.flags & (PR_BLEND_RAST_CAUCHY | PR_BLEND_RAST_WOVR);
   if (a.sigma_dev) p.sigma = a.sigma_dev[0];
   return p;
 }
@@ -756,22 +840,32 @@ int check_params(const PRBlendParams& p, bool need_rast) {
   return PR_OK;
 }
 
+int color_mode(int flags) {
+  return !(flags & PR_BLEND_COLOR) ? 0 : ((flags & PR_BLEND_VERTEX) ? 2 : 1);
+}
+
 template <int NOISE>
 void launch_fwd(const PRBlendFwdArgs& a, Geo geo, int NC, hipStream_t st, size_t lds, int nblk) {
-  const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
-  if (rast && color) blend_fwd_kernel<NOISE, true, true><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (rast) blend_fwd_kernel<NOISE, true, false><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (color) blend_fwd_kernel<NOISE, false, true><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else blend_fwd_kernel<NOISE, false, false><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  const bool rast = a.p.flags & PR_BLEND_RAST;
+  const int cm = color_mode(a.p.flags);
+  if (rast && cm == 2) blend_fwd_kernel<NOISE, true, 2><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (rast && cm == 1) blend_fwd_kernel<NOISE, true, 1><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (rast) blend_fwd_kernel<NOISE, true, 0><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (cm == 1) blend_fwd_kernel<NOISE, false, 1><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (cm == 2) blend_fwd_kernel<NOISE, false, 2><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else blend_fwd_kernel<NOISE, false, 0><<<nblk, kThreads, lds, st>>>(a, geo, NC);
 }
 
 template <int NOISE>
 void launch_bwd(const PRBlendBwdArgs& a, Geo geo, hipStream_t st, size_t lds, int nblk, float* part) {
-  const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
-  if (rast && color) blend_bwd_kernel<NOISE, true, true><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (rast) blend_bwd_kernel<NOISE, true, false><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (color) blend_bwd_kernel<NOISE, false, true><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else blend_bwd_kernel<NOISE, false, false><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  const bool rast = a.p.flags & PR_BLEND_RAST;
+  const int cm = color_mode(a.p.flags);
+  if (rast && cm == 2) blend_bwd_kernel<NOISE, true, 2><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (rast && cm == 1) blend_bwd_kernel<NOISE, true, 1><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (rast) blend_bwd_kernel<NOISE, true, 0><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (cm == 1) blend_bwd_kernel<NOISE, false, 1><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (cm == 2) blend_bwd_kernel<NOISE, false, 2><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else blend_bwd_kernel<NOISE, false, 0><<<nblk, kThreads, lds, st>>>(a, geo, part);
 }
 
 Geo make_geo(const PRBlendParams& p, int PB) {
@@ -806,8 +900,10 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
   const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
   if (int e = check_params(a.p, rast)) return e;
   if (!a.pix_to_face && !a.mask) return set_error(PR_ERR_ARG, "blend_fwd: need pix_to_face or mask");
+  const int cm = color_mode(a.p.flags);
   if (!a.zbuf || !a.winners || (rast && !a.dists) || (!rast && !a.prob) ||
-      (color && (!a.colors || !a.image)) || (!color && !a.weights))
+      (cm == 1 && (!a.colors || !a.image)) || (!color && !a.weights) ||
+      (cm == 2 && (!a.image || !a.bary || !a.faces || !a.vert_colors || !a.pix_to_face)))
     return set_error(PR_ERR_ARG, "blend_fwd: missing buffer");
   const int KP1 = a.p.K + 1;
   const int PB = pick_pb(KP1, a.p.Sa, false);
@@ -837,7 +933,10 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
   if (!a.pix_to_face && !a.mask) return set_error(PR_ERR_ARG, "blend_bwd: need pix_to_face or mask");
   if (!a.zbuf || !a.winners || !a.grad_zbuf || !a.grad_scalars ||
       (rast && (!a.dists || !a.grad_dists)) || (!rast && (!a.prob || !a.grad_prob)) ||
-      (color && (!a.colors || !a.grad_image || !a.grad_colors)) || (!color && !a.grad_weights))
+      (color_mode(a.p.flags) == 1 && (!a.colors || !a.grad_image || !a.grad_colors)) ||
+      (color_mode(a.p.flags) == 2 && (!a.grad_image || !a.bary || !a.faces || !a.vert_colors ||
+                                      !a.grad_bary || !a.pix_to_face)) ||
+      (!color && !a.grad_weights))
     return set_error(PR_ERR_ARG, "blend_bwd: missing buffer");
   const size_t need = pr_blend_bwd_workspace_size(args);
   if (!a.workspace || a.workspace_bytes < need) return set_error(PR_ERR_WORKSPACE, "blend_bwd: workspace too small");

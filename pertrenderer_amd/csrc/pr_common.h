@@ -5,7 +5,8 @@
 //   yields 4 words = 4 Monte-Carlo samples of one (pixel, slot), so forward and
 //   backward regenerate identical noise without storing it.
 // * Gaussian samples by Box-Muller on the hardware transcendentals
-//   (v_log_f32 = log2, v_sqrt_f32, v_sin/cos_f32 taking revolutions).
+//   (v_log_f32 = log2, v_sqrt_f32, v_sin/cos_f32 taking revolutions); Cauchy
+//   samples as tan(pi (u - 1/2)) on the same sin/cos.
 // * Error plumbing for the C ABI (thread-local message).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -60,6 +61,22 @@ PR_DEV void gauss4(const U4& u, float e[4]) {
   e[2] = r1 * __builtin_amdgcn_cosf(a1);
   e[3] = r1 * __builtin_amdgcn_sinf(a1);
 }
+
+// 4 standard Cauchy samples tan(pi (u - 1/2)) from one Philox block, on the hardware
+// sin/cos (revolutions: angle pi (u - 1/2) = 2 pi t with t = (u - 1/2) / 2), clamped
+// to +-1e7 as the reference clamps its draws (smoothrast.py:24, smoothagg.py:27).
+PR_DEV void cauchy4(const U4& u, float e[4]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float t = (u01(w[i]) - 0.5f) * 0.5f;
+    const float c = __builtin_amdgcn_sinf(t) * __builtin_amdgcn_rcpf(__builtin_amdgcn_cosf(t));
+    e[i] = fminf(fmaxf(c, -1e7f), 1e7f);
+  }
+}
+
+// score function d/d eps (-log density): eps (Gaussian) or 2 eps / (1 + eps^2) (Cauchy)
+PR_DEV float noise_score(float e, bool cauchy) { return cauchy ? (2.f * e) / (1.f + e * e) : e; }
 
 PR_DEV U4 philox_block(uint64_t seed, uint32_t pixel, uint32_t slot, uint32_t group, uint32_t tag) {
   return philox4x32_10(U4{pixel, slot, group, tag}, (uint32_t)seed, (uint32_t)(seed >> 32));

@@ -108,23 +108,33 @@ def use_device_seed(ds):
     _DEVICE_SEED = ds
 
 
-def draw_rast(shape, Sr, device):
+def _torch_draw(kind, shape):
+    """The reference's draws on the CPU generator: torch.normal(0, 1) (smoothrast.py:21,
+    smoothagg.py:21) or Cauchy(0, 1) samples clamped to +-1e7 (smoothrast.py:23-24,
+    smoothagg.py:26-27)."""
+    if kind == "gaussian":
+        return torch.randn(shape)
+    m = torch.distributions.cauchy.Cauchy(torch.tensor([0.0]), torch.tensor([1.0]))
+    return torch.clamp(m.sample(shape).squeeze(-1), min=-1e7, max=1e7)
+
+
+def draw_rast(shape, Sr, device, kind="gaussian"):
     """Noise for one perturbed-Heaviside call over fragments of `shape` (N,H,W,K)."""
     if _SOURCE == "torch":
-        return Noise.injected(noise_r=torch.randn((Sr,) + tuple(shape)).to(device))
+        return Noise.injected(noise_r=_torch_draw(kind, (Sr,) + tuple(shape)).to(device))
     if _DEVICE_SEED is not None:
         return Noise.philox(seed_r=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor)
     return Noise.philox(seed_r=draw_key())
 
 
-def draw_agg(shape, Sa, device, fixed_noise=False):
+def draw_agg(shape, Sa, device, fixed_noise=False, kind="gaussian"):
     """Noise for one perturbed-argmax call over logits of `shape` (N,H,W,K+1).
     fixed_noise reseeds the global generator with 1 first, as smoothagg.py:18-19
     (and then ignores any device seed: the noise must be the same every call)."""
     if fixed_noise:
         torch.manual_seed(1)
     if _SOURCE == "torch":
-        return Noise.injected(noise_a=torch.randn((Sa,) + tuple(shape)).to(device))
+        return Noise.injected(noise_a=_torch_draw(kind, (Sa,) + tuple(shape)).to(device))
     if _DEVICE_SEED is not None and not fixed_noise:
         return Noise.philox(seed_a=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor)
     return Noise.philox(seed_a=draw_key())

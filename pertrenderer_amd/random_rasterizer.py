@@ -16,15 +16,22 @@ import torch.nn as nn
 
 from . import blend as _blend
 from .renderer.cameras import OpenGLPerspectiveCameras, look_at_view_transform
+from .renderer.mesh import TexturesVertex
 from .renderer.renderer import BlendParams, Materials, PointLights
 from .renderer.shading import phong_shading
-from .smoothagg import GaussianAgg, SoftAgg
-from .smoothrast import GaussianRast, SoftRast
+from .smoothagg import GaussianAgg, SoftAgg, _PerturbedAgg
+from .smoothrast import GaussianRast, SoftRast, _PerturbedRast
 
 
 def _is_fusable(smoothrast, smoothagg, fragments):
-    return (type(smoothrast) is GaussianRast and type(smoothagg) is GaussianAgg
+    """A native Monte-Carlo (rast, agg) pair on the GPU: fused into one pr_blend launch."""
+    return (isinstance(smoothrast, _PerturbedRast) and isinstance(smoothagg, _PerturbedAgg)
             and fragments.pix_to_face.is_cuda)
+
+
+def _variant_kw(smoothrast, smoothagg):
+    return dict(rast_kind=smoothrast.noise_kind, rast_vr=smoothrast.variance_reduction,
+                agg_kind=smoothagg.noise_kind, agg_vr=smoothagg.variance_reduction)
 
 
 def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, znear=1.0, zfar=100):
@@ -37,7 +44,7 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
             colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
             smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
             eps=smoothagg.eps, background=background, znear=znear, zfar=zfar,
-            fixed_noise=smoothagg.fixed_noise)
+            fixed_noise=smoothagg.fixed_noise, **_variant_kw(smoothrast, smoothagg))
     if not torch.is_tensor(background):
         background = torch.tensor(background, dtype=torch.float32, device=device)
     else:
@@ -48,6 +55,21 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
     weights = smoothagg.aggregate(fragments.zbuf, zfar, znear, prob_map, mask)
     rgb = (weights[..., :-1, None] * colors).sum(dim=-2) + weights[..., -1:] * background
     return torch.cat([rgb, (1.0 - alpha_chan)[..., None]], dim=-1)
+
+
+# RandomSimpleShader fuses TexturesVertex sampling into the blend on the GPU (set
+# False to sample texels first; results are bit-identical, see tests/test_gpu_fused_texture.py)
+FUSE_VERTEX_TEXTURES = True
+
+
+def _vertex_colors(meshes):
+    """Packed (V,3) per-vertex colours when the mesh's texture is a 3-channel
+    TexturesVertex on the GPU (the fused-sampling case), else None."""
+    tex = getattr(meshes, "textures", None)
+    if not FUSE_VERTEX_TEXTURES or not isinstance(tex, TexturesVertex):
+        return None
+    vc = tex.verts_features_packed()
+    return vc if vc.is_cuda and vc.dim() == 2 and vc.shape[-1] == 3 else None
 
 
 def _planes_from(cameras, kwargs):
@@ -136,9 +158,18 @@ class RandomSimpleShader(_RandomShaderBase):
         if cameras is None:
             raise ValueError("Cameras must be specified either at initialization or in the forward "
                              "pass of RandomSimpleShader")
-        texels = meshes.sample_textures(fragments)
         blend_params = kwargs.get("blend_params", self.blend_params)
         znear, zfar = _planes_from(cameras, kwargs)
+        vc = _vertex_colors(meshes)
+        if vc is not None and _is_fusable(self.smoothrast, self.smoothagg, fragments):
+            # TexturesVertex sampling fused into the blend (no (N,H,W,K,3) texel tensor)
+            sr, sa = self.smoothrast, self.smoothagg
+            return _blend.perturbed_blend_vertex(
+                vc, meshes.faces_packed(), fragments.pix_to_face, fragments.bary_coords, fragments.dists,
+                fragments.zbuf, sr.sigma, sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,
+                background=blend_params.background_color, znear=znear, zfar=zfar, fixed_noise=sa.fixed_noise,
+                **_variant_kw(sr, sa))
+        texels = meshes.sample_textures(fragments)
         return smooth_rgb_blend(texels, fragments, self.smoothrast, self.smoothagg, blend_params,
                                 znear=znear, zfar=zfar)
 

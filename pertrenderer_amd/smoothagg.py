@@ -2,8 +2,9 @@
 
 Mirrors smoothagg.py:145-289: ``gamma`` / ``alpha`` are CPU 0-d leaves with
 requires_grad, ``nb_samples`` an int, ``eps`` the background logit weight.
-``GaussianAgg.aggregate`` runs on the native kernels (pr_blend with flags=0);
-inside ``smooth_rgb_blend`` GaussianRast + GaussianAgg fuse into one launch.
+The Monte-Carlo operators (GaussianAgg, CauchyAgg, GaussianAgg_wovr) run on the
+native kernels (pr_blend without RAST/COLOR, PR_BLEND_AGG_* variant flags); inside
+``smooth_rgb_blend`` they fuse with a native rasterization operator into one launch.
 ``log_corrected`` / ``prod_corrected`` keep the reference's inf/nan-safe
 backward conventions (smoothagg.py:292-337).
 """
@@ -13,6 +14,18 @@ from torch.nn import Module
 from . import blend as _blend
 from . import variants as _variants
 from .variants import log_corrected as _log_c, prod_corrected as _prod_c
+
+
+class _PerturbedAgg:
+    """aggregate() of the Monte-Carlo operators: the native perturbed argmax."""
+
+    noise_kind = "gaussian"
+    variance_reduction = True
+
+    def aggregate(self, zbuf, zfar, znear, prob_map, mask):
+        return _blend.perturbed_aggregate(zbuf, zfar, znear, prob_map, mask, self.gamma, self.alpha,
+                                          self.nb_samples, eps=self.eps, fixed_noise=self.fixed_noise,
+                                          kind=self.noise_kind, variance_reduction=self.variance_reduction)
 
 
 class SmoothAggBase(Module):
@@ -44,7 +57,7 @@ class SoftAgg(SmoothAggBase):
         return torch.softmax(_prod_c(1.0 / self.gamma, z), dim=-1)
 
 
-class GaussianAgg(SmoothAggBase):
+class GaussianAgg(_PerturbedAgg, SmoothAggBase):
     """Monte-Carlo perturbed argmax with Gaussian noise (smoothagg.py:185-205)."""
 
     noise_kind = "gaussian"
@@ -54,12 +67,8 @@ class GaussianAgg(SmoothAggBase):
         super().__init__(gamma, alpha, eps, nb_samples)
         self.fixed_noise = fixed_noise
 
-    def aggregate(self, zbuf, zfar, znear, prob_map, mask):
-        return _blend.perturbed_aggregate(zbuf, zfar, znear, prob_map, mask, self.gamma, self.alpha,
-                                          self.nb_samples, eps=self.eps, fixed_noise=self.fixed_noise)
 
-
-class GaussianAgg_wovr(SmoothAggBase):
+class GaussianAgg_wovr(_PerturbedAgg, SmoothAggBase):
     """Gaussian perturbed argmax without variance reduction (smoothagg.py:207-227)."""
 
     noise_kind = "gaussian"
@@ -69,13 +78,8 @@ class GaussianAgg_wovr(SmoothAggBase):
         super().__init__(gamma, alpha, eps, nb_samples)
         self.fixed_noise = fixed_noise
 
-    def aggregate(self, zbuf, zfar, znear, prob_map, mask):
-        return _variants.perturbed_aggregate_variant(
-            zbuf, zfar, znear, prob_map, mask, self.gamma, self.alpha, self.nb_samples, self.eps,
-            "gaussian", variance_reduction=False, fixed_noise=self.fixed_noise)
 
-
-class CauchyAgg(SmoothAggBase):
+class CauchyAgg(_PerturbedAgg, SmoothAggBase):
     """Cauchy-perturbed argmax (smoothagg.py:230-250)."""
 
     noise_kind = "cauchy"
@@ -84,11 +88,6 @@ class CauchyAgg(SmoothAggBase):
     def __init__(self, nb_samples=16, gamma=4e-2, alpha=1.0, eps=1e-10, fixed_noise=False):
         super().__init__(gamma, alpha, eps, nb_samples)
         self.fixed_noise = fixed_noise
-
-    def aggregate(self, zbuf, zfar, znear, prob_map, mask):
-        return _variants.perturbed_aggregate_variant(
-            zbuf, zfar, znear, prob_map, mask, self.gamma, self.alpha, self.nb_samples, self.eps,
-            "cauchy", variance_reduction=True, fixed_noise=self.fixed_noise)
 
 
 class UniformAgg(SmoothAggBase):

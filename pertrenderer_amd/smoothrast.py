@@ -2,16 +2,28 @@
 
 Class names, constructor signatures, attributes (``sigma`` a CPU 0-d leaf with
 requires_grad, ``nb_samples`` an int) and the ``update_*`` mutators mirror
-smoothrast.py:111-194.  ``GaussianRast.rasterize`` runs on the native kernels
-(pr_heaviside_*); inside ``smooth_rgb_blend`` a GaussianRast + GaussianAgg pair is
-fused into one pr_blend launch.  The deterministic variants (SoftRast, AffineRast,
-HardRast) are elementwise torch expressions, as in the reference.
+smoothrast.py:111-194.  The Monte-Carlo operators (GaussianRast, ArctanRast =
+Cauchy noise, GaussianRast_wovr = no variance reduction) run on the native kernels
+(pr_heaviside_* with PR_BLEND_RAST_* variant flags); inside ``smooth_rgb_blend`` any
+of them paired with a native aggregation operator is fused into one pr_blend launch.
+The deterministic variants (SoftRast, AffineRast, HardRast) are elementwise torch
+expressions, as in the reference.
 """
 import torch
 from torch.nn import Module
 
 from . import blend as _blend
-from . import variants as _variants
+
+
+class _PerturbedRast:
+    """rasterize() of the Monte-Carlo operators: the native perturbed Heaviside."""
+
+    noise_kind = "gaussian"
+    variance_reduction = True
+
+    def rasterize(self, dists):
+        return _blend.perturbed_heaviside(dists, self.sigma, self.nb_samples, kind=self.noise_kind,
+                                          variance_reduction=self.variance_reduction)
 
 
 class SmoothRastBase(Module):
@@ -39,7 +51,7 @@ class SoftRast(SmoothRastBase):
         return torch.sigmoid(-dists / self.sigma)
 
 
-class GaussianRast(SmoothRastBase):
+class GaussianRast(_PerturbedRast, SmoothRastBase):
     """Monte-Carlo perturbed Heaviside with Gaussian noise (smoothrast.py:136-147)."""
 
     noise_kind = "gaussian"
@@ -49,11 +61,8 @@ class GaussianRast(SmoothRastBase):
         super().__init__(sigma)
         self.nb_samples = nb_samples
 
-    def rasterize(self, dists):
-        return _blend.perturbed_heaviside(dists, self.sigma, self.nb_samples)
 
-
-class GaussianRast_wovr(SmoothRastBase):
+class GaussianRast_wovr(_PerturbedRast, SmoothRastBase):
     """Gaussian perturbed Heaviside without variance reduction (smoothrast.py:149-160)."""
 
     noise_kind = "gaussian"
@@ -63,12 +72,8 @@ class GaussianRast_wovr(SmoothRastBase):
         super().__init__(sigma)
         self.nb_samples = nb_samples
 
-    def rasterize(self, dists):
-        return _variants.perturbed_heaviside_variant(dists, self.sigma, self.nb_samples,
-                                                     "gaussian", variance_reduction=False)
 
-
-class ArctanRast(SmoothRastBase):
+class ArctanRast(_PerturbedRast, SmoothRastBase):
     """Cauchy-perturbed Heaviside (smoothrast.py:162-173)."""
 
     noise_kind = "cauchy"
@@ -77,10 +82,6 @@ class ArctanRast(SmoothRastBase):
     def __init__(self, nb_samples=16, sigma=2e-4):
         super().__init__(sigma)
         self.nb_samples = nb_samples
-
-    def rasterize(self, dists):
-        return _variants.perturbed_heaviside_variant(dists, self.sigma, self.nb_samples, "cauchy",
-                                                     variance_reduction=True)
 
 
 class AffineRast(SmoothRastBase):

@@ -186,6 +186,59 @@ def run_agg_case(name, ref, fr, prob, Sa, gamma, alpha, znear, zfar, seed, eps=1
     print("wrote", name, tuple(Wt.shape))
 
 
+def redraw(kind, shape):
+    """The reference's own noise draw (smoothrast.py:20-24, smoothagg.py:20-27) replayed
+    from the same global generator state."""
+    if kind == "gaussian":
+        return torch.normal(mean=torch.zeros(shape), std=1.0)
+    m = torch.distributions.cauchy.Cauchy(torch.tensor([0.0]), torch.tensor([1.0]))
+    return torch.clamp(m.sample(shape).squeeze(-1), min=-1e7, max=1e7)
+
+
+RAST_KIND = {"GaussianRast": ("gaussian", True), "GaussianRast_wovr": ("gaussian", False),
+             "ArctanRast": ("cauchy", True)}
+AGG_KIND = {"GaussianAgg": ("gaussian", True), "GaussianAgg_wovr": ("gaussian", False),
+            "CauchyAgg": ("cauchy", True)}
+
+
+def run_variant_blend_case(name, ref, fr, colors, rast_cls, agg_cls, Sr, Sa, sigma, gamma, alpha, bg,
+                           znear, zfar, seed, eps=1e-10):
+    """smooth_rgb_blend with a non-default (rast, agg) pair: Cauchy noise and/or no variance
+    reduction."""
+    rr, sr, sa, BlendParams = ref
+    N, H, W, K = fr.pix_to_face.shape
+    rast = getattr(sr, rast_cls)(nb_samples=Sr, sigma=sigma)
+    agg = getattr(sa, agg_cls)(nb_samples=Sa, gamma=gamma, alpha=alpha, eps=eps)
+    dists = fr.dists.clone().requires_grad_(True)
+    zbuf = fr.zbuf.clone().requires_grad_(True)
+    cols = colors.clone().requires_grad_(True)
+    frag = Fragments(fr.pix_to_face, zbuf, fr.bary_coords, dists)
+    zn = torch.full((N,), znear)[:, None, None, None]
+    zf = torch.full((N,), zfar)[:, None, None, None]
+    torch.manual_seed(seed)
+    img = rr.smooth_rgb_blend(cols, frag, rast, agg, BlendParams(sigma, gamma, tuple(bg)), znear=zn, zfar=zf)
+    gup = torch.randn(img.shape, generator=torch.Generator().manual_seed(seed + 1))
+    (img * gup).sum().backward()
+    torch.manual_seed(seed)
+    rk, rvr = RAST_KIND[rast_cls]
+    ak, avr = AGG_KIND[agg_cls]
+    er = redraw(rk, (Sr, N, H, W, K))
+    ea = redraw(ak, (Sa, N, H, W, K + 1))
+    np.savez_compressed(
+        os.path.join(OUT, name + ".npz"),
+        pix_to_face=fr.pix_to_face.numpy(), zbuf=fr.zbuf.numpy(), dists=fr.dists.numpy(),
+        colors=colors.numpy(), znear=np.float32(znear), zfar=np.float32(zfar),
+        background=np.asarray(bg, np.float32), sigma=np.float32(sigma), gamma=np.float32(gamma),
+        alpha=np.float32(alpha), eps=np.float64(eps), Sr=np.int64(Sr), Sa=np.int64(Sa),
+        seed=np.int64(seed), rast_cls=np.str_(rast_cls), agg_cls=np.str_(agg_cls),
+        rast_kind=np.str_(rk), rast_vr=np.bool_(rvr), agg_kind=np.str_(ak), agg_vr=np.bool_(avr),
+        noise_r=er.numpy(), noise_a=ea.numpy(), grad_image=gup.numpy(),
+        image=img.detach().numpy(), grad_dists=dists.grad.numpy(), grad_zbuf=zbuf.grad.numpy(),
+        grad_colors=cols.grad.numpy(), grad_sigma=rast.sigma.grad.numpy(),
+        grad_gamma=agg.gamma.grad.numpy(), grad_alpha=agg.alpha.grad.numpy())
+    print("wrote", name, tuple(img.shape))
+
+
 def run_soft_case(name, ref, fr, colors, sigma, gamma, alpha, bg, znear, zfar, eps=1e-10):
     """Deterministic SoftRast + SoftAgg blend (eval.py's default "softras" renderer)."""
     rr, sr, sa, BlendParams = ref
@@ -248,6 +301,16 @@ def main():
     prob[0, 0, 0, :3] = 1.0
     prob[0, 1, 1, 1] = 0.0
     run_agg_case("agg_only", ref, fr, prob, 5, 1e-2, 1.0, 1.0, 100.0, 41)
+    # noise variants (Cauchy / no variance reduction), fused blend
+    g = torch.Generator().manual_seed(9)
+    fr = synth_fragments(g, 2, 4, 5, 12, 1e-3, packed=True)
+    cols = torch.rand((2, 4, 5, 12, 3), generator=g)
+    run_variant_blend_case("var_arctan_cauchy", ref, fr, cols, "ArctanRast", "CauchyAgg", 8, 8, 1e-3, 1e-2, 1.0,
+                           (0.1, 0.2, 0.3), 1.0, 100.0, 61)
+    run_variant_blend_case("var_wovr", ref, fr, cols, "GaussianRast_wovr", "GaussianAgg_wovr", 8, 8, 1e-3, 1e-2,
+                           1.0, (0.1, 0.2, 0.3), 1.0, 100.0, 62)
+    run_variant_blend_case("var_mixed", ref, fr, cols, "ArctanRast", "GaussianAgg_wovr", 6, 5, 1e-3, 2e-2,
+                           1.3, (0.0, 0.0, 0.0), 1.0, 100.0, 63)
     # deterministic soft path (eval.py "softras")
     g = torch.Generator().manual_seed(8)
     fr = synth_fragments(g, 1, 4, 5, 9, 1e-3)

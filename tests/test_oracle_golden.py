@@ -70,3 +70,30 @@ def test_golden_noise_is_the_reference_draw_order():
     ea = torch.randn(f["noise_a"].shape)
     np.testing.assert_array_equal(er.numpy(), f["noise_r"])
     np.testing.assert_array_equal(ea.numpy(), f["noise_a"])
+
+
+VARIANT_CASES = ["var_arctan_cauchy", "var_wovr", "var_mixed"]
+
+
+def variant_kinds(f):
+    return str(f["rast_kind"]), bool(f["rast_vr"]), str(f["agg_kind"]), bool(f["agg_vr"])
+
+
+@pytest.mark.parametrize("case", VARIANT_CASES)
+def test_variant_blend_oracle_matches_reference(case):
+    """ArctanRast / GaussianRast_wovr x CauchyAgg / GaussianAgg_wovr (smoothrast.py:61-173,
+    smoothagg.py:75-250): bitwise, except d gamma with Cauchy agg noise (the reference
+    contracts score.eps with a matmul: fp32 summation order)."""
+    f = load_golden(case)
+    zn, zf = _planes(f, f["pix_to_face"].shape[0])
+    rk, rvr, ak, avr = variant_kinds(f)
+    img, saved = bo.blend_forward(T(f["pix_to_face"]), T(f["dists"]), T(f["zbuf"]), T(f["colors"]),
+                                  T(f["noise_r"]), T(f["noise_a"]), T(f["sigma"]), T(f["gamma"]),
+                                  T(f["alpha"]), float(f["eps"]), T(f["background"]), zn, zf, rk, rvr, ak, avr)
+    g = bo.blend_backward(T(f["grad_image"]), saved)
+    np.testing.assert_array_equal(img.numpy(), f["image"])
+    for k in ("dists", "zbuf", "colors", "sigma", "gamma", "alpha"):
+        if k == "gamma" and ak == "cauchy":
+            np.testing.assert_allclose(g[k].numpy(), f["grad_" + k], rtol=2e-6, err_msg=k)
+        else:
+            np.testing.assert_array_equal(g[k].numpy(), f["grad_" + k], err_msg=k)
