@@ -33,6 +33,14 @@ namespace {
 constexpr float kNegInf = -__builtin_inff();
 constexpr float kEpsMaxBM = 5.8f;               // > sqrt(-2 ln 2^-24) = 5.7683
 
+#ifdef PR_BLEND_PROFILE
+#define PR_BPROF_DECL long long bst_[6] = {0, 0, 0, 0, 0, 0}, bt_ = __builtin_amdgcn_s_memtime()
+#define PR_BSTAMP(i) (bst_[i] = __builtin_amdgcn_s_memtime() - bt_, bt_ = __builtin_amdgcn_s_memtime())
+#else
+#define PR_BPROF_DECL (void)0
+#define PR_BSTAMP(i) (void)0
+#endif
+
 struct Geo {
   int64_t P, PK;  // pixels, slots
   int K, KP1, PB, HW;
@@ -216,6 +224,7 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
   float* PX = B + PB * KP1;        // [PB][4] z_max, alpha, max logit
   int* CNT = reinterpret_cast<int*>(A);
   const int tid = threadIdx.x;
+  PR_BPROF_DECL;
   const int64_t pix0 = (int64_t)blockIdx.x * PB;
   const int npix = (int)min((int64_t)PB, g.P - pix0);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
@@ -250,6 +259,7 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
     B[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
   }
   __syncthreads();
+  PR_BSTAMP(0);
 
   // ---- 2: per pixel (8 lanes): alpha, z_max, logits, largest logit
   {
@@ -286,6 +296,7 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
     }
   }
   __syncthreads();
+  PR_BSTAMP(1);
 
   // ---- 3: Monte-Carlo argmax: thread = (pixel, 4-sample group, slot chunk)
   {
@@ -342,6 +353,7 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
     }
   }
   __syncthreads();
+  PR_BSTAMP(2);
 
   // ---- 4: outputs
   const float fSa = (float)p.Sa;
@@ -381,6 +393,12 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
       a.weights[(pix0 + pl) * KP1 + k] = (float)CNT[pl * KP1 + k] / fSa;
     }
   }
+#ifdef PR_BLEND_PROFILE
+  __syncthreads();
+  PR_BSTAMP(3);
+  if (tid == 0 && (blockIdx.x % 97) == 0)
+    printf("fwd blk %d | p1 %lld p2 %lld p3 %lld p4 %lld\n", blockIdx.x, bst_[0], bst_[1], bst_[2], bst_[3]);
+#endif
 }
 
 // ================================================================= backward
@@ -400,6 +418,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
   float* AS = reinterpret_cast<float*>(CN + PB * KP1);  // [PB][Sa] a_s
   float* PX = AS + PB * Sa;            // [PB][8] per-pixel scalars
   const int tid = threadIdx.x;
+  PR_BPROF_DECL;
   const int64_t pix0 = (int64_t)blockIdx.x * PB;
   const int npix = (int)min((int64_t)PB, g.P - pix0);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
@@ -457,6 +476,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     }
   }
   __syncthreads();
+  PR_BSTAMP(0);
 
   // ---- B2: per pixel (8 lanes, contiguous chunks): z_max + first argmax, exclusive
   //          products for the alpha gradient, logits, unperturbed argmax j0
@@ -521,6 +541,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     }
   }
   __syncthreads();
+  PR_BSTAMP(1);
 
   // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0], win counts
   PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
@@ -554,6 +575,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     atomicAdd(&CN[pl * KP1 + jw], 1);
   }
   __syncthreads();
+  PR_BSTAMP(2);
 
   // ---- B6: dz_j = mean_s(a_s * score(eps_sj) / gamma) and sum_s a_s * eps_sj * score(eps_sj)
   //          (d gamma; score = eps for Gaussian noise, 2 eps / (1 + eps^2) for Cauchy)
@@ -592,6 +614,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     }
   }
   __syncthreads();
+  PR_BSTAMP(3);
 
   // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps
   {
@@ -610,6 +633,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     }
   }
   __syncthreads();
+  PR_BSTAMP(4);
 
   // ---- B8: per-slot gradients
   PR_FOR_SLOTS(K, g.qK, g.rK, npix * K) {
@@ -693,6 +717,12 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
   if (tid < 4) {
     partials[(int64_t)blockIdx.x * 4 + tid] = (RED[tid] + RED[4 + tid]) + (RED[8 + tid] + RED[12 + tid]);
   }
+#ifdef PR_BLEND_PROFILE
+  PR_BSTAMP(5);
+  if (tid == 0 && (blockIdx.x % 97) == 0)
+    printf("bwd blk %d | B1 %lld B2 %lld B5 %lld B6 %lld B7 %lld B8+red %lld\n", blockIdx.x, bst_[0], bst_[1], bst_[2],
+           bst_[3], bst_[4], bst_[5]);
+#endif
 }
 
 // d sigma, d gamma, d alpha from the per-block partials (one workgroup, fixed order)
