@@ -1,13 +1,16 @@
 """Benchmark of the perturbed-renderer hot path (BASELINE.json configs[1]).
 
-One step = one pose-optimisation iteration of experiments/eval.py:343-370 on one
-frame per GPU: rotate the mesh (so3 exp map), MeshRasterizer (native K-nearest
-rasterizer, 256x256, faces_per_pixel=50, blur = ln(1/1e-4 - 1)*sigma),
-RandomSimpleShader with GaussianRast(nb_samples=8) + GaussianAgg(nb_samples=8)
-(fused native blend), L2 loss to a fixed synthetic target, backward through
-blend -> interpolation -> rasterizer -> vertices -> pose, and (N>1) one RCCL
-all-reduce averaging the pose/smoothing gradients across ranks.  Per-GPU work is
-fixed (one frame per rank per step): weak scaling.
+One step = one pose-optimisation iteration of experiments/eval.py:343-370: rotate
+the mesh (so3 exp map), MeshRasterizer (native K-nearest rasterizer, 256x256,
+faces_per_pixel=50, blur = ln(1/1e-4 - 1)*sigma), RandomSimpleShader with
+GaussianRast(nb_samples=8) + GaussianAgg(nb_samples=8) (fused native blend with
+TexturesVertex sampling), L2 loss to a fixed synthetic target, backward through
+blend -> rasterizer -> vertices -> pose.  With N ranks the Monte-Carlo sample
+dimension is sharded (BASELINE north star): every rank renders the SAME frame and
+pose with its own disjoint range of global sample indices (Philox offset rank*S),
+and one RCCL all-reduce averages the gradient estimates, i.e. each step is one
+pose update from an (N*8)-sample estimator.  Per-GPU work is fixed (one 8-sample
+render per rank per step): weak scaling; `value` counts renders over all ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
@@ -281,10 +284,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    torch.manual_seed(1234 + rank)
+    torch.manual_seed(1234)  # same Philox keys on every rank ...
+    pa.noise.set_sample_shard(rank)  # ... disjoint global sample ranges
     pa.native_library()
 
-    wl = Workload(device, args.image_size, args.faces_per_pixel, args.samples, seed=rank)
+    wl = Workload(device, args.image_size, args.faces_per_pixel, args.samples, seed=0)  # same frame on all ranks
     P = args.image_size * args.image_size
     mode, note = args.mode, None
     try:
@@ -292,7 +296,7 @@ def main():
     except Exception as e:  # graph capture unavailable: measure eagerly and say so
         note = f"graph capture failed ({type(e).__name__}: {e}); eager fallback"
         pa.noise.use_device_seed(None)
-        wl = Workload(device, args.image_size, args.faces_per_pixel, args.samples, seed=rank)
+        wl = Workload(device, args.image_size, args.faces_per_pixel, args.samples, seed=0)
         mode = "eager"
         step = build_step(wl, world, mode, device)
 
@@ -342,7 +346,8 @@ def main():
                                "Sr=Sa=8 Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, fwd+bwd",
                    "image_size": args.image_size, "faces_per_pixel": args.faces_per_pixel,
                    "nb_samples": args.samples, "frames_per_rank_per_step": 1, "execution": mode,
-                   "parallelism": f"dp{world} (one frame per rank, RCCL gradient all-reduce)"},
+                   "parallelism": f"sample-parallel x{world} (same frame, Philox sample shard per rank, "
+                                  f"one RCCL gradient all-reduce per step)"},
         "ms_forward": round(ms_fwd, 4), "ms_backward": round(ms_bwd, 4),
         "fwd_bwd_split_from": "eager instrumented replica (HIP events around forward / loss.backward())",
         "fwd_frames_per_s": round(world * 1e3 / ms_fwd, 2), "kernels": kern, "roofline": roof,

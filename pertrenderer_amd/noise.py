@@ -100,6 +100,21 @@ class DeviceSeed:
 
 
 _DEVICE_SEED = None
+_SHARD = 0  # this process's Monte-Carlo sample shard index (set_sample_shard)
+
+
+def set_sample_shard(index):
+    """Sample-parallel rendering (BASELINE north star): every Philox draw of an
+    operator with S samples takes the global sample indices [index*S, (index+1)*S) of one
+    estimator, so ranks sharing keys (same seed / DeviceSeed base) draw disjoint sample shards
+    of the same frame, and averaging their gradients (parallel.average_gradients) is the
+    (world*S)-sample estimator.  Index 0 (default) is the single-process behaviour."""
+    global _SHARD
+    _SHARD = int(index)
+
+
+def sample_shard():
+    return _SHARD
 
 
 def use_device_seed(ds):
@@ -123,8 +138,8 @@ def draw_rast(shape, Sr, device, kind="gaussian"):
     if _SOURCE == "torch":
         return Noise.injected(noise_r=_torch_draw(kind, (Sr,) + tuple(shape)).to(device))
     if _DEVICE_SEED is not None:
-        return Noise.philox(seed_r=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor)
-    return Noise.philox(seed_r=draw_key())
+        return Noise.philox(seed_r=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor, offset_r=_SHARD * Sr)
+    return Noise.philox(seed_r=draw_key(), offset_r=_SHARD * Sr)
 
 
 def draw_agg(shape, Sa, device, fixed_noise=False, kind="gaussian"):
@@ -136,5 +151,5 @@ def draw_agg(shape, Sa, device, fixed_noise=False, kind="gaussian"):
     if _SOURCE == "torch":
         return Noise.injected(noise_a=_torch_draw(kind, (Sa,) + tuple(shape)).to(device))
     if _DEVICE_SEED is not None and not fixed_noise:
-        return Noise.philox(seed_a=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor)
-    return Noise.philox(seed_a=draw_key())
+        return Noise.philox(seed_a=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor, offset_a=_SHARD * Sa)
+    return Noise.philox(seed_a=draw_key(), offset_a=_SHARD * Sa)

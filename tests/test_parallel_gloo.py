@@ -57,7 +57,18 @@ def _worker(rank, world, port, q):
         dist.all_reduce(counts)
         P_full, _, _ = bo.heaviside_fwd(D, noise, torch.tensor(1e-3))
         ok2 = torch.equal(counts / S, P_full)
-        q.put((rank, bool(ok1), bool(ok2)))
+        # 3) bench's sample-parallel mode: same keys, rank r draws global samples [r*S, (r+1)*S)
+        from pertrenderer_amd import noise as nz
+        nz.set_sample_shard(rank)
+        torch.manual_seed(5)
+        nr = nz.draw_rast((1, 2, 2, 3), 8, "cpu")
+        na = nz.draw_agg((1, 2, 2, 4), 8, "cpu")
+        keys = torch.tensor([nr.seed_r, na.seed_a], dtype=torch.int64)
+        allk = [torch.zeros_like(keys) for _ in range(world)]
+        dist.all_gather(allk, keys)
+        ok3 = (nr.offset_r == 8 * rank and na.offset_a == 8 * rank and all(torch.equal(k, allk[0]) for k in allk))
+        nz.set_sample_shard(0)
+        q.put((rank, bool(ok1), bool(ok2 and ok3)))
     finally:
         dist.destroy_process_group()
 

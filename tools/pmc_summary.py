@@ -13,9 +13,12 @@ import json
 import os
 import sys
 
-SHORT = {"blend_fwd_kernel": "blend_fwd", "blend_bwd_kernel": "blend_bwd", "rast_fwd_kernel": "rast_fwd",
-         "rast_bwd_kernel": "rast_bwd", "interp_fwd_kernel": "interp_fwd", "interp_bwd_kernel": "interp_bwd",
-         "rast_frag_kernel": "rast_frag"}
+# C-ABI call (bench.py's timed unit) -> the kernels it launches
+CALLS = {"rast_fwd": ["face_prep_kernel", "rast_fwd_kernel", "rast_frag_kernel"],
+         "rast_bwd": ["rast_bwd_kernel"],
+         "blend_fwd": ["blend_fwd_kernel"],
+         "blend_bwd": ["blend_bwd_kernel", "blend_finalize_kernel"],
+         "interp_fwd": ["interp_fwd_kernel"], "interp_bwd": ["interp_bwd_kernel"]}
 
 
 def kname(raw):
@@ -40,14 +43,19 @@ def load(dirs):
 
 
 def traffic(res):
+    """Per C-ABI call: summed HBM bytes per launch of its kernels."""
     tr = {}
-    for k, c in res.items():
-        short = SHORT.get(k.split("<")[0])
-        if short is None or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
-            continue
-        rd, wr = 2.0 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
-        tr[short] = {"bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
-                     "kernel": k, "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes"}
+    for call, kernels in CALLS.items():
+        rd = wr = 0.0
+        found = []
+        for k, c in res.items():
+            if k.split("<")[0] in kernels and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                rd += 2.0 * c["FETCH_SIZE"] * 1024
+                wr += c["WRITE_SIZE"] * 1024
+                found.append(k)
+        if found:
+            tr[call] = {"bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
+                        "kernels": found, "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes"}
     return tr
 
 
