@@ -191,6 +191,12 @@ PR_DEV bool in_bbox(const FaceRec& r, V2 p) {
   return !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
 }
 
+#ifdef PR_RAST_PROFILE
+#define PR_STAMP(i) (stamp[i] += (long long)__builtin_amdgcn_s_memtime() - t_, t_ = __builtin_amdgcn_s_memtime())
+#else
+#define PR_STAMP(i) ((void)0)
+#endif
+
 constexpr int kCap = 512;    // per-round tile face list (faces beyond it are handled in later rounds)
 static_assert(kCap <= 8 * 64, "suffix-min pass holds kCap / 64 <= 8 entries per lane");
 constexpr int kCullU = 4;    // 64-face cull chunks whose loads are in flight together (per wave)
@@ -215,6 +221,58 @@ PR_DEV void bitonic_sort(float* key, int* val, int n2, int tid) {
       __syncthreads();
     }
   }
+}
+
+// Bitonic sort of E*64 (key, val) pairs held in one wave's registers, element
+// i = e*64 + lane.  Strides < 64 exchange through __shfl_xor, larger strides swap
+// registers of the same lane; no LDS and no barriers.  Equal keys keep their own
+// element on both sides, so the network stays a permutation.
+template <int E>
+PR_DEV void wave_bitonic_sort(float (&key)[E], int (&val)[E], int lane) {
+#pragma unroll
+  for (int k = 2; k <= E * 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        const int je = j >> 6;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int pe = e ^ je;
+          if (pe > e) {
+            const bool up = ((e * 64 + lane) & k) == 0;
+            const float a = key[e], b = key[pe];
+            if ((a > b) == up) {
+              key[e] = b; key[pe] = a;
+              const int t = val[e]; val[e] = val[pe]; val[pe] = t;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float ok = __shfl_xor(key[e], j);
+          const int ov = __shfl_xor(val[e], j);
+          const int i = e * 64 + lane;
+          const bool up = (i & k) == 0, lower = (lane & j) == 0;
+          // lower index keeps min when ascending, max when descending; upper the opposite
+          const bool take = lower == up ? (ok < key[e]) : (ok > key[e]);
+          if (take) { key[e] = ok; val[e] = ov; }
+        }
+      }
+    }
+  }
+}
+
+// sort lkey/lidx[0, n2) (n2 a power of two, <= 512) by wave 0 of the workgroup
+template <int E>
+PR_DEV void wave_sort_lds(float* lkey, int* lidx, int lane) {
+  float kk[E];
+  int vv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { kk[e] = lkey[e * 64 + lane]; vv[e] = lidx[e * 64 + lane]; }
+  wave_bitonic_sort<E>(kk, vv, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) { lkey[e * 64 + lane] = kk[e]; lidx[e * 64 + lane] = vv[e]; }
 }
 
 PR_DEV bool ekey_less(float2 x, float2 y) { return key_less(x.x, __float_as_int(x.y), y.x, __float_as_int(y.y)); }
@@ -296,6 +354,10 @@ __global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const F
   float qlast_z = __builtin_inff();
   int qlast_f = 0x7fffffff;
   int64_t base = fb;
+#ifdef PR_RAST_PROFILE
+  long long stamp[6] = {0, 0, 0, 0, 0, 0}, t_ = __builtin_amdgcn_s_memtime();
+  int nlist = 0;
+#endif
   while (base < fe) {
     // ---- gather this round's culled faces (expanded bbox overlaps the tile)
     if (tid == 0) *lcount = 0;
@@ -326,12 +388,16 @@ __global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const F
       nl = *lcount;
       __syncthreads();
     }
+    PR_STAMP(0);
+#ifdef PR_RAST_PROFILE
+    nlist += nl;
+#endif
     if (nl == 0) continue;
     bool done = !inimg;  // the early exit below is only valid inside one sorted round
     // ---- sort key: the face plane's depth at the tile centre, clamped to the face's
     //      z range (an ordering heuristic only: it makes the per-pixel inserts mostly
     //      appends).  Exactness does not depend on it; the early exit uses z_min.
-    int n2 = 1;
+    int n2 = 64;
     while (n2 < nl) n2 <<= 1;
     for (int i = tid; i < n2; i += NT) {
       float key = __builtin_inff();
@@ -354,7 +420,15 @@ __global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const F
       lidx[i] = i < nl ? i : 0x7fffffff;
     }
     __syncthreads();
-    bitonic_sort<NT>(lkey, lidx, n2, tid);
+    PR_STAMP(1);
+    if (wv == 0) {
+      if (n2 == 64) wave_sort_lds<1>(lkey, lidx, lane);
+      else if (n2 == 128) wave_sort_lds<2>(lkey, lidx, lane);
+      else if (n2 == 256) wave_sort_lds<4>(lkey, lidx, lane);
+      else wave_sort_lds<8>(lkey, lidx, lane);
+    }
+    __syncthreads();
+    PR_STAMP(2);
     // suffix minimum of z_min along the sorted order (faces after position i cannot
     // produce pz below lsuf[i] when barycentrics are clipped); wave 0 computes it
     {
@@ -388,34 +462,49 @@ __global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const F
       }
     }
     __syncthreads();
+    PR_STAMP(3);
     // ---- traversal: this wave's sorted positions wv, wv+WV, ... in chunks of 64
     const int nmine = nl > wv ? (nl - wv + WV - 1) / WV : 0;
+    // the chunk's records are gathered one chunk ahead (registers), so the global
+    // latency of chunk c+1 overlaps the tests of chunk c
+    FaceRec nrec;
+    int nfid = 0;
+    float nsuf = 0.f;
+    if (nmine > 0) {
+      const int cnt = min(64, nmine);
+      const int sp = wv + WV * min(lane, cnt - 1);
+      nfid = lfid[lidx[sp]];
+      nsuf = lsuf[sp];
+      nrec = faces[nfid];
+    }
     for (int c0 = 0; c0 < nmine && __ballot(!done) != 0; c0 += 64) {
       const int cnt = min(64, nmine - c0);
-      const int sp = wv + WV * (c0 + min(lane, cnt - 1));  // sorted position held by this lane
       // lane i holds chunk entry i's face id and suffix-min z (read back with readlane)
-      const int cfid = lfid[lidx[sp]];
-      const float csuf = lsuf[sp];
+      const int cfid = nfid;
+      const float csuf = nsuf;
       __builtin_amdgcn_wave_barrier();
-      if (lane < cnt) lrec[lane] = faces[cfid];
+      if (lane < cnt) lrec[lane] = nrec;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
+      if (c0 + 64 < nmine) {
+        const int ncnt = min(64, nmine - c0 - 64);
+        const int sp = wv + WV * (c0 + 64 + min(lane, ncnt - 1));
+        nfid = lfid[lidx[sp]];
+        nsuf = lsuf[sp];
+        nrec = faces[nfid];
+      }
       for (int t = 0; t < cnt; t += kGroup) {
         bool cand[kGroup];
         float pzv[kGroup];
+        FaceRec rr[kGroup];
         bool any = false;
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j) {
-          const int tt = min(t + j, cnt - 1);
-          any |= t + j < cnt && __ballot(in_bbox(lrec[tt], p)) != 0;
-        }
+        for (int j = 0; j < kGroup; ++j) rr[j] = lrec[min(t + j, cnt - 1)];  // one LDS wait per group
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) any |= t + j < cnt && __ballot(in_bbox(rr[j], p)) != 0;
         if (!any) continue;
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j) {
-          const int tt = min(t + j, cnt - 1);
-          const FaceRec rr = lrec[tt];
-          cand[j] = face_test<PERSP, CLIP>(rr, p, blur, pzv[j]) && t + j < cnt;
-        }
+        for (int j = 0; j < kGroup; ++j) cand[j] = face_test<PERSP, CLIP>(rr[j], p, blur, pzv[j]) && t + j < cnt;
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           if (t + j >= cnt) break;
@@ -464,6 +553,7 @@ __global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const F
       }
     }
     __syncthreads();
+    PR_STAMP(4);
   }
   qsz[wv * 64 + lane] = inimg ? qs : 0;
   __syncthreads();
@@ -479,25 +569,44 @@ __global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const F
       __syncthreads();
     }
   }
-  // ---- coalesced output: each tile row's 8 pixels own a contiguous 8*K slot range
+  // ---- coalesced output: each tile row's 8 pixels own a contiguous 8*K slot range;
+  //      the wave walks the tile's rows as one flat index (4 slots per lane in flight)
   const float2* q0 = qall;
-  const int q64 = 64 / K, r64 = 64 % K;
-  for (int r = wv; r < kTile; r += WV) {
-    const int prow = row0 + r;
-    if (prow >= H) break;
-    const int ncols = min(kTile, W - col0);
-    const int total = ncols * K;
-    const int64_t obase = (((int64_t)n * H + prow) * W + col0) * K;
-    for (int i = lane, c = lane / K, k = lane - (lane / K) * K; i < total;
-         i += 64, c += q64, k += r64, (k >= K ? (k -= K, ++c) : 0)) {
-      const int tl = r * kTile + c;
-      const int64_t o = obase + i;
-      const float2 e = q0[k * 64 + tl];  // read with the size (stale beyond it, unused)
-      const bool valid = k < qsz[tl];
-      a.pix_to_face[o] = valid ? (int64_t)__float_as_int(e.y) : (int64_t)-1;
-      a.zbuf[o] = valid ? e.x : -1.f;
+  {
+    const int ncols = min(kTile, W - col0), nrows = min(kTile, H - row0);
+    const int per_row = ncols * K, total = nrows * per_row;
+    constexpr int U = 4;
+    for (int base = wv * 64 * U; base < total; base += WV * 64 * U) {
+      float2 e[U];
+      int sz[U], kk[U];
+      int64_t o[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(base + u * 64 + lane, total - 1);
+        const int r = i / per_row, rem = i - r * per_row;
+        const int c = rem / K;
+        kk[u] = rem - c * K;
+        const int tl = r * kTile + c;
+        o[u] = (((int64_t)n * H + row0 + r) * W + col0) * K + rem;
+        e[u] = q0[kk[u] * 64 + tl];  // read with the size (stale beyond it, unused)
+        sz[u] = qsz[tl];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (base + u * 64 + lane >= total) break;
+        const bool valid = kk[u] < sz[u];
+        a.pix_to_face[o[u]] = valid ? (int64_t)__float_as_int(e[u].y) : (int64_t)-1;
+        a.zbuf[o[u]] = valid ? e[u].x : -1.f;
+      }
     }
   }
+#ifdef PR_RAST_PROFILE
+  __syncthreads();
+  PR_STAMP(5);
+  if (tid == 0 && nlist >= 88)
+    printf("tile %d,%d WV %d list %d | cull %lld key %lld sort %lld suf %lld test %lld merge+out %lld\n", blockIdx.x,
+           blockIdx.y, WV, nlist, stamp[0], stamp[1], stamp[2], stamp[3], stamp[4], stamp[5]);
+#endif
 }
 
 template <bool PERSP, bool CLIP>
