@@ -87,6 +87,39 @@ PR_DEV int image_of(int n0, int rem0, int pl, int HW) {
   for (int i_ = tid, pl = tid / (L), k = tid - (tid / (L)) * (L); i_ < (NTOT);          \
        i_ += kThreads, pl += (Q), k += (R), (k >= (L) ? (k -= (L), ++pl) : 0))
 
+// Batched slot walk: the same (pl, k) sequence as PR_FOR_SLOTS, kU items per thread per
+// batch, so a batch's global loads are all in flight before the first is consumed
+// (the slot phases are latency-bound: one HBM round trip per dependent iteration).
+constexpr int kU = 4;
+struct Batch {
+  int pl[kU], k[kU];
+  bool ok[kU];
+};
+PR_DEV void batch_next(Batch& b, int& pl, int& k, int i0, int L, int Q, int R, int NTOT) {
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    b.pl[u] = pl;
+    b.k[u] = k;
+    b.ok[u] = i0 + u * kThreads < NTOT;
+    pl += Q;
+    k += R;
+    if (k >= L) { k -= L; ++pl; }
+  }
+}
+
+// Wave-wide append of the lanes with `want` to an LDS queue: one LDS atomic per wave,
+// returns the lane's queue position (-1 if !want).
+PR_DEV int wave_append(bool want, int* counter) {
+  const uint64_t b = __ballot(want);
+  if (b == 0) return -1;
+  const int lane = __lane_id();
+  const int leader = __ffsll((unsigned long long)b) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(b));
+  base = __shfl(base, leader);
+  return want ? base + __popcll(b & ((1ull << lane) - 1ull)) : -1;
+}
+
 // ---------------------------------------------------------------- rast noise
 // Both noise modes evaluate smoothrast.py:32-33 literally, m_s = H(D + sigma*eps_s)
 // with H(0)=1 and D = -dist; Philox mode draws eps_s by Box-Muller (4 per Philox
@@ -117,14 +150,16 @@ PR_DEV int rast_count(const PRBlendParams& p, const Sc& sc, float dist, uint32_t
       const int sat = rast_saturated(dist, sc.sigma);
       if (sat) return sat < 0 ? p.Sr : 0;
     }
-    float e[4];
-    for (int s = 0; s < p.Sr; ++s) {
-      const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
-      if (s == 0 || (sg & 3u) == 0) {
-        const U4 u = philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast);
-        if (cauchy) cauchy4(u, e); else gauss4(u, e);
+    const uint32_t s0 = (uint32_t)p.sample_offset_r, s1 = s0 + (uint32_t)p.Sr;
+    for (uint32_t g4 = s0 >> 2; 4u * g4 < s1; ++g4) {
+      const U4 u = philox_block(sc.kr, gp, (uint32_t)k, g4, kTagRast);
+      float e[4];
+      if (cauchy) cauchy4(u, e); else gauss4(u, e);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t sg = 4u * g4 + (uint32_t)q;
+        cnt += (sg >= s0 && sg < s1 && (D + sc.sigma * e[q]) >= 0.f) ? 1 : 0;
       }
-      cnt += (D + sc.sigma * pick4(e, sg & 3u)) >= 0.f ? 1 : 0;
     }
   }
   return cnt;
@@ -152,18 +187,25 @@ PR_DEV int rast_count_score(const PRBlendParams& p, const Sc& sc, float dist, ui
       const int sat = rast_saturated(dist, sc.sigma);
       if (sat) return sat < 0 ? p.Sr : 0;  // m_s = vr for every sample: no score
     }
-    float e[4];
-    for (int s = 0; s < p.Sr; ++s) {
-      const uint32_t sg = (uint32_t)(p.sample_offset_r + s);
-      if (s == 0 || (sg & 3u) == 0) {
-        const U4 u = philox_block(sc.kr, gp, (uint32_t)k, sg >> 2, kTagRast);
-        if (cauchy) cauchy4(u, e); else gauss4(u, e);
+    // one Philox block per 4 samples, straight-line over the block; base_s is
+    // b_in / b_out, the score sum is divided by sigma once at the end
+    const float b_in = wovr ? 1.f : 1.f - vr, b_out = wovr ? 0.f : -vr;
+    const uint32_t s0 = (uint32_t)p.sample_offset_r, s1 = s0 + (uint32_t)p.Sr;
+    float acc = 0.f;
+    for (uint32_t g4 = s0 >> 2; 4u * g4 < s1; ++g4) {
+      const U4 u = philox_block(sc.kr, gp, (uint32_t)k, g4, kTagRast);
+      float e[4];
+      if (cauchy) cauchy4(u, e); else gauss4(u, e);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t sg = 4u * g4 + (uint32_t)q;
+        if (sg < s0 || sg >= s1) continue;
+        const bool in = (D + sc.sigma * e[q]) >= 0.f;
+        cnt += in ? 1 : 0;
+        acc = __builtin_fmaf(in ? b_in : b_out, noise_score(e[q], cauchy), acc);
       }
-      const float ee = pick4(e, sg & 3u);
-      const float m = heaviside1(D + sc.sigma * ee);
-      cnt += (int)m;
-      gacc += ((wovr ? m : m - vr) * noise_score(ee, cauchy)) / sc.sigma;
     }
+    gacc = acc / sc.sigma;
   }
   return cnt;
 }
@@ -221,47 +263,101 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
   const int K = g.K, KP1 = g.KP1, PB = g.PB;
   float* A = smem;                 // [PB][KP1] prob, then int win counts
   float* B = A + PB * KP1;         // [PB][KP1] z_inv, then logits z
-  float* PX = B + PB * KP1;        // [PB][4] z_max, alpha, max logit
+  float* PX = B + PB * KP1;        // [PB][4] z_max, alpha, max logit, candidate count
+  int* QN = reinterpret_cast<int*>(PX + PB * 4);            // rast queue length
+  uint16_t* Q = reinterpret_cast<uint16_t*>(QN + 4);        // [PB*K] rast queue (pl << 8 | k)
+  uint8_t* LC = reinterpret_cast<uint8_t*>(Q);              // [PB][KP1] argmax candidates (after 1b)
   int* CNT = reinterpret_cast<int*>(A);
+  int* PXI = reinterpret_cast<int*>(PX);
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
   const int64_t pix0 = (int64_t)blockIdx.x * PB;
   const int npix = (int)min((int64_t)PB, g.P - pix0);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
+  if (tid == 0) *QN = 0;
+  __syncthreads();
 
-  // ---- 1: slots: mask, probability, z_inv
-  PR_FOR_SLOTS(K, g.qK, g.rK, npix * K) {
-    const int64_t gp = pix0 + pl, gs = gp * K + k;
-    const bool m = slot_mask(a.pix_to_face, a.mask, gs);
-    const float mf = m ? 1.f : 0.f;
-    float prob;
-    if constexpr (RAST) {
-      if (a.rast_cache) {  // also keep the score mean for the backward (same arithmetic as its B1)
-        float gm = 0.f;
-        prob = 0.f;
-        if (m) {
-          float gacc;
-          const int cnt = rast_count_score<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK, gacc);
-          prob = ((float)cnt / (float)p.Sr) * mf;
-          gm = gacc / (float)p.Sr;
+  // ---- 1a: slots, kU per thread in flight: mask, z_inv, and the probability wherever
+  //          it needs no noise (masked, or saturated Gaussian); the rest is queued
+  {
+    // saturation shortcut of rast_count / rast_count_score (Philox Gaussian; the score
+    // form also needs variance reduction)
+    const bool sat_ok = NOISE == PR_NOISE_PHILOX && !(p.flags & PR_BLEND_RAST_CAUCHY) &&
+                        !(a.rast_cache && (p.flags & PR_BLEND_RAST_WOVR));
+    int cpl = tid / K, ck = tid - (tid / K) * K;
+    for (int i0 = tid; i0 < npix * K; i0 += kU * kThreads) {
+      Batch bt;
+      batch_next(bt, cpl, ck, i0, K, g.qK, g.rK, npix * K);
+      bool mk[kU];
+      float dd[kU], zb[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        mk[u] = false;
+        dd[u] = zb[u] = 0.f;
+        if (bt.ok[u]) {
+          const int64_t gs = (pix0 + bt.pl[u]) * K + bt.k[u];
+          mk[u] = slot_mask(a.pix_to_face, a.mask, gs);
+          dd[u] = RAST ? a.dists[gs] : a.prob[gs];
+          zb[u] = a.zbuf[gs];
         }
-        reinterpret_cast<float2*>(a.rast_cache)[gs] = make_float2(prob, gm);
-      } else {
-        prob = m ? ((float)rast_count<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK) / (float)p.Sr) * mf
-                 : 0.f;
       }
-    } else {
-      prob = a.prob[gs];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int pl = bt.pl[u], k = bt.k[u], li = pl * KP1 + k;
+        bool want = false;
+        if (bt.ok[u]) {
+          const int64_t gs = (pix0 + pl) * K + k;
+          const bool m = mk[u];
+          const int n = image_of(n0, rem0, pl, g.HW);
+          const float zf = p.zfar[n], zn = p.znear[n];
+          B[li] = ((zf - zb[u]) / (zf - zn)) * (m ? 1.f : 0.f);
+          if constexpr (RAST) {
+            const int sat = m && sat_ok ? rast_saturated(dd[u], sc.sigma) : 0;
+            want = m && sat == 0;
+            if (want) {
+              A[li] = dd[u];  // the distance, for 1b
+            } else {          // count Sr (saturated inside) or 0: prob Sr/Sr * 1 = 1, or 0
+              const float prob = sat < 0 ? 1.f : 0.f;
+              A[li] = prob;
+              if (a.rast_cache) reinterpret_cast<float2*>(a.rast_cache)[gs] = make_float2(prob, 0.f);
+            }
+          } else {
+            A[li] = dd[u];
+          }
+        }
+        if constexpr (RAST) {
+          const int pos = wave_append(want, QN);
+          if (want) Q[pos] = (uint16_t)((pl << 8) | k);
+        }
+      }
     }
-    const int n = image_of(n0, rem0, pl, g.HW);
-    const float zf = p.zfar[n], zn = p.znear[n];
-    A[pl * KP1 + k] = prob;
-    B[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
   }
   __syncthreads();
+
+  // ---- 1b: queued slots (valid, unsaturated): Monte-Carlo rasterization, all lanes busy
+  if constexpr (RAST) {
+    const int nq = *QN;
+    for (int i = tid; i < nq; i += kThreads) {
+      const int e = Q[i], pl = e >> 8, k = e & 255, li = pl * KP1 + k;
+      const int64_t gp = pix0 + pl, gs = gp * K + k;
+      const float dist = A[li];
+      float prob;
+      if (a.rast_cache) {  // also keep the score mean for the backward (same arithmetic as its B1)
+        float gacc;
+        const int cnt = rast_count_score<NOISE>(p, sc, dist, (uint32_t)gp, k, gs, g.PK, gacc);
+        prob = ((float)cnt / (float)p.Sr) * 1.f;
+        reinterpret_cast<float2*>(a.rast_cache)[gs] = make_float2(prob, gacc / (float)p.Sr);
+      } else {
+        prob = ((float)rast_count<NOISE>(p, sc, dist, (uint32_t)gp, k, gs, g.PK) / (float)p.Sr) * 1.f;
+      }
+      A[li] = prob;
+    }
+    __syncthreads();
+  }
   PR_BSTAMP(0);
 
-  // ---- 2: per pixel (8 lanes): alpha, z_max, logits, largest logit
+  // ---- 2: per pixel (8 lanes): alpha, z_max, logits, largest logit, and the list of
+  //         argmax candidates (ascending j)
   {
     const int pl = tid >> 3, l = tid & 7;
     const bool act = pl < npix;
@@ -289,23 +385,45 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
       }
 #pragma unroll
     for (int m = 1; m < 8; m <<= 1) zl = fmaxf(zl, __shfl_xor(zl, m));
+    // candidates: finite logits not below zl - skipm (bounded Box-Muller noise only: a
+    // logit further below the best can never win); lane chunks are contiguous, so an
+    // exclusive scan of the lane counts gives each lane its output offset
+    const float skipm = NOISE == PR_NOISE_PHILOX && !(p.flags & PR_BLEND_AGG_CAUCHY) ? 2.f * kEpsMaxBM * sc.gamma
+                                                                                    : __builtin_inff();
+    const float zfloor = zl - skipm;
+    int nc = 0;
+    if (act)
+      for (int j = j0; j < j1; ++j) {
+        const float z = B[pl * KP1 + j];
+        nc += (z > kNegInf && z >= zfloor) ? 1 : 0;
+      }
+    int off = 0, tot = 0;
+    const int lane8 = (tid & 63) & ~7;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      const int t = __shfl(nc, lane8 + o);
+      off += o < l ? t : 0;
+      tot += t;
+    }
+    if (act)
+      for (int j = j0; j < j1; ++j) {
+        const float z = B[pl * KP1 + j];
+        if (z > kNegInf && z >= zfloor) LC[pl * KP1 + off++] = (uint8_t)j;
+      }
     if (act && l == 0) {
       PX[pl * 4 + 0] = zmax;
       PX[pl * 4 + 1] = al;
       PX[pl * 4 + 2] = zl;
+      PXI[pl * 4 + 3] = tot;
     }
   }
   __syncthreads();
   PR_BSTAMP(1);
 
-  // ---- 3: Monte-Carlo argmax: thread = (pixel, 4-sample group, slot chunk)
+  // ---- 3: Monte-Carlo argmax: thread = (pixel, 4-sample group, candidate stripe c::NC)
   {
     const int ng = agg_num_groups(p), g0 = agg_first_group(p);
-    const int CS = (KP1 + NC - 1) / NC;
     const int npairs = npix * ng * NC;
-    // bounded (Box-Muller) noise only: a logit this far below the best can never win
-    const float skipm = NOISE == PR_NOISE_PHILOX && !(p.flags & PR_BLEND_AGG_CAUCHY) ? 2.f * kEpsMaxBM * sc.gamma
-                                                                                    : __builtin_inff();
     for (int base = 0; base < npairs; base += kThreads) {
       const int t = base + tid;
       const bool act = t < npairs;
@@ -316,11 +434,10 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
       float best[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
       int bidx[4] = {-1, -1, -1, -1};
       if (act) {
-        const float zfloor = PX[pl * 4 + 2] - skipm;
-        const int j1 = min(KP1, (c + 1) * CS);
-        for (int j = c * CS; j < j1; ++j) {
+        const int len = PXI[pl * 4 + 3];
+        for (int i = c; i < len; i += NC) {  // ascending j within the thread
+          const int j = LC[pl * KP1 + i];
           const float z = B[pl * KP1 + j];
-          if (!(z > kNegInf) || !(z >= zfloor)) continue;  // can never be the argmax
           float e[4];
           agg_noise4<NOISE>(p, sc, (uint32_t)gp, j, gg, g.P, KP1, e);
 #pragma unroll
@@ -425,54 +542,80 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
   const float gal = sc.gamma / sc.alpha;
   float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
 
-  // ---- B1: slots + background entry: prob, z_inv, rast score, dL/dW
-  PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
-    const int64_t gp = pix0 + pl;
-    CN[pl * KP1 + k] = 0;
-    if (k < K) {
-      const int64_t gs = gp * K + k;
-      const bool m = slot_mask(a.pix_to_face, a.mask, gs);
-      const float mf = m ? 1.f : 0.f;
-      float prob, gm = 0.f;
-      if constexpr (RAST) {
-        if (a.rast_cache) {
-          const float2 c = reinterpret_cast<const float2*>(a.rast_cache)[gs];
-          prob = c.x;
-          gm = c.y;
-        } else if (m) {
-          float gacc;
-          const int cnt = rast_count_score<NOISE>(p, sc, a.dists[gs], (uint32_t)gp, k, gs, g.PK, gacc);
-          prob = ((float)cnt / (float)p.Sr) * mf;
-          gm = gacc / (float)p.Sr;
+  // ---- B1: slots + background entry: prob, z_inv, rast score, dL/dW (kU items per
+  //          thread with their global loads in flight together)
+  {
+    int cpl = tid / KP1, ck = tid - (tid / KP1) * KP1;
+    for (int i0 = tid; i0 < npix * KP1; i0 += kU * kThreads) {
+      Batch bt;
+      batch_next(bt, cpl, ck, i0, KP1, g.qK1, g.rK1, npix * KP1);
+      bool mk[kU];
+      float2 pg[kU];  // (prob, gm) from the cache / input prob, or (dist, -) to recount
+      float zb[kU], dw[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        mk[u] = false;
+        pg[u] = make_float2(0.f, 0.f);
+        zb[u] = dw[u] = 0.f;
+        if (!bt.ok[u]) continue;
+        const int pl = bt.pl[u], k = bt.k[u];
+        const int64_t gp = pix0 + pl;
+        if (k < K) {
+          const int64_t gs = gp * K + k;
+          mk[u] = slot_mask(a.pix_to_face, a.mask, gs);
+          if constexpr (RAST) {
+            if (a.rast_cache) pg[u] = reinterpret_cast<const float2*>(a.rast_cache)[gs];
+            else pg[u].x = a.dists[gs];
+          } else {
+            pg[u].x = a.prob[gs];
+          }
+          zb[u] = a.zbuf[gs];
+          // CM 2: dW computed on demand in B5 (only winners and j0 need it)
+          if constexpr (CM == 1) {
+            const float4 gi = reinterpret_cast<const float4*>(a.grad_image)[gp];
+            const float* c = a.colors + gs * 3;
+            dw[u] = (gi.x * c[0] + gi.y * c[1]) + gi.z * c[2];
+          } else if constexpr (CM == 0) {
+            dw[u] = a.grad_weights[gp * KP1 + k];
+          }
         } else {
-          prob = 0.f;
+          if constexpr (CM != 0) {
+            const float4 gi = reinterpret_cast<const float4*>(a.grad_image)[gp];
+            dw[u] = (gi.x * p.background[0] + gi.y * p.background[1]) + gi.z * p.background[2];
+          } else {
+            dw[u] = a.grad_weights[gp * KP1 + K];
+          }
         }
-      } else {
-        prob = a.prob[gs];
       }
-      const int n = image_of(n0, rem0, pl, g.HW);
-      const float zf = p.zfar[n], zn = p.znear[n];
-      PR[pl * KP1 + k] = prob;
-      ZZ[pl * KP1 + k] = ((zf - a.zbuf[gs]) / (zf - zn)) * mf;
-      GM[pl * KP1 + k] = gm;
-      float dw = 0.f;  // CM 2: computed on demand in B5 (only winners and j0 need it)
-      if constexpr (CM == 1) {
-        const float* gi = a.grad_image + gp * 4;
-        const float* c = a.colors + gs * 3;
-        dw = (gi[0] * c[0] + gi[1] * c[1]) + gi[2] * c[2];
-      } else if constexpr (CM == 0) {
-        dw = a.grad_weights[gp * KP1 + k];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (!bt.ok[u]) continue;
+        const int pl = bt.pl[u], k = bt.k[u], li = pl * KP1 + k;
+        CN[li] = 0;
+        DW[li] = dw[u];
+        if (k == K) continue;
+        const int64_t gp = pix0 + pl, gs = gp * K + k;
+        const bool m = mk[u];
+        const float mf = m ? 1.f : 0.f;
+        float prob = pg[u].x, gm = pg[u].y;
+        if constexpr (RAST) {
+          if (!a.rast_cache) {
+            gm = 0.f;
+            prob = 0.f;
+            if (m) {
+              float gacc;
+              const int cnt = rast_count_score<NOISE>(p, sc, pg[u].x, (uint32_t)gp, k, gs, g.PK, gacc);
+              prob = ((float)cnt / (float)p.Sr) * mf;
+              gm = gacc / (float)p.Sr;
+            }
+          }
+        }
+        const int n = image_of(n0, rem0, pl, g.HW);
+        const float zf = p.zfar[n], zn = p.znear[n];
+        PR[li] = prob;
+        ZZ[li] = ((zf - zb[u]) / (zf - zn)) * mf;
+        GM[li] = gm;
       }
-      DW[pl * KP1 + k] = dw;
-    } else {
-      float dw;
-      if constexpr (CM != 0) {
-        const float* gi = a.grad_image + gp * 4;
-        dw = (gi[0] * p.background[0] + gi[1] * p.background[1]) + gi[2] * p.background[2];
-      } else {
-        dw = a.grad_weights[gp * KP1 + K];
-      }
-      DW[pl * KP1 + K] = dw;
     }
   }
   __syncthreads();
@@ -635,10 +778,35 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
   __syncthreads();
   PR_BSTAMP(4);
 
-  // ---- B8: per-slot gradients
-  PR_FOR_SLOTS(K, g.qK, g.rK, npix * K) {
+  // ---- B8: per-slot gradients (kU slots per thread, mask and upstream gradient loads batched)
+  int cpl = tid / K, ck = tid - (tid / K) * K;
+  for (int i0 = tid; i0 < npix * K; i0 += kU * kThreads) {
+    Batch bt;
+    batch_next(bt, cpl, ck, i0, K, g.qK, g.rK, npix * K);
+    int64_t fk[kU];
+    bool mk[kU];
+    float4 gik[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      fk[u] = -1;
+      mk[u] = false;
+      gik[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!bt.ok[u]) continue;
+      const int64_t gp = pix0 + bt.pl[u], gs = gp * K + bt.k[u];
+      if (a.pix_to_face) {
+        fk[u] = a.pix_to_face[gs];
+        mk[u] = fk[u] >= 0;
+      } else {
+        mk[u] = a.mask[gs] != 0;
+      }
+      if constexpr (CM != 0) gik[u] = reinterpret_cast<const float4*>(a.grad_image)[gp];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+    if (!bt.ok[u]) continue;
+    const int pl = bt.pl[u], k = bt.k[u];
     const int64_t gp = pix0 + pl, gs = gp * K + k;
-    const bool m = slot_mask(a.pix_to_face, a.mask, gs);
+    const bool m = mk[u];
     const float mf = m ? 1.f : 0.f;
     const float dzk = ZZ[pl * KP1 + k];
     const float dzinv = dzk + (k == (int)PX[pl * 8 + 2] ? PX[pl * 8 + 4] : 0.f);
@@ -653,10 +821,8 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     float r = 1.f / prob;
     if (__builtin_isinf(r)) r = 0.f;
     float dprob = r * dL;
-    if constexpr (CM != 0) {
-      const float ga = a.grad_image[gp * 4 + 3];
-      dprob = -((-ga) * EX[pl * KP1 + k]) + dprob;
-    }
+    const float4 gi = gik[u];
+    if constexpr (CM != 0) dprob = -((-gi.w) * EX[pl * KP1 + k]) + dprob;
     if constexpr (RAST) {
       const float dD = GM[pl * KP1 + k] * (dprob * mf);
       a.grad_dists[gs] = -dD;
@@ -666,20 +832,18 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
     }
     if constexpr (CM == 1) {
       const float w = (float)CN[pl * KP1 + k] / (float)Sa;
-      const float* gi = a.grad_image + gp * 4;
       float* dc = a.grad_colors + gs * 3;
-      dc[0] = w * gi[0];
-      dc[1] = w * gi[1];
-      dc[2] = w * gi[2];
+      dc[0] = w * gi.x;
+      dc[1] = w * gi.y;
+      dc[2] = w * gi.z;
     } else if constexpr (CM == 2) {
       // d colour = w * g_rgb, pushed through the interpolation (interp_bwd_kernel's order)
       const int cnt = CN[pl * KP1 + k];
       float gb[3] = {0.f, 0.f, 0.f};
-      const int64_t f = m ? a.pix_to_face[gs] : -1;
+      const int64_t f = m ? fk[u] : -1;
       if (cnt != 0 && f >= 0) {
         const float w = (float)cnt / (float)Sa;
-        const float* gi = a.grad_image + gp * 4;
-        const float dc[3] = {w * gi[0], w * gi[1], w * gi[2]};
+        const float dc[3] = {w * gi.x, w * gi.y, w * gi.z};
         const int64_t v[3] = {a.faces[f * 3], a.faces[f * 3 + 1], a.faces[f * 3 + 2]};
         const float bw[3] = {a.bary[gs * 3], a.bary[gs * 3 + 1], a.bary[gs * 3 + 2]};
 #pragma unroll
@@ -694,6 +858,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
       a.grad_bary[gs * 3] = gb[0];
       a.grad_bary[gs * 3 + 1] = gb[1];
       a.grad_bary[gs * 3 + 2] = gb[2];
+    }
     }
   }
 
@@ -827,7 +992,11 @@ __global__ void seed_advance_kernel(uint64_t* seeds, int n) {
 }
 
 // ================================================================== host side
-size_t fwd_lds(int PB, int KP1) { return (size_t)(2 * PB * KP1 + 4 * PB) * sizeof(float); }
+// A, B, PX, queue length (+pad), then the uint16 rast queue [PB*K] (which also holds the
+// uint8 candidate lists [PB][KP1]: 2K >= K+1)
+size_t fwd_lds(int PB, int KP1) {
+  return (size_t)(2 * PB * KP1 + 4 * PB + 4) * sizeof(float) + (size_t)PB * (KP1 - 1) * sizeof(uint16_t);
+}
 size_t bwd_lds(int PB, int KP1, int Sa) {
   const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + 8 * PB) * sizeof(float);
   return b < 16 * sizeof(float) ? 16 * sizeof(float) : b;
