@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 5
+#define PR_ABI_VERSION 6
 
 /* error codes */
 #define PR_OK 0
@@ -80,7 +80,8 @@ typedef struct PRBlendParams {
   const float* zfar;         /* (N,) */
   int32_t flags;             /* PR_BLEND_* */
   /* graph-capture support (both nullable):                                    */
-  const float* scalars;      /* device [sigma, gamma, alpha]; overrides the by-value fields */
+  const float* scalars[3];   /* nullable device 0-d sigma, gamma, alpha (the leaves' own storage); */
+                             /* each non-null one overrides its by-value field                   */
   const uint64_t* seeds;     /* device [base]; Philox keys become mix64(base ^ seed_r/a),  */
                              /* so a captured graph draws fresh noise after pr_seed_advance; */
                              /* a seed_r/seed_a with bit 63 set is used as-is (fixed noise) */

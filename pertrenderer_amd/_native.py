@@ -34,7 +34,7 @@ class PRBlendParams(C.Structure):
                 ("background", C.c_float * 3), ("noise_mode", C.c_int32),
                 ("seed_r", C.c_uint64), ("seed_a", C.c_uint64),
                 ("noise_r", _vp), ("noise_a", _vp), ("znear", _vp), ("zfar", _vp),
-                ("flags", C.c_int32), ("scalars", _vp), ("seeds", _vp)]
+                ("flags", C.c_int32), ("scalars", _vp * 3), ("seeds", _vp)]
 
 
 class PRBlendFwdArgs(C.Structure):
@@ -117,7 +117,7 @@ EXPORTS = {
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
 }
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 

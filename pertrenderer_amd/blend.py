@@ -50,11 +50,13 @@ def _contig(t, dtype=F32):
 
 
 def _scalars(vals, device):
-    """(host floats, device tensor or None) for the smoothing scalars.  All-device inputs are
-    passed by pointer (capture-safe); otherwise their values are read on the host."""
-    if all(torch.is_tensor(v) and v.is_cuda for v in vals):
-        dev = torch.stack([v.detach().reshape(()).to(F32) for v in vals]).contiguous()
-        return (0.0,) * len(vals), dev
+    """(host floats, device 0-d tensors or None) for the smoothing scalars.  When every tensor
+    input lives on the device they are passed by pointer to their own storage (capture-safe,
+    no stacking kernel); plain floats stay by-value.  Otherwise values are read on the host."""
+    tens = [v for v in vals if torch.is_tensor(v)]
+    if tens and all(v.is_cuda for v in tens):
+        dev = [v.detach().reshape(()).to(F32) if torch.is_tensor(v) else None for v in vals]
+        return tuple(0.0 if torch.is_tensor(v) else float(v) for v in vals), dev
     return tuple(float(v.detach().cpu()) if torch.is_tensor(v) else float(v) for v in vals), None
 
 
@@ -89,7 +91,8 @@ def _params(shape, Sr, Sa, sc, sc_dev, eps, bg, noise, znear, zfar, flags):
     p.noise_r, p.noise_a = nat.ptr(noise.noise_r), nat.ptr(noise.noise_a)
     p.znear, p.zfar = nat.ptr(znear), nat.ptr(zfar)
     p.flags = flags
-    p.scalars = nat.ptr(sc_dev)
+    for i in range(3):
+        p.scalars[i] = nat.ptr(sc_dev[i]) if sc_dev is not None and i < len(sc_dev) else None
     p.seeds = nat.ptr(noise.seeds)
     return p
 
@@ -160,14 +163,16 @@ class _FusedBlendFn(torch.autograd.Function):
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
         _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
-        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, sc_dev, cache)
+        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, cache)
+        ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
         ctx.refs = (sigma, gamma, alpha)
         return image
 
     @staticmethod
     def backward(ctx, gimg):
-        p2f_c, d_c, z_c, c_c, zn, zf, winners, sc_dev, cache = ctx.saved_tensors
+        p2f_c, d_c, z_c, c_c, zn, zf, winners, cache = ctx.saved_tensors
+        sc_dev = ctx.sc_dev
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
         lib = nat.load()
         N, H, W, K = p2f_c.shape
@@ -220,14 +225,16 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         a.bary, a.faces, a.vert_colors = nat.ptr(b_c), nat.ptr(f_c), nat.ptr(v_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
         _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
-        ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, sc_dev, cache)
+        ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache)
+        ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc, ctx.flags = cfg, noise, sc, flags
         ctx.refs = (sigma, gamma, alpha)
         return image
 
     @staticmethod
     def backward(ctx, gimg):
-        p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, sc_dev, cache = ctx.saved_tensors
+        p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache = ctx.saved_tensors
+        sc_dev = ctx.sc_dev
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
         lib = nat.load()
         N, H, W, K = p2f_c.shape
@@ -313,7 +320,7 @@ def _heaviside_args(shape, Sr, noise, sigma_val, sigma_dev, d_c, flags=0):
     a.N, a.H, a.W, a.K, a.Sr = N, H, W, K, int(Sr)
     a.sample_offset_r, a.noise_mode, a.sigma = noise.offset_r, noise.mode, sigma_val
     a.seed_r, a.noise_r, a.dists = noise.seed_r & (2 ** 64 - 1), nat.ptr(noise.noise_r), nat.ptr(d_c)
-    a.sigma_dev, a.seeds = nat.ptr(sigma_dev), nat.ptr(noise.seeds)
+    a.sigma_dev, a.seeds = nat.ptr(sigma_dev[0] if sigma_dev else None), nat.ptr(noise.seeds)
     return a
 
 
@@ -329,13 +336,15 @@ class _HeavisideFn(torch.autograd.Function):
         prob = torch.empty_like(d_c)
         a.prob = nat.ptr(prob)
         nat.check(lib.pr_heaviside_fwd(a, nat.stream_of(prob)), "pr_heaviside_fwd")
-        ctx.save_for_backward(d_c, sdev)
+        ctx.save_for_backward(d_c)
+        ctx.sdev = sdev
         ctx.noise, ctx.Sr, ctx.sv, ctx.sigma_ref, ctx.flags = noise, int(Sr), sv, sigma, flags
         return prob
 
     @staticmethod
     def backward(ctx, gP):
-        d_c, sdev = ctx.saved_tensors
+        d_c, = ctx.saved_tensors
+        sdev = ctx.sdev
         lib = nat.load()
         a = _heaviside_args(tuple(d_c.shape), ctx.Sr, ctx.noise, ctx.sv, sdev, d_c, ctx.flags)
         g = gP.detach().to(F32).contiguous()
@@ -375,8 +384,7 @@ class _AggregateFn(torch.autograd.Function):
         m_c = mask.detach().to(torch.uint8).contiguous()
         zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
         noise = cfg["noise"].to(dev)
-        one = torch.ones((), dtype=F32, device=dev) if (torch.is_tensor(gamma) and gamma.is_cuda) else 1.0
-        sc, sc_dev = _scalars((one, gamma, alpha), dev)
+        sc, sc_dev = _scalars((1.0, gamma, alpha), dev)
         p = _params((N, H, W, K), 1, cfg["Sa"], sc, sc_dev, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf,
                     cfg["vflags"])
         weights = torch.empty((N, H, W, K + 1), dtype=F32, device=dev)
@@ -386,13 +394,15 @@ class _AggregateFn(torch.autograd.Function):
         a.mask, a.prob, a.zbuf = nat.ptr(m_c), nat.ptr(p_c), nat.ptr(z_c)
         a.weights, a.winners = nat.ptr(weights), nat.ptr(winners)
         nat.check(lib.pr_blend_fwd(a, nat.stream_of(weights)), "pr_blend_fwd(aggregate)")
-        ctx.save_for_backward(z_c, p_c, m_c, zn, zf, winners, sc_dev)
+        ctx.save_for_backward(z_c, p_c, m_c, zn, zf, winners)
+        ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc, ctx.refs = cfg, noise, sc, (gamma, alpha)
         return weights
 
     @staticmethod
     def backward(ctx, gW):
-        z_c, p_c, m_c, zn, zf, winners, sc_dev = ctx.saved_tensors
+        z_c, p_c, m_c, zn, zf, winners = ctx.saved_tensors
+        sc_dev = ctx.sc_dev
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
         lib = nat.load()
         N, H, W, K = z_c.shape

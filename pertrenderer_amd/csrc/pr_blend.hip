@@ -61,7 +61,9 @@ PR_DEV uint64_t mix64(uint64_t z) {
 
 PR_DEV Sc resolve(const PRBlendParams& p) {
   Sc s{p.sigma, p.gamma, p.alpha, p.seed_r, p.seed_a};
-  if (p.scalars) { s.sigma = p.scalars[0]; s.gamma = p.scalars[1]; s.alpha = p.scalars[2]; }
+  if (p.scalars[0]) s.sigma = *p.scalars[0];
+  if (p.scalars[1]) s.gamma = *p.scalars[1];
+  if (p.scalars[2]) s.alpha = *p.scalars[2];
   if (p.seeds) {  // bit 63 marks an absolute key that ignores the device base (fixed noise)
     const uint64_t b = p.seeds[0];
     if (!(p.seed_r >> 63)) s.kr = mix64(b ^ p.seed_r);

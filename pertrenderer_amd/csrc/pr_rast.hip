@@ -775,70 +775,165 @@ PR_DEV void slot_grad(const PRRastArgs& a, V2 p, const float* v, int64_t o, floa
   g[6] = gbv[2].x + gdv[2].x; g[7] = gbv[2].y + gdv[2].y; g[8] = gzb * bc[2] + gz[2];
 }
 
-constexpr int kHash = 512;     // LDS table entries per workgroup (distinct faces of one tile)
-constexpr int kBwdTile = 8;    // 8 pixels wide; rows per tile chosen at launch (default 8)
+constexpr int kHash = 512;      // LDS hash entries per workgroup (distinct faces of one tile)
+constexpr int kBwdTile = 8;     // tile width; rows per tile (<= 8) chosen at launch
 constexpr int kBwdThreads = 256;
+constexpr int kBwdEnt = 512;    // slots scanned (and at most valid) per round: 2 per thread
+constexpr int kBwdFaces = 128;  // faces per tile reduced by the transpose; later ones use global atomics
 
-// One 256-thread workgroup per 8 x tile_rows pixel tile.  The tile's slots share few
-// faces, so an LDS hash keyed by face id pre-reduces the 9 vertex-gradient components;
-// the flush then adds each (face, component) once to global memory.  Global float
-// atomics run at the memory side at a per-byte rate that collapses when a wave's 64
-// lanes hit 64 scattered rows (MI355X guide, Global float atomics), so the flush walks
-// (entry, component) lane-contiguously (36-B runs per face).  Small tiles keep the
-// heavy (foreground) work spread over all CUs: 8x4 measured fastest (8x2, 8x8, 16x16 slower).  Tile rows
-// are contiguous ncols*K slot ranges: coalesced reads.
-__global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int tile_rows) {
+// q = i / d, r = i - q d for 0 <= i < 2^20 and 0 < d < 2^20 (float reciprocal + one correction)
+PR_DEV int divmod_small(int i, int d, float inv_d, int& r) {
+  int q = (int)((float)i * inv_d);
+  r = i - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+  return q;
+}
+
+// One 256-thread workgroup per 8 x tile_rows pixel tile (tile_rows <= 8), rounds of
+// kBwdEnt slots.  No per-slot atomics on the gradient values (LDS float atomics cost
+// ~4 cycles per lane on gfx950, and a slot has 9 components):
+//  1. scan: the round's slots (tile rows are contiguous ncols*K slot ranges: coalesced
+//     p2f reads) are compacted into an LDS list of the valid ones (wave ballot, one
+//     LDS append per wave); each new face id gets a tile-local index through an LDS
+//     hash (one CAS per slot, a second atomic per distinct face).
+//  2. gradient: one lane per valid slot, densely: the 9 vertex-gradient components go
+//     to gbuf[entry] (plain LDS stores) and the entry index to M[face][pixel] (a pixel
+//     holds a face at most once, so every (face, pixel) cell has one writer).
+//  3. transpose: the owner lane of each tile-local face walks its M row (the tile's
+//     pixels) and sums its entries' gbuf rows in registers.
+//  4. after the last round the owners' sums go to LDS and the flush adds each (face,
+//     component) once to global memory, lane-contiguously (global float atomics run at
+//     the memory side; 64 lanes on 64 scattered rows collapse that rate — MI355X guide,
+//     Global float atomics).
+// Faces past the first kBwdFaces of a tile, and hash overflow, add their slots straight
+// to global memory (correct, slower; dense meshes under large tiles only).
+template <int ROWS>
+__global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a) {
+  constexpr int tile_rows = ROWS, TP = kBwdTile * ROWS;  // tile pixels
   __shared__ int hkey[kHash];
-  __shared__ float hval[kHash * 9];
-  __shared__ int hlist[kHash];   // compacted used entries
-  __shared__ int hcount;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < kHash; i += kBwdThreads) hkey[i] = -1;
-  for (int i = tid; i < kHash * 9; i += kBwdThreads) hval[i] = 0.f;
-  if (tid == 0) hcount = 0;
-  __syncthreads();
+  __shared__ int hfl[kHash];                      // tile-local face index of a hash entry
+  __shared__ int flist[kBwdFaces];                // face id of each tile-local index
+  __shared__ uint16_t M[kBwdFaces * TP];          // [face][pixel] -> entry index of this round
+  __shared__ float gbuf[9 * kBwdEnt];             // [component][entry]; reused for the sums
+  __shared__ int2 clist[kBwdEnt];                 // (pixel << 16 | k, face id)
+  __shared__ int ccount, nface;
+  __shared__ float pxs[kBwdTile], pys[ROWS];
+  const int tid = threadIdx.x, lane = tid & 63;
   const int K = a.K, H = a.H, W = a.W;
   const int n = blockIdx.z, row0 = blockIdx.y * tile_rows, col0 = blockIdx.x * kBwdTile;
   const int ncols = min(kBwdTile, W - col0), nrows = min(tile_rows, H - row0);
   const int per_row = ncols * K;
   const int total = nrows * per_row;
-  // (row, slot-in-row) tracked incrementally: no integer division in the loop
-  const int q = kBwdThreads / per_row, rr = kBwdThreads - q * per_row;
-  for (int i = tid, r = tid / per_row, rem = tid - (tid / per_row) * per_row; i < total;
-       i += kBwdThreads, r += q, rem += rr, (rem >= per_row ? (rem -= per_row, ++r) : 0)) {
-    const int64_t o = (((int64_t)n * H + row0 + r) * W + col0) * K + rem;
-    const int64_t f = a.pix_to_face[o];
-    if (f < 0) continue;
-    const int c = rem / K;
-    const int row = row0 + r, col = col0 + c;
-    const V2 p{ndc(W - 1 - col, W, H), ndc(H - 1 - row, H, W)};
-    float g[9];
-    slot_grad(a, p, a.face_verts + f * 9, o, g);
-    // LDS hash pre-reduction (linear probing; overflow goes straight to global)
-    uint32_t h = ((uint32_t)f * 2654435761u) & (kHash - 1);
-    bool done = false;
-    for (int probe = 0; probe < 32 && !done; ++probe) {
-      const int cur = atomicCAS(&hkey[h], -1, (int)f);
-      if (cur == -1 || cur == (int)f) {
-        if (cur == -1) hlist[atomicAdd(&hcount, 1)] = (int)h;
+  const float inv_row = 1.f / (float)per_row, inv_k = 1.f / (float)K;
+  const int64_t tile_o = (((int64_t)n * H + row0) * W + col0) * K;  // slot offset of the tile's first row
+  const int64_t row_stride = (int64_t)W * K;
+  for (int i = tid; i < kHash; i += kBwdThreads) hkey[i] = -1;
+  for (int i = tid; i < kBwdFaces * TP; i += kBwdThreads) M[i] = 0xffff;
+  if (tid < kBwdTile) pxs[tid] = ndc(W - 1 - min(col0 + tid, W - 1), W, H);
+  if (tid >= 64 && tid < 64 + ROWS) pys[tid - 64] = ndc(H - 1 - min(row0 + tid - 64, H - 1), H, W);
+  if (tid == 0) nface = 0;
+  float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // owner lane tid < kBwdFaces
+  for (int c0 = 0; c0 < total; c0 += kBwdEnt) {
+    if (tid == 0) ccount = 0;
+    __syncthreads();  // also: the previous round's transpose is done (M reset, gbuf free)
+    // ---- 1. scan + compaction + face registration
+    int64_t f[kBwdEnt / kBwdThreads];
 #pragma unroll
-        for (int cc = 0; cc < 9; ++cc) atomicAdd(&hval[h * 9 + cc], g[cc]);
-        done = true;
-      } else {
+    for (int u = 0; u < kBwdEnt / kBwdThreads; ++u) {
+      const int i = c0 + u * kBwdThreads + tid;
+      f[u] = -1;
+      if (i < total) {
+        int rem;
+        const int r = divmod_small(i, per_row, inv_row, rem);
+        f[u] = a.pix_to_face[tile_o + r * row_stride + rem];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBwdEnt / kBwdThreads; ++u) {
+      const bool keep = f[u] >= 0;
+      const uint64_t bal = __ballot(keep);
+      if (bal == 0) continue;
+      int off = 0;
+      if (lane == 0) off = atomicAdd(&ccount, __popcll(bal));
+      off = __shfl(off, 0);
+      if (!keep) continue;
+      const int i = c0 + u * kBwdThreads + tid;
+      int rem, k;
+      const int r = divmod_small(i, per_row, inv_row, rem);
+      const int c = divmod_small(rem, K, inv_k, k);
+      const int fi = (int)f[u];
+      clist[off + __popcll(bal & ((1ull << lane) - 1ull))] = make_int2(((r * kBwdTile + c) << 16) | k, fi);
+      uint32_t h = ((uint32_t)fi * 2654435761u) & (kHash - 1);
+      for (int probe = 0; probe < 32; ++probe) {
+        const int cur = atomicCAS(&hkey[h], -1, fi);
+        if (cur == -1) {  // first slot of this face in the tile: assign its local index
+          const int fl = atomicAdd(&nface, 1);
+          hfl[h] = fl;
+          if (fl < kBwdFaces) flist[fl] = fi;
+          break;
+        }
+        if (cur == fi) break;
         h = (h + 1) & (kHash - 1);
       }
     }
-    if (!done) {
+    __syncthreads();
+    // ---- 2. dense per-slot gradients
+    const int nv = ccount;
+    for (int j = tid; j < nv; j += kBwdThreads) {
+      const int2 e = clist[j];
+      const int pix = e.x >> 16, k = e.x & 0xffff, fi = e.y;
+      const int r = pix >> 3, c = pix & 7;
+      const int64_t o = tile_o + r * row_stride + c * K + k;
+      const V2 p{pxs[c], pys[r]};
+      float g[9];
+      slot_grad(a, p, a.face_verts + (int64_t)fi * 9, o, g);
+      uint32_t h = ((uint32_t)fi * 2654435761u) & (kHash - 1);
+      int fl = kBwdFaces;  // not found (hash overflow): global path
+      for (int probe = 0; probe < 32; ++probe) {
+        const int cur = hkey[h];
+        if (cur == fi) { fl = hfl[h]; break; }
+        if (cur == -1) break;
+        h = (h + 1) & (kHash - 1);
+      }
+      if (fl < kBwdFaces) {
 #pragma unroll
-      for (int cc = 0; cc < 9; ++cc) atomicAdd(&a.grad_face_verts[f * 9 + cc], g[cc]);
+        for (int cc = 0; cc < 9; ++cc) gbuf[cc * kBwdEnt + j] = g[cc];
+        M[fl * TP + pix] = (uint16_t)j;
+      } else {
+#pragma unroll
+        for (int cc = 0; cc < 9; ++cc) atomicAdd(&a.grad_face_verts[(int64_t)fi * 9 + cc], g[cc]);
+      }
+    }
+    __syncthreads();
+    // ---- 3. transpose: owner lanes sum their face's entries (and reset their M row)
+    if (tid < min(nface, kBwdFaces)) {
+      uint16_t* row = M + tid * TP;
+      for (int q = 0; q < nrows * kBwdTile; q += 4) {
+        const uint64_t four = *reinterpret_cast<const uint64_t*>(row + q);
+        if (four == ~0ull) continue;
+        *reinterpret_cast<uint64_t*>(row + q) = ~0ull;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t jj = (uint32_t)(four >> (16 * t)) & 0xffffu;
+          if (jj == 0xffffu) continue;
+#pragma unroll
+          for (int cc = 0; cc < 9; ++cc) acc[cc] += gbuf[cc * kBwdEnt + jj];
+        }
+      }
     }
   }
   __syncthreads();
-  // flush: lane-contiguous over (used entry, component)
-  const int nflush = hcount * 9;
-  for (int i = tid; i < nflush; i += kBwdThreads) {
-    const int e = hlist[i / 9], cc = i - (i / 9) * 9;
-    atomicAdd(&a.grad_face_verts[(int64_t)hkey[e] * 9 + cc], hval[e * 9 + cc]);
+  // ---- 4. flush: sums to LDS, then lane-contiguous over (face, component)
+  const int nf = min(nface, kBwdFaces);
+  if (tid < nf) {
+#pragma unroll
+    for (int cc = 0; cc < 9; ++cc) gbuf[tid * 9 + cc] = acc[cc];
+  }
+  __syncthreads();
+  for (int i = tid; i < nf * 9; i += kBwdThreads) {
+    const int fl = i / 9, cc = i - fl * 9;
+    atomicAdd(&a.grad_face_verts[(int64_t)flist[fl] * 9 + cc], gbuf[i]);
   }
 }
 
@@ -1015,11 +1110,15 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
     if (hipMemsetAsync(a.grad_face_verts, 0, (size_t)a.F * 9 * sizeof(float), st) != hipSuccess)
       return set_error(PR_ERR_HIP, "rast_bwd: memset failed");
   }
-  // rows per 8-wide workgroup tile; PR_RAST_BWD_ROWS overrides (sweeps)
+  // rows per 8-wide workgroup tile: 2 measured fastest on the bench frame (more, smaller
+  // workgroups hide the per-round latency chain); PR_RAST_BWD_ROWS=4|8 overrides (sweeps)
   const char* er = getenv("PR_RAST_BWD_ROWS");
-  const int rows = er && atoi(er) > 0 && atoi(er) <= 64 ? atoi(er) : 4;  // 8x4 measured best
+  const int rows = er && (atoi(er) == 1 || atoi(er) == 4 || atoi(er) == 8) ? atoi(er) : 2;
   dim3 grid((a.W + kBwdTile - 1) / kBwdTile, (a.H + rows - 1) / rows, a.N);
-  rast_bwd_kernel<<<grid, kBwdThreads, 0, st>>>(a, rows);
+  if (rows == 8) rast_bwd_kernel<8><<<grid, kBwdThreads, 0, st>>>(a);
+  else if (rows == 4) rast_bwd_kernel<4><<<grid, kBwdThreads, 0, st>>>(a);
+  else if (rows == 1) rast_bwd_kernel<1><<<grid, kBwdThreads, 0, st>>>(a);
+  else rast_bwd_kernel<2><<<grid, kBwdThreads, 0, st>>>(a);
   return check_launch("rast_bwd");
 }
 

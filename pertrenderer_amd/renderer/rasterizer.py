@@ -78,6 +78,7 @@ class _RasterizeFn(torch.autograd.Function):
         ctx.save_for_backward(fv, first, nfaces, p2f)
         ctx.cfg = (H, W, K, float(blur), int(persp), int(clip), int(cull))
         ctx.mark_non_differentiable(p2f)
+        ctx.set_materialize_grads(False)  # no zero-filled int64 grad for pix_to_face
         return p2f, zbuf, bary, dists
 
     @staticmethod

@@ -112,6 +112,30 @@ def test_rasterizer_backward_matches_oracle(persp, clip, device):
     assert_close(fvt.grad, ref, rtol=1e-4, atol_rel=1e-5, name="grad_face_verts")
 
 
+@pytest.mark.parametrize("F,H,K,size", [(400, 16, 50, 0.5), (900, 20, 120, 0.9), (60, 40, 8, 0.2)])
+def test_rasterizer_backward_dense_tiles(F, H, K, size, device):
+    """Tiles with more valid slots than one backward round (1024) and more distinct faces than the
+    tile-local transpose holds (128: the global-atomic overflow path), plus a sparse case; two meshes."""
+    fv = np.concatenate([_soup(F, 11, spread=0.6, size=size), _soup(F // 2, 12, spread=0.6, size=size)])
+    first, nf = np.array([0, F]), np.array([F, F // 2])
+    blur = 2e-2
+    fvt, (p2f, zbuf, bary, dists) = _run_native(fv, first, nf, H, H, K, blur, False, True, False, device)
+    pc = p2f.cpu().numpy()
+    g = np.random.default_rng(13)
+    gz = g.standard_normal(zbuf.shape).astype(np.float32)
+    gb = g.standard_normal(bary.shape).astype(np.float32)
+    gd = g.standard_normal(dists.shape).astype(np.float32)
+    loss = (zbuf * torch.tensor(gz, device=device)).sum() + (bary * torch.tensor(gb, device=device)).sum() \
+        + (dists * torch.tensor(gd, device=device)).sum()
+    loss.backward()
+    ref = rast_ref.rast_bwd(fv, pc, gz, gb, gd, False, True)
+    assert_close(fvt.grad, ref, rtol=1e-4, atol_rel=1e-5, name="grad_face_verts")
+    if K >= 50:
+        per_tile = (pc[0, :8, :8] >= 0).sum()
+        faces_tile = len(np.unique(pc[0, :8, :8][pc[0, :8, :8] >= 0]))
+        assert per_tile > 1024 and faces_tile > 128, (per_tile, faces_tile)
+
+
 def test_interpolation_matches_oracle_and_backward(device):
     rng = np.random.default_rng(5)
     F, D = 300, 4
