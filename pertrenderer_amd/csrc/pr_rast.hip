@@ -26,7 +26,7 @@ namespace pr {
 namespace {
 
 constexpr float kEps = 1e-8f;  // PyTorch3D kEpsilon
-constexpr int kTile = 8;       // 8x8 pixels per wave
+constexpr int kTile = 4;       // narrowest forward tile width (4x4 tiles at 4 slices)
 
 struct V2 {
   float x, y;
@@ -108,7 +108,8 @@ struct FaceRec {
   float4 f;  // D20.x D20.y l2_20 z_min   (D20 = v0 - v2)
 };
 
-__global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cull_backfaces, FaceRec* out) {
+__global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cull_backfaces, FaceRec* out,
+                                 float4* bbox) {
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < F; f += (int64_t)gridDim.x * blockDim.x) {
     const float* v = fv + f * 9;
     const float x0 = v[0], y0 = v[1], z0 = v[2], x1 = v[3], y1 = v[4], z1 = v[5], x2 = v[6], y2 = v[7], z2 = v[8];
@@ -131,7 +132,17 @@ __global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cul
     rec.e = make_float4(d01x, d01y, d12x, d12y);
     rec.f = make_float4(d20x, d20y, d20x * d20x + d20y * d20y, fminf(z0, fminf(z1, z2)));
     out[f] = rec;
+    bbox[f] = make_float4(xmin, xmax, ymin, ymax);
   }
+}
+
+// q = i / d, r = i - q d for 0 <= i < 2^20 and 0 < d < 2^20 (float reciprocal + one correction)
+PR_DEV int divmod_small(int i, int d, float inv_d, int& r) {
+  int q = (int)((float)i * inv_d);
+  r = i - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+  return q;
 }
 
 PR_DEV bool key_less(float za, int fa, float zb, int fb) { return za < zb || (za == zb && fa < fb); }
@@ -150,13 +161,13 @@ PR_DEV float seg_dist2_d(V2 p, V2 a, float bax, float bay, float l2, V2 b) {
   return l2 <= kEps ? db : ds;
 }
 
-// Full per-pixel test of one face, branch-free so that several faces' division
-// chains interleave (one wave per SIMD: ILP is the latency hiding).  Same decisions
-// as PyTorch3D's per-face body: in bbox -> bary -> perspective -> clip -> pz >= 0 ->
-// inside or dist < blur.  Perspective correction / clipping are compile-time.
+// Per-pixel evaluation of one face from its record: (clipped) barycentrics, their
+// depth, the inside flag and the squared distance to the nearest edge, with exactly
+// the operations of bary_fwd / persp_fwd / clip_fwd / tri_dist2 (bit-identical).
+// Branch-free so that several faces' division chains interleave (ILP is the latency
+// hiding at one wave per SIMD).  Perspective correction / clipping are compile-time.
 template <bool PERSP, bool CLIP>
-PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, float& pz) {
-  const bool inbox = !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
+PR_DEV void face_eval(const FaceRec& r, V2 p, float bc[3], float& pz, bool& inside, float& d) {
   const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
   const float z0 = r.a.z, z1 = r.b.y, z2 = r.c.x;
   const float area = r.d.y;
@@ -167,23 +178,32 @@ PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, float& pz) {
   float b[3] = {e0 / area, e1 / area, e2 / area};
   if constexpr (PERSP) {
     const float t0 = b[0] * z1 * z2, t1 = z0 * b[1] * z2, t2 = z0 * z1 * b[2];
-    float d = t0 + t1 + t2;
-    d = d > kEps ? d : kEps;
-    b[0] = t0 / d; b[1] = t1 / d; b[2] = t2 / d;
+    float s = t0 + t1 + t2;
+    s = s > kEps ? s : kEps;
+    b[0] = t0 / s; b[1] = t1 / s; b[2] = t2 / s;
   }
   if constexpr (CLIP) {
-    float bc[3];
     clip_fwd(b, bc);
-    pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
   } else {
-    pz = b[0] * z0 + b[1] * z1 + b[2] * z2;
+    bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2];
   }
-  const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
+  pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
+  inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
   const float d01 = seg_dist2_d(p, v0, r.e.x, r.e.y, r.d.z, v1);
   const float d02 = seg_dist2_d(p, v0, -r.f.x, -r.f.y, r.f.z, v2);
   const float d12 = seg_dist2_d(p, v1, r.e.z, r.e.w, r.d.w, v2);
-  float d = d01 < d02 ? d01 : d02;
+  d = d01 < d02 ? d01 : d02;
   d = d < d12 ? d : d12;
+}
+
+// PyTorch3D's per-face decisions: in bbox -> bary -> perspective -> clip -> pz >= 0 ->
+// inside or dist < blur
+template <bool PERSP, bool CLIP>
+PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, float& pz) {
+  const bool inbox = !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
+  float bc[3], d;
+  bool inside;
+  face_eval<PERSP, CLIP>(r, p, bc, pz, inside, d);
   return inbox && !(pz < 0.f) && (inside || d < blur);
 }
 
@@ -192,15 +212,24 @@ PR_DEV bool in_bbox(const FaceRec& r, V2 p) {
 }
 
 #ifdef PR_RAST_PROFILE
+constexpr unsigned kProfTiles = 1 << 16;
+__device__ long long g_rast_prof[kProfTiles * 16];  // per tile: x y z list t0 t1 hwid stamps[6] SL
 #define PR_STAMP(i) (stamp[i] += (long long)__builtin_amdgcn_s_memtime() - t_, t_ = __builtin_amdgcn_s_memtime())
 #else
 #define PR_STAMP(i) ((void)0)
 #endif
 
-constexpr int kCap = 512;    // per-round tile face list (faces beyond it are handled in later rounds)
-static_assert(kCap <= 8 * 64, "suffix-min pass holds kCap / 64 <= 8 entries per lane");
-constexpr int kCullU = 4;    // 64-face cull chunks whose loads are in flight together (per wave)
-constexpr int kGroup = 4;    // faces tested together (independent chains)
+// per-slice-count forward configuration: per-round tile face list capacity (faces beyond
+// it go to later rounds), faces tested together per lane (independent chains), LDS
+// staging chunk.  Smaller tiles have shorter lists and want more resident waves
+// (LDS, VGPRs) rather than per-wave ILP.
+template <int SL> struct RastCfg {
+  static constexpr int CAP = SL == 1 ? 512 : (SL == 2 ? 256 : 128);
+  static constexpr int G = SL == 1 ? 4 : 2;
+  static constexpr int CH = SL == 4 ? 32 : 64;
+  static_assert(CAP <= 8 * 64, "suffix-min pass holds CAP / 64 <= 8 entries per lane");
+};
+constexpr int kCullU = 16;   // 64-face cull chunks whose boxes are in flight together
 
 // Bitonic sort (ascending key) of n2 (power of two) LDS entries by NT threads.
 template <int NT>
@@ -277,117 +306,121 @@ PR_DEV void wave_sort_lds(float* lkey, int* lidx, int lane) {
 
 PR_DEV bool ekey_less(float2 x, float2 y) { return key_less(x.x, __float_as_int(x.y), y.x, __float_as_int(y.y)); }
 
-// In-place merge of the lane's sorted columns A (a entries) and B (b entries), keys
-// all distinct: A[0..m) becomes the m = min(K, a+b) smallest, ascending.  Runs from
-// the back (writes land at or above A's read cursor); the a+b-m largest are dropped.
-PR_DEV int merge_columns(float2* A, const float2* B, int a, int b, int K, int lane) {
-  const int m = min(K, a + b);
-  int i = a - 1, j = b - 1;
-  float2 ea = i >= 0 ? A[i * 64 + lane] : make_float2(0.f, 0.f);
-  float2 eb = j >= 0 ? B[j * 64 + lane] : make_float2(0.f, 0.f);
-  for (int skip = a + b - m; skip > 0; --skip) {
-    if (j < 0 || (i >= 0 && ekey_less(eb, ea))) { --i; if (i >= 0) ea = A[i * 64 + lane]; }
-    else { --j; if (j >= 0) eb = B[j * 64 + lane]; }
-  }
-  for (int pos = m - 1; j >= 0; --pos) {  // once B is exhausted A[0..i] is already in place
-    if (i >= 0 && ekey_less(eb, ea)) {
-      A[pos * 64 + lane] = ea;
-      --i;
-      if (i >= 0) ea = A[i * 64 + lane];
-    } else {
-      A[pos * 64 + lane] = eb;
-      --j;
-      if (j >= 0) eb = B[j * 64 + lane];
+template <int SL>
+size_t rast_fwd_lds_sl(int K) {
+  using C = RastCfg<SL>;
+  return C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL) * 8 + (size_t)C::CAP * 12 + 64 * 4 + C::CH * 8 + 16;
+}
+
+size_t rast_fwd_lds(int K, int SL) {
+  return SL == 4 ? rast_fwd_lds_sl<4>(K) : (SL == 2 ? rast_fwd_lds_sl<2>(K) : rast_fwd_lds_sl<1>(K));
+}
+
+// v from the lane of the same pixel that holds slice s (lane = pixel * SL + slice):
+// one DPP quad permutation
+template <int SL>
+PR_DEV int from_slice(int v, int s) {
+  if constexpr (SL == 1) {
+    return v;
+  } else if constexpr (SL == 2) {
+    switch (s) {
+      case 0: return __builtin_amdgcn_update_dpp(0, v, 0xA0, 0xf, 0xf, false);  // quad_perm [0,0,2,2]
+      default: return __builtin_amdgcn_update_dpp(0, v, 0xF5, 0xf, 0xf, false); // quad_perm [1,1,3,3]
+    }
+  } else {
+    switch (s) {
+      case 0: return __builtin_amdgcn_update_dpp(0, v, 0x00, 0xf, 0xf, false);  // quad_perm [0,0,0,0]
+      case 1: return __builtin_amdgcn_update_dpp(0, v, 0x55, 0xf, 0xf, false);
+      case 2: return __builtin_amdgcn_update_dpp(0, v, 0xAA, 0xf, 0xf, false);
+      default: return __builtin_amdgcn_update_dpp(0, v, 0xFF, 0xf, 0xf, false);
     }
   }
-  return m;
 }
 
-template <bool PERSP, bool CLIP>
-void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, dim3 grid, int wv, size_t lds, hipStream_t st);
-
-size_t rast_fwd_lds(int K, int WV) {
-  return (size_t)WV * 64 * sizeof(FaceRec) + (size_t)WV * K * 64 * 8 + (size_t)kCap * 12 + (size_t)WV * 64 * 4 + 16;
-}
-
-// Forward, pass 1: per-pixel K nearest (z, face) keys -> pix_to_face, zbuf.
-// One workgroup of WV waves per 8x8 tile, one lane per pixel.  Per round: the waves
-// cull the mesh's faces against the tile (ballot compaction, LDS append), sort the
-// survivors by their depth near the tile centre, then wave w walks sorted positions
-// w, w+WV, ... in 64-face chunks staged in its own LDS slice, testing kGroup faces
-// at once (broadcast reads, independent chains) into its own per-pixel K-queue (an
-// LDS column sorted by (z, face id), PyTorch3D's order).  The WV queues are then
-// merged per pixel.  The final queue is the K smallest keys of all candidates, so
-// it does not depend on WV or on the traversal order.  WV > 1 spreads a heavy
-// tile over several SIMDs and lets the dispatcher balance light and heavy tiles.
-// Barycentrics / distances of the winners come from rast_frag_kernel.
-template <int WV, bool PERSP, bool CLIP>
-__global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces) {
+// Forward: per-pixel K nearest (z, face) keys -> pix_to_face, zbuf (+ barycentrics and
+// signed distances with FRAG).  One wave per tile of TP = 64 / SL pixels (8x8, 8x4 or
+// 4x4); lane = pixel * SL + slice.  The SL lanes of a pixel (one DPP quad) split the
+// tile's face list -- slice h tests sorted positions h, h+SL, ... -- and share ONE
+// K-queue per pixel in LDS: after each test group the slices insert their candidates
+// in turn, the pixel's queue state (size, last key) travelling between them by DPP.
+// Slicing cuts the heaviest tiles' serial face loop (the kernel's critical path) by SL
+// while the per-pixel queue keeps LDS at K*TP*8 B, so several tiles share a SIMD.
+// Per round: cull the mesh's faces against the tile (boxes of 16 chunks in flight,
+// ballot compaction), sort the survivors by their depth near the tile centre, then
+// walk the sorted list in CH-face chunks staged in LDS, each lane testing kGroup faces
+// at once (independent chains).  The queue is an LDS column sorted by (z, face id),
+// PyTorch3D's order, and ends as the K smallest keys of all candidates: it depends
+// neither on SL nor on the traversal order.
+template <int SL, bool PERSP, bool CLIP, bool FRAG>
+__global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces,
+                                                      const float4* __restrict__ fbox) {
+  constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
+  constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
   extern __shared__ float smem[];
-  constexpr int NT = 64 * WV;
   const int K = a.K;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  FaceRec* lrec = reinterpret_cast<FaceRec*>(smem) + wv * 64;        // [WV][64] staged chunk per wave
-  float2* qall = reinterpret_cast<float2*>(reinterpret_cast<FaceRec*>(smem) + WV * 64);
-  float2* q = qall + (size_t)wv * K * 64;                              // [WV][K][64] per-wave queues
-  int* lfid = reinterpret_cast<int*>(qall + (size_t)WV * K * 64);      // [kCap] tile face list (cull order)
-  float* lkey = reinterpret_cast<float*>(lfid + kCap);                 // [kCap] sort key, then
-  float* lsuf = lkey;                                                  //   suffix min of z_min
-  int* lidx = reinterpret_cast<int*>(lkey + kCap);                     // [kCap] sorted -> cull order
-  int* qsz = lidx + kCap;                                              // [WV][64] queue sizes
-  int* lcount = qsz + WV * 64;                                         // cull append counter
+  const int lane = threadIdx.x, pix = lane / SL, slice = lane % SL;
+  FaceRec* lrec = reinterpret_cast<FaceRec*>(smem);                // [CH] staged chunk
+  float2* q = reinterpret_cast<float2*>(lrec + CH);                 // [K][TP] per-pixel queues
+  int* lfid = reinterpret_cast<int*>(q + (size_t)K * TP);           // [kCap] tile face list (cull order)
+  float* lkey = reinterpret_cast<float*>(lfid + kCap);              // [kCap] sort key, then
+  float* lsuf = lkey;                                               //   suffix min of z_min
+  int* lidx = reinterpret_cast<int*>(lkey + kCap);                  // [kCap] sorted -> cull order
+  int* qsz = lidx + kCap;                                           // [64] queue sizes (per pixel)
+  int* lcf = qsz + 64;                                              // [CH] staged chunk face ids
+  float* lcs = reinterpret_cast<float*>(lcf + CH);                  // [CH] staged chunk suffix mins
   const int n = blockIdx.z;
   const int H = a.H, W = a.W;
-  const int row0 = blockIdx.y * kTile, col0 = blockIdx.x * kTile;
-  const int row = row0 + lane / kTile, col = col0 + lane % kTile;
+  const int row0 = blockIdx.y * TH, col0 = blockIdx.x * TW;
+  const int row = row0 + pix / TW, col = col0 + pix % TW;
   const bool inimg = row < H && col < W;
   const V2 p{ndc(W - 1 - min(col, W - 1), W, H), ndc(H - 1 - min(row, H - 1), H, W)};
   // tile rectangle in NDC (pixel centres); +X points left, +Y up
-  const int c1 = min(col0 + kTile - 1, W - 1), r1 = min(row0 + kTile - 1, H - 1);
+  const int c1 = min(col0 + TW - 1, W - 1), r1 = min(row0 + TH - 1, H - 1);
   const float txmax = ndc(W - 1 - col0, W, H), txmin = ndc(W - 1 - c1, W, H);
   const float tymax = ndc(H - 1 - row0, H, W), tymin = ndc(H - 1 - r1, H, W);
   const float tcx = 0.5f * (txmin + txmax), tcy = 0.5f * (tymin + tymax);
   const int64_t fb = a.mesh_first_face[n], fe = fb + a.mesh_num_faces[n];
   constexpr bool clip = CLIP;
   const float blur = a.blur_radius;
+  // the pixel's queue state, replicated in its SL lanes
   int qs = 0;
   float qlast_z = __builtin_inff();
   int qlast_f = 0x7fffffff;
   int64_t base = fb;
 #ifdef PR_RAST_PROFILE
   long long stamp[6] = {0, 0, 0, 0, 0, 0}, t_ = __builtin_amdgcn_s_memtime();
-  int nlist = 0;
+  const long long rt0 = __builtin_amdgcn_s_memrealtime();
+  int nlist = 0, n_app = 0, n_ins = 0, w_ins = 0;
 #endif
   while (base < fe) {
-    // ---- gather this round's culled faces (expanded bbox overlaps the tile)
-    if (tid == 0) *lcount = 0;
-    __syncthreads();
+    // ---- gather this round's culled faces (expanded bbox overlaps the tile): kCullU
+    //      chunks' boxes in flight at once, appended in face order without atomics; a
+    //      chunk that would overflow the round's list starts the next round
     int nl = 0;
-    constexpr int U = kCullU / WV > 0 ? kCullU / WV : 1;  // chunks per wave: 64*kCullU faces per pass
-    while (base < fe && nl <= kCap - 64 * U * WV) {
-      float4 cc[U], dd[U];
+    while (base < fe && nl <= kCap - 64) {
+      float4 bb[kCullU];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t f = base + (wv * U + u) * 64 + lane;
-        const int64_t fl = f < fe ? f : fe - 1;
-        cc[u] = faces[fl].c; dd[u] = faces[fl].d;
+      for (int u = 0; u < kCullU; ++u) {
+        const int64_t f = base + u * 64 + lane;
+        bb[u] = fbox[f < fe ? f : fe - 1];
       }
+      int64_t next = base + 64 * kCullU;
+      bool stop = false;  // wave-uniform; no break, so bb[] stays in registers
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t f = base + (wv * U + u) * 64 + lane;
-        const bool keep = f < fe && !(cc[u].y > txmax || cc[u].z < txmin || cc[u].w > tymax || dd[u].x < tymin);
+      for (int u = 0; u < kCullU; ++u) {
+        const int64_t f = base + u * 64 + lane;
+        const bool keep = f < fe && !(bb[u].x > txmax || bb[u].y < txmin || bb[u].z > tymax || bb[u].w < tymin);
         const uint64_t bal = __ballot(keep);
-        if (bal == 0) continue;
-        int off = 0;
-        if (lane == 0) off = atomicAdd(lcount, __popcll(bal));
-        off = __shfl(off, 0);
-        if (keep) lfid[off + __popcll(bal & ((1ull << lane) - 1ull))] = (int)f;
+        const int cnt = __popcll(bal);
+        if (!stop && nl + cnt > kCap) { stop = true; next = base + u * 64; }
+        if (!stop) {
+          if (keep) lfid[nl + __popcll(bal & ((1ull << lane) - 1ull))] = (int)f;
+          nl += cnt;
+        }
       }
-      base += 64 * U * WV;
-      __syncthreads();
-      nl = *lcount;
-      __syncthreads();
+      base = next < fe ? next : fe;
     }
+    __syncthreads();
     PR_STAMP(0);
 #ifdef PR_RAST_PROFILE
     nlist += nl;
@@ -399,7 +432,7 @@ __global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const F
     //      appends).  Exactness does not depend on it; the early exit uses z_min.
     int n2 = 64;
     while (n2 < nl) n2 <<= 1;
-    for (int i = tid; i < n2; i += NT) {
+    for (int i = lane; i < n2; i += 64) {
       float key = __builtin_inff();
       if (i < nl) {
         const FaceRec& r = faces[lfid[i]];
@@ -421,207 +454,257 @@ __global__ void __launch_bounds__(64 * WV) rast_fwd_kernel(PRRastArgs a, const F
     }
     __syncthreads();
     PR_STAMP(1);
-    if (wv == 0) {
-      if (n2 == 64) wave_sort_lds<1>(lkey, lidx, lane);
-      else if (n2 == 128) wave_sort_lds<2>(lkey, lidx, lane);
-      else if (n2 == 256) wave_sort_lds<4>(lkey, lidx, lane);
-      else wave_sort_lds<8>(lkey, lidx, lane);
-    }
+    if (n2 == 64) wave_sort_lds<1>(lkey, lidx, lane);
+    else if (kCap >= 128 && n2 == 128) wave_sort_lds<2>(lkey, lidx, lane);
+    else if (kCap >= 256 && n2 == 256) wave_sort_lds<4>(lkey, lidx, lane);
+    else if constexpr (kCap >= 512) wave_sort_lds<8>(lkey, lidx, lane);
     __syncthreads();
     PR_STAMP(2);
     // suffix minimum of z_min along the sorted order (faces after position i cannot
-    // produce pz below lsuf[i] when barycentrics are clipped); wave 0 computes it
+    // produce pz below lsuf[i] when barycentrics are clipped)
     {
       const int per = (nl + 63) / 64;  // contiguous run of sorted positions per lane
       const int i0 = lane * per, i1 = min(nl, i0 + per);
       float zl[8];  // z_min of this lane's run (per <= kCap / 64)
-      float run = __builtin_inff();
-      if (wv == 0) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) zl[u] = i0 + u < i1 ? faces[lfid[lidx[i0 + u]]].f.w : __builtin_inff();
-        float m = __builtin_inff();
+      for (int u = 0; u < 8; ++u) zl[u] = i0 + u < i1 ? faces[lfid[lidx[i0 + u]]].f.w : __builtin_inff();
+      float m = __builtin_inff();
 #pragma unroll
-        for (int u = 0; u < 8; ++u) m = fminf(m, zl[u]);
-        // exclusive suffix-min across lanes (lanes above this one)
-        float ex = m;
+      for (int u = 0; u < 8; ++u) m = fminf(m, zl[u]);
+      // exclusive suffix-min across lanes (lanes above this one)
+      float ex = m;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const float t = __shfl_down(ex, o);
-          if (lane + o < 64) ex = fminf(ex, t);
-        }
-        run = __shfl_down(ex, 1);
-        if (lane == 63) run = __builtin_inff();
+      for (int o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_down(ex, o);
+        if (lane + o < 64) ex = fminf(ex, t);
       }
-      __syncthreads();  // lsuf aliases lkey: every thread is past its sorted reads
-      if (wv == 0) {
+      float run = __shfl_down(ex, 1);
+      if (lane == 63) run = __builtin_inff();
+      __syncthreads();  // lsuf aliases lkey: every lane is past its sorted reads
 #pragma unroll
-        for (int u = 7; u >= 0; --u) {
-          run = fminf(run, zl[u]);
-          if (i0 + u < i1) lsuf[i0 + u] = run;
-        }
+      for (int u = 7; u >= 0; --u) {
+        run = fminf(run, zl[u]);
+        if (i0 + u < i1) lsuf[i0 + u] = run;
       }
     }
     __syncthreads();
     PR_STAMP(3);
-    // ---- traversal: this wave's sorted positions wv, wv+WV, ... in chunks of 64
-    const int nmine = nl > wv ? (nl - wv + WV - 1) / WV : 0;
-    // the chunk's records are gathered one chunk ahead (registers), so the global
-    // latency of chunk c+1 overlaps the tests of chunk c
-    FaceRec nrec;
+    // ---- traversal in chunks of CH sorted positions; the chunk's records are gathered
+    //      one chunk ahead (registers), so the global latency of chunk c+1 overlaps the
+    //      tests of chunk c
+    float4 nra, nrb, nrc, nrd, nre, nrf;  // next chunk's record (explicit registers: no scratch)
     int nfid = 0;
     float nsuf = 0.f;
-    if (nmine > 0) {
-      const int cnt = min(64, nmine);
-      const int sp = wv + WV * min(lane, cnt - 1);
+    if (lane < CH) {
+      const int sp = min(lane, nl - 1);
       nfid = lfid[lidx[sp]];
       nsuf = lsuf[sp];
-      nrec = faces[nfid];
+      const FaceRec* fp = faces + nfid;
+      nra = fp->a; nrb = fp->b; nrc = fp->c; nrd = fp->d; nre = fp->e; nrf = fp->f;
     }
-    for (int c0 = 0; c0 < nmine && __ballot(!done) != 0; c0 += 64) {
-      const int cnt = min(64, nmine - c0);
-      // lane i holds chunk entry i's face id and suffix-min z (read back with readlane)
-      const int cfid = nfid;
-      const float csuf = nsuf;
+    for (int c0 = 0; c0 < nl && __ballot(!done) != 0; c0 += CH) {
+      const int cnt = min(CH, nl - c0);
       __builtin_amdgcn_wave_barrier();
-      if (lane < cnt) lrec[lane] = nrec;
+      if (lane < cnt) {
+        FaceRec& d = lrec[lane];
+        d.a = nra; d.b = nrb; d.c = nrc; d.d = nrd; d.e = nre; d.f = nrf;
+        lcf[lane] = nfid;
+        lcs[lane] = nsuf;
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      if (c0 + 64 < nmine) {
-        const int ncnt = min(64, nmine - c0 - 64);
-        const int sp = wv + WV * (c0 + 64 + min(lane, ncnt - 1));
+      if (c0 + CH < nl && lane < CH) {
+        const int sp = c0 + CH + min(lane, nl - c0 - CH - 1);
         nfid = lfid[lidx[sp]];
         nsuf = lsuf[sp];
-        nrec = faces[nfid];
+        const FaceRec* fp = faces + nfid;
+        nra = fp->a; nrb = fp->b; nrc = fp->c; nrd = fp->d; nre = fp->e; nrf = fp->f;
       }
-      for (int t = 0; t < cnt; t += kGroup) {
-        bool cand[kGroup];
+      const int steps = (cnt + SL - 1) / SL;  // positions per slice in this chunk (upper bound)
+      for (int t = 0; t < steps; t += kGroup) {
+        bool cand[kGroup], ok[kGroup];
         float pzv[kGroup];
+        int idx[kGroup];
         FaceRec rr[kGroup];
         bool any = false;
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j) rr[j] = lrec[min(t + j, cnt - 1)];  // one LDS wait per group
+        for (int j = 0; j < kGroup; ++j) {
+          idx[j] = (t + j) * SL + slice;
+          ok[j] = idx[j] < cnt;
+          rr[j] = lrec[min(idx[j], cnt - 1)];  // one LDS wait per group
+        }
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j) any |= t + j < cnt && __ballot(in_bbox(rr[j], p)) != 0;
+        for (int j = 0; j < kGroup; ++j) any |= __ballot(ok[j] && in_bbox(rr[j], p)) != 0;
         if (!any) continue;
+#ifdef PR_RAST_PROFILE
+        const int ins_before = n_ins;
+#endif
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j) cand[j] = face_test<PERSP, CLIP>(rr[j], p, blur, pzv[j]) && t + j < cnt;
+        for (int j = 0; j < kGroup; ++j) cand[j] = face_test<PERSP, CLIP>(rr[j], p, blur, pzv[j]) && ok[j];
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
-          if (t + j >= cnt) break;
           // clipped barycentrics make pz a convex combination of the vertex depths, so
-          // pz >= z_min for this and every later face (up to rounding: 1e-6 margin)
-          const float zk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, csuf), t + j));
-          if (clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
-          if (done || !cand[j]) continue;
-          const int fid = __builtin_amdgcn_readlane(cfid, t + j);
-          const float pz = pzv[j];
-          // (qlast_z, qlast_f) = the queue's last (largest) key, kept in registers
-          if (qs == K && !key_less(pz, fid, qlast_z, qlast_f)) continue;
-          if (qs == 0 || key_less(qlast_z, qlast_f, pz, fid)) {
-            // append (the common case: faces arrive roughly in depth order)
-            q[qs * 64 + lane] = make_float2(pz, __int_as_float(fid));
-            ++qs;
-            qlast_z = pz;
-            qlast_f = fid;
-            continue;
-          }
-          int pos = qs < K ? qs : K - 1;
-          if (qs < K) ++qs;
-          // shift the entries greater than the key up by one, reading up to four of
-          // them per LDS round trip
-          while (pos > 0) {
-            float2 e[4];
+          // pz >= z_min for this and every later face of the slice (up to rounding:
+          // 1e-6 margin)
+          const float zk = lcs[min(idx[j], cnt - 1)];
+          const int fid = lcf[min(idx[j], cnt - 1)];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) e[i] = q[max(pos - 1 - i, 0) * 64 + lane];
-            int sh = 0;
+          for (int sl = 0; sl < SL; ++sl) {
+            if (slice == sl && ok[j]) {
+              if (clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
+              const float pz = pzv[j];
+              // (qlast_z, qlast_f) = the queue's last (largest) key
+              if (!done && cand[j] && (qs < K || key_less(pz, fid, qlast_z, qlast_f))) {
+                if (qs == 0 || key_less(qlast_z, qlast_f, pz, fid)) {
+                  // append (the common case: faces arrive roughly in depth order)
+                  q[qs * TP + pix] = make_float2(pz, __int_as_float(fid));
+                  ++qs;
+                  qlast_z = pz;
+                  qlast_f = fid;
+#ifdef PR_RAST_PROFILE
+                  ++n_app;
+#endif
+                } else {
+#ifdef PR_RAST_PROFILE
+                  ++n_ins;
+#endif
+                  int pos = qs < K ? qs : K - 1;
+                  if (qs < K) ++qs;
+                  // shift the entries greater than the key up by one, reading up to four
+                  // of them per LDS round trip
+                  while (pos > 0) {
+                    float2 e[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              if (sh == i && pos - 1 - i >= 0 && key_less(pz, fid, e[i].x, __float_as_int(e[i].y))) {
-                q[(pos - i) * 64 + lane] = e[i];
-                sh = i + 1;
+                    for (int i = 0; i < 4; ++i) e[i] = q[max(pos - 1 - i, 0) * TP + pix];
+                    int sh = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                      if (sh == i && pos - 1 - i >= 0 && key_less(pz, fid, e[i].x, __float_as_int(e[i].y))) {
+                        q[(pos - i) * TP + pix] = e[i];
+                        sh = i + 1;
+                      }
+                    }
+                    pos -= sh;
+                    if (sh < 4) break;
+                  }
+                  q[pos * TP + pix] = make_float2(pz, __int_as_float(fid));
+                  const float2 last = q[(qs - 1) * TP + pix];
+                  qlast_z = last.x;
+                  qlast_f = __float_as_int(last.y);
+                }
               }
             }
-            pos -= sh;
-            if (sh < 4) break;
+            if constexpr (SL > 1) {  // slice sl's queue state to the pixel's other lanes
+              qs = from_slice<SL>(qs, sl);
+              qlast_z = __int_as_float(from_slice<SL>(__float_as_int(qlast_z), sl));
+              qlast_f = from_slice<SL>(qlast_f, sl);
+            }
           }
-          q[pos * 64 + lane] = make_float2(pz, __int_as_float(fid));
-          const float2 last = q[(qs - 1) * 64 + lane];
-          qlast_z = last.x;
-          qlast_f = __float_as_int(last.y);
         }
+#ifdef PR_RAST_PROFILE
+        w_ins += __ballot(n_ins != ins_before) != 0;
+#endif
         if (__ballot(!done) == 0) break;
       }
     }
     __syncthreads();
     PR_STAMP(4);
   }
-  qsz[wv * 64 + lane] = inimg ? qs : 0;
+  if (slice == 0) qsz[pix] = inimg ? qs : 0;
   __syncthreads();
-  // ---- merge the WV per-wave queues into wave 0's (pairwise, from the back)
-  if constexpr (WV >= 2) {
-#pragma unroll
-    for (int step = 1; step < WV; step <<= 1) {
-      if ((wv & (2 * step - 1)) == 0) {
-        const int other = wv + step;
-        qsz[wv * 64 + lane] = merge_columns(q, qall + (size_t)other * K * 64, qsz[wv * 64 + lane],
-                                            qsz[other * 64 + lane], K, lane);
-      }
-      __syncthreads();
-    }
-  }
-  // ---- coalesced output: each tile row's 8 pixels own a contiguous 8*K slot range;
+  // ---- coalesced output: each tile row's pixels own a contiguous ncols*K slot range;
   //      the wave walks the tile's rows as one flat index (4 slots per lane in flight)
-  const float2* q0 = qall;
   {
-    const int ncols = min(kTile, W - col0), nrows = min(kTile, H - row0);
+    const int ncols = min(TW, W - col0), nrows = min(TH, H - row0);
     const int per_row = ncols * K, total = nrows * per_row;
+    const float inv_row = 1.f / (float)per_row, inv_k = 1.f / (float)K;
     constexpr int U = 4;
-    for (int base = wv * 64 * U; base < total; base += WV * 64 * U) {
+    for (int base = 0; base < total; base += 64 * U) {
       float2 e[U];
-      int sz[U], kk[U];
+      int sz[U], kk[U], cc[U], rr[U];
       int64_t o[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = min(base + u * 64 + lane, total - 1);
-        const int r = i / per_row, rem = i - r * per_row;
-        const int c = rem / K;
-        kk[u] = rem - c * K;
-        const int tl = r * kTile + c;
-        o[u] = (((int64_t)n * H + row0 + r) * W + col0) * K + rem;
-        e[u] = q0[kk[u] * 64 + tl];  // read with the size (stale beyond it, unused)
+        int rem;
+        rr[u] = divmod_small(i, per_row, inv_row, rem);
+        cc[u] = divmod_small(rem, K, inv_k, kk[u]);
+        const int tl = rr[u] * TW + cc[u];
+        o[u] = (((int64_t)n * H + row0 + rr[u]) * W + col0) * K + rem;
+        e[u] = q[kk[u] * TP + tl];  // read with the size (stale beyond it, unused)
         sz[u] = qsz[tl];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (base + u * 64 + lane >= total) break;
         const bool valid = kk[u] < sz[u];
-        a.pix_to_face[o[u]] = valid ? (int64_t)__float_as_int(e[u].y) : (int64_t)-1;
+        const int fid = __float_as_int(e[u].y);
+        a.pix_to_face[o[u]] = valid ? (int64_t)fid : (int64_t)-1;
         a.zbuf[o[u]] = valid ? e[u].x : -1.f;
+        if constexpr (FRAG) {
+          float bc[3] = {-1.f, -1.f, -1.f}, dist = -1.f;
+          if (valid) {
+            const V2 pp{ndc(W - 1 - (col0 + cc[u]), W, H), ndc(H - 1 - (row0 + rr[u]), H, W)};
+            const FaceRec r = faces[fid];
+            float pz, d;
+            bool inside;
+            face_eval<PERSP, CLIP>(r, pp, bc, pz, inside, d);
+            dist = inside ? -d : d;
+          }
+          a.dists[o[u]] = dist;
+          a.bary[o[u] * 3 + 0] = bc[0];
+          a.bary[o[u] * 3 + 1] = bc[1];
+          a.bary[o[u] * 3 + 2] = bc[2];
+        }
       }
     }
   }
 #ifdef PR_RAST_PROFILE
   __syncthreads();
   PR_STAMP(5);
-  if (tid == 0 && nlist >= 88)
-    printf("tile %d,%d WV %d list %d | cull %lld key %lld sort %lld suf %lld test %lld merge+out %lld\n", blockIdx.x,
-           blockIdx.y, WV, nlist, stamp[0], stamp[1], stamp[2], stamp[3], stamp[4], stamp[5]);
+  int n_app_tot = n_app, n_ins_tot = n_ins;
+  for (int o = 32; o > 0; o >>= 1) { n_app_tot += __shfl_xor(n_app_tot, o); n_ins_tot += __shfl_xor(n_ins_tot, o); }
+  if (lane == 0) {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const unsigned t = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (t < kProfTiles) {
+      long long* rec = g_rast_prof + (size_t)t * 16;
+      rec[0] = blockIdx.x; rec[1] = blockIdx.y; rec[2] = blockIdx.z; rec[3] = nlist;
+      rec[4] = rt0; rec[5] = (long long)__builtin_amdgcn_s_memrealtime(); rec[6] = hw;
+      for (int i = 0; i < 6; ++i) rec[7 + i] = stamp[i];
+      rec[13] = SL;
+      rec[14] = n_app_tot;
+      rec[15] = ((long long)n_ins_tot << 32) | (unsigned)w_ins;
+    }
+  }
 #endif
 }
 
-template <bool PERSP, bool CLIP>
-void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, dim3 grid, int wv, size_t lds, hipStream_t st) {
-  if (wv == 4) rast_fwd_kernel<4, PERSP, CLIP><<<grid, 256, lds, st>>>(a, fr);
-  else if (wv == 2) rast_fwd_kernel<2, PERSP, CLIP><<<grid, 128, lds, st>>>(a, fr);
-  else rast_fwd_kernel<1, PERSP, CLIP><<<grid, 64, lds, st>>>(a, fr);
+template <int SL, bool PERSP, bool CLIP>
+void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const float4* fb, bool frag, size_t lds,
+                        hipStream_t st) {
+  constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW;
+  dim3 grid((a.W + TW - 1) / TW, (a.H + TH - 1) / TH, a.N);
+  if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb);
+  else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb);
 }
 
-void launch_rast_fwd(const PRRastArgs& a, const FaceRec* fr, dim3 grid, int wv, size_t lds, hipStream_t st) {
+template <bool PERSP, bool CLIP>
+void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, const float4* fb, int sl, bool frag, size_t lds,
+                        hipStream_t st) {
+  if (sl == 4) launch_rast_fwd_sl<4, PERSP, CLIP>(a, fr, fb, frag, lds, st);
+  else if (sl == 2) launch_rast_fwd_sl<2, PERSP, CLIP>(a, fr, fb, frag, lds, st);
+  else launch_rast_fwd_sl<1, PERSP, CLIP>(a, fr, fb, frag, lds, st);
+}
+
+void launch_rast_fwd(const PRRastArgs& a, const FaceRec* fr, const float4* fb, int sl, bool frag, size_t lds,
+                     hipStream_t st) {
   const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
-  if (persp && clip) launch_rast_fwd_pc<true, true>(a, fr, grid, wv, lds, st);
-  else if (persp) launch_rast_fwd_pc<true, false>(a, fr, grid, wv, lds, st);
-  else if (clip) launch_rast_fwd_pc<false, true>(a, fr, grid, wv, lds, st);
-  else launch_rast_fwd_pc<false, false>(a, fr, grid, wv, lds, st);
+  if (persp && clip) launch_rast_fwd_pc<true, true>(a, fr, fb, sl, frag, lds, st);
+  else if (persp) launch_rast_fwd_pc<true, false>(a, fr, fb, sl, frag, lds, st);
+  else if (clip) launch_rast_fwd_pc<false, true>(a, fr, fb, sl, frag, lds, st);
+  else launch_rast_fwd_pc<false, false>(a, fr, fb, sl, frag, lds, st);
 }
 
 // Forward, pass 2: barycentrics (perspective-corrected, clipped) and signed squared
@@ -780,15 +863,6 @@ constexpr int kBwdTile = 8;     // tile width; rows per tile (<= 8) chosen at la
 constexpr int kBwdThreads = 256;
 constexpr int kBwdEnt = 512;    // slots scanned (and at most valid) per round: 2 per thread
 constexpr int kBwdFaces = 128;  // faces per tile reduced by the transpose; later ones use global atomics
-
-// q = i / d, r = i - q d for 0 <= i < 2^20 and 0 < d < 2^20 (float reciprocal + one correction)
-PR_DEV int divmod_small(int i, int d, float inv_d, int& r) {
-  int q = (int)((float)i * inv_d);
-  r = i - q * d;
-  if (r < 0) { --q; r += d; }
-  else if (r >= d) { ++q; r -= d; }
-  return q;
-}
 
 // One 256-thread workgroup per 8 x tile_rows pixel tile (tile_rows <= 8), rounds of
 // kBwdEnt slots.  No per-slot atomics on the gradient values (LDS float atomics cost
@@ -1058,9 +1132,17 @@ int rast_check(const PRRastArgs& a) {
 
 using namespace pr;
 
+#ifdef PR_RAST_PROFILE
+// diagnostic build only: copy the per-tile profile records of the last launches to the host
+extern "C" int pr_rast_prof_dump(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rast_prof), bytes < sizeof(g_rast_prof) ? bytes : sizeof(g_rast_prof),
+                             0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" size_t pr_rast_fwd_workspace_size(const PRRastArgs* a) {
   if (!a) return 0;
-  return (size_t)(a->F > 0 ? a->F : 1) * sizeof(FaceRec);
+  return (size_t)(a->F > 0 ? a->F : 1) * (sizeof(FaceRec) + sizeof(float4));  // records + compact boxes
 }
 
 extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
@@ -1072,25 +1154,27 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
     return set_error(PR_ERR_WORKSPACE, "rast_fwd: workspace too small");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   FaceRec* fr = reinterpret_cast<FaceRec*>(a.workspace);
+  float4* fbox = reinterpret_cast<float4*>(fr + (a.F > 0 ? a.F : 1));
   if (a.F > 0) {
     const int nb = (int)std::min<int64_t>((a.F + kThreads - 1) / kThreads, 1024);
-    face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr);
+    face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr, fbox);
     if (int e = check_launch("rast_face_prep")) return e;
   }
-  dim3 grid((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, a.N);
-  // waves per tile: 1 measured fastest on the bench frame (256^2, 1024 tiles: the
-  // split's per-tile cull/sort/merge overhead outweighs the shorter traversal);
-  // PR_RAST_WAVES=2|4 selects the split variant (sweeps, few-tile heavy meshes)
-  int wv = 1;
-  if (const char* ew = getenv("PR_RAST_WAVES")) {
-    const int v = atoi(ew);
-    if (v == 1 || v == 2 || v == 4) wv = v;
+  // face slices per pixel (tile 8x8 / 8x4 / 4x4): 2 measured fastest on the bench frame
+  // (113 us vs 117 at 4 and 157 at 1); PR_RAST_SLICES=1|2|4 overrides (sweeps).  FRAG: barycentrics / distances written by the rasterizer itself
+  // (no second pass over pix_to_face); PR_RAST_FRAG=0 selects the separate pass.
+  int sl = 2;
+  if (const char* e = getenv("PR_RAST_SLICES")) {
+    const int v = atoi(e);
+    if (v == 1 || v == 2 || v == 4) sl = v;
   }
-  while (wv > 1 && rast_fwd_lds(a.K, wv) > 160 * 1024) wv >>= 1;
-  const size_t lds = rast_fwd_lds(a.K, wv);
+  bool frag = true;
+  if (const char* e = getenv("PR_RAST_FRAG")) frag = atoi(e) != 0;
+  const size_t lds = rast_fwd_lds(a.K, sl);
   if (lds > 160 * 1024) return set_error(PR_ERR_ARG, "rast_fwd: faces_per_pixel too large for the LDS queue (max 300)");
-  launch_rast_fwd(a, fr, grid, wv, lds, st);
+  launch_rast_fwd(a, fr, fbox, sl, frag, lds, st);
   if (int e = check_launch("rast_fwd")) return e;
+  if (frag) return PR_OK;
   const int64_t total = (int64_t)a.N * a.H * a.W * a.K;
   const int nb = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 1 << 20);
   if (total * 3 < (int64_t(1) << 32)) rast_frag_kernel<false><<<nb, kThreads, 0, st>>>(a, total);
