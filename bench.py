@@ -5,7 +5,8 @@ the mesh (so3 exp map), MeshRasterizer (native K-nearest rasterizer, 256x256,
 faces_per_pixel=50, blur = ln(1/1e-4 - 1)*sigma), RandomSimpleShader with
 GaussianRast(nb_samples=8) + GaussianAgg(nb_samples=8) (fused native blend with
 TexturesVertex sampling), L2 loss to a fixed synthetic target, backward through
-blend -> rasterizer -> vertices -> pose.  With N ranks the Monte-Carlo sample
+blend -> rasterizer -> vertices -> pose, Adam step on the pose (lr 5e-2, eval.py:337).
+With N ranks the Monte-Carlo sample
 dimension is sharded (BASELINE north star): every rank renders the SAME frame and
 pose with its own disjoint range of global sample indices (Philox offset rank*S),
 and one RCCL all-reduce averages the gradient estimates, i.e. each step is one
@@ -198,14 +199,19 @@ class WorkloadCPU:
 
 
 def build_step(wl, world, mode, device):
-    """Returns step(timed) for eager or HIP-graph mode.  In graph mode the whole
-    forward+backward (incl. the Philox key advance) is one captured graph; sigma/gamma/
-    alpha live on the device so no host synchronisation remains inside the step."""
+    """Returns step() for eager or HIP-graph mode.  A step is one full pose-optimisation
+    iteration of eval.py:343-376: forward, loss, backward, (N>1: the gradient all-reduce),
+    Adam step on the pose (lr 5e-2, eval.py:320,337).  In graph mode forward+backward
+    (incl. the Philox key advance) and the Adam step are captured HIP graphs (one graph at
+    N=1); sigma/gamma/alpha live on the device so no host synchronisation remains."""
     if mode == "eager":
+        wl.opt = torch.optim.Adam([wl.log_rot], lr=5e-2)
+
         def step():
             wl.forward().backward()
             if world > 1:
                 allreduce_grads(wl.params(), world)
+            wl.opt.step()
             wl.zero_grad()
         return step
 
@@ -213,12 +219,14 @@ def build_step(wl, world, mode, device):
     pa.noise.use_device_seed(ds)
     wl.device_scalars()
     wl.seed = ds
+    wl.opt = torch.optim.Adam([wl.log_rot], lr=5e-2, capturable=True, fused=True)
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
         for _ in range(3):
             ds.advance()
             wl.forward().backward()
+            wl.opt.step()
             wl.zero_grad()
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
@@ -226,12 +234,20 @@ def build_step(wl, world, mode, device):
     with torch.cuda.graph(graph):
         ds.advance()
         wl.forward().backward()
+        if world == 1:
+            wl.opt.step()
     wl.graph = graph
+    if world == 1:
+        return graph.replay
+    opt_graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(opt_graph):
+        wl.opt.step()
+    wl.opt_graph = opt_graph
 
     def step():
         graph.replay()
-        if world > 1:
-            allreduce_grads(wl.params(), world)
+        allreduce_grads(wl.params(), world)
+        opt_graph.replay()
     return step
 
 
@@ -343,7 +359,8 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (sphere_642 mesh from the reference data, random vertex colours, random target)",
         "config": {"workload": "pose-opt step: sphere_642 (1280 faces) 256x256, faces_per_pixel=50, "
-                               "Sr=Sa=8 Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, fwd+bwd",
+                               "Sr=Sa=8 Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, "
+                               "fwd + L2 loss + bwd + Adam step on the pose (lr 5e-2)",
                    "image_size": args.image_size, "faces_per_pixel": args.faces_per_pixel,
                    "nb_samples": args.samples, "frames_per_rank_per_step": 1, "execution": mode,
                    "parallelism": f"sample-parallel x{world} (same frame, Philox sample shard per rank, "

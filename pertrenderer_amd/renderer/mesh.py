@@ -173,7 +173,11 @@ class Meshes:
         return Meshes(verts, None, self.textures, _topo=self._topo)
 
     def update_padded(self, new_verts_padded):
-        return self._new([new_verts_padded[i, : n] for i, n in enumerate(self._topo.nverts)])
+        nv = self._topo.nverts
+        if len(nv) == 1 and new_verts_padded.shape[1] == nv[0]:
+            # a reshape, not a slice: its backward is a view (a slice's is a zero-fill + copy)
+            return self._new([new_verts_padded.reshape(nv[0], new_verts_padded.shape[-1])])
+        return self._new([new_verts_padded[i, : n] for i, n in enumerate(nv)])
 
     def offset_verts(self, vert_offsets_packed):
         off = vert_offsets_packed
