@@ -47,21 +47,41 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def load_sphere(device):
-    verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
+def load_mesh(device, name="sphere_642.obj"):
+    """A reference data mesh (data/objs, copied to tests/golden), centred, max |coord| = 1."""
+    verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", name))
     center = verts.mean(0)
     verts = verts - center
     verts = verts / verts.abs().max()
     return verts.to(device), faces.verts_idx.to(device)
 
 
+def load_sphere(device):
+    return load_mesh(device, "sphere_642.obj")
+
+
+# BASELINE.json configs: cfg2 is the headline (metric's) workload; cfg3/cfg4 are the batch
+# configurations (16 meshes alternating sphere_642 / cube2, each with its own pose)
+CONFIGS = {
+    "cfg2": dict(batch=1, image_size=256, K=50, samples=8),
+    "cfg3": dict(batch=16, image_size=256, K=100, samples=16),
+    "cfg4": dict(batch=16, image_size=512, K=150, samples=64),
+}
+
+
 class Workload:
-    def __init__(self, device, image_size=256, K=50, samples=8, sigma=1e-3, gamma=1e-2, dist_cam=2.7, seed=0):
+    def __init__(self, device, image_size=256, K=50, samples=8, sigma=1e-3, gamma=1e-2, dist_cam=2.7, seed=0,
+                 batch=1):
         self.device = device
         g = torch.Generator().manual_seed(seed)
-        verts, faces = load_sphere(device)
-        colors = torch.rand((1, verts.shape[0], 3), generator=g).to(device)
-        self.base = Meshes([verts], [faces], TexturesVertex(colors))
+        vl, fl, cl = [], [], []
+        for i in range(batch):
+            verts, faces = load_mesh(device, "sphere_642.obj" if i % 2 == 0 else "cube2.obj")
+            vl.append(verts)
+            fl.append(faces)
+            cl.append(torch.rand((verts.shape[0], 3), generator=g).to(device))
+        self.base = Meshes(vl, fl, TexturesVertex(cl))
+        faces = torch.cat(fl)
         R, T = look_at_view_transform(dist_cam, 30.0, 120.0, device=device)
         self.cameras = FoVPerspectiveCameras(R=R, T=T, device=device, fov=60.0)
         self.settings = RasterizationSettings(image_size=image_size,
@@ -75,9 +95,9 @@ class Workload:
             shader=pa.RandomSimpleShader(device=device, cameras=self.cameras, smoothrast=self.rast,
                                          smoothagg=self.agg,
                                          blend_params=pa.random_rasterizer.BlendParams(sigma, gamma, (0.0, 0.0, 0.0))))
-        self.log_rot = (0.3 * torch.randn((1, 3), generator=g)).to(device).requires_grad_(True)
-        self.target = torch.rand((1, image_size, image_size, 3), generator=g).to(device)
-        self.K, self.S, self.H = K, samples, image_size
+        self.log_rot = (0.3 * torch.randn((batch, 3), generator=g)).to(device).requires_grad_(True)
+        self.target = torch.rand((batch, image_size, image_size, 3), generator=g).to(device)
+        self.K, self.S, self.H, self.batch = K, samples, image_size, batch
         self.F = faces.shape[0]
 
     def params(self):
@@ -284,13 +304,22 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
-    ap.add_argument("--image-size", type=int, default=256)
-    ap.add_argument("--faces-per-pixel", type=int, default=50)
-    ap.add_argument("--samples", type=int, default=8)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
+                    help="BASELINE.json configuration (cfg2 = the metric's headline workload)")
+    ap.add_argument("--image-size", type=int, default=None)
+    ap.add_argument("--faces-per-pixel", type=int, default=None)
+    ap.add_argument("--samples", type=int, default=None, help="Monte-Carlo samples per rank")
+    ap.add_argument("--batch", type=int, default=None, help="meshes per rank")
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
     args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    for key, val in (("image_size", args.image_size), ("K", args.faces_per_pixel), ("samples", args.samples),
+                     ("batch", args.batch)):
+        if val is not None:
+            cfg[key] = val
+    headline = cfg == CONFIGS["cfg2"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -304,15 +333,17 @@ def main():
     pa.noise.set_sample_shard(rank)  # ... disjoint global sample ranges
     pa.native_library()
 
-    wl = Workload(device, args.image_size, args.faces_per_pixel, args.samples, seed=0)  # same frame on all ranks
-    P = args.image_size * args.image_size
+    mk_wl = lambda: Workload(device, cfg["image_size"], cfg["K"], cfg["samples"], seed=0,  # same frame on all ranks
+                             batch=cfg["batch"])
+    wl = mk_wl()
+    P = cfg["batch"] * cfg["image_size"] * cfg["image_size"]
     mode, note = args.mode, None
     try:
         step = build_step(wl, world, mode, device)
     except Exception as e:  # graph capture unavailable: measure eagerly and say so
         note = f"graph capture failed ({type(e).__name__}: {e}); eager fallback"
         pa.noise.use_device_seed(None)
-        wl = Workload(device, args.image_size, args.faces_per_pixel, args.samples, seed=0)
+        wl = mk_wl()
         mode = "eager"
         step = build_step(wl, world, mode, device)
 
@@ -346,34 +377,37 @@ def main():
             "timing": "mean of HIP events around each launch on its stream, eager replica of the "
                       "timed step right after the timed region (same kernels and arguments)"}
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if headline and os.path.exists(pmc):  # PMC passes are taken on the headline workload
         tr = json.load(open(pmc)).get(dom)
         if tr:
             roof["traffic"] = tr.get("bytes_per_launch")
 
-    frames = args.steps * world
+    B, Hs, K, S = cfg["batch"], cfg["image_size"], cfg["K"], cfg["samples"]
+    frames = args.steps * world * B
     value = frames / elapsed
+    meshes = ("sphere_642 (1280 faces)" if B == 1 else
+              f"{B} meshes alternating sphere_642 / cube2 ({wl.F} faces), one pose each")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s (fwd+bwd)", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (sphere_642 mesh from the reference data, random vertex colours, random target)",
-        "config": {"workload": "pose-opt step: sphere_642 (1280 faces) 256x256, faces_per_pixel=50, "
-                               "Sr=Sa=8 Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, "
+        "data": "synthetic (meshes from the reference data, random vertex colours, random target)",
+        "config": {"workload": f"{args.config} pose-opt step: {meshes}, {Hs}x{Hs}, faces_per_pixel={K}, "
+                               f"Sr=Sa={S} Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, "
                                "fwd + L2 loss + bwd + Adam step on the pose (lr 5e-2)",
-                   "image_size": args.image_size, "faces_per_pixel": args.faces_per_pixel,
-                   "nb_samples": args.samples, "frames_per_rank_per_step": 1, "execution": mode,
-                   "parallelism": f"sample-parallel x{world} (same frame, Philox sample shard per rank, "
+                   "image_size": Hs, "faces_per_pixel": K, "nb_samples": S, "batch": B,
+                   "frames_per_rank_per_step": B, "execution": mode,
+                   "parallelism": f"sample-parallel x{world} (same frames, Philox sample shard per rank, "
                                   f"one RCCL gradient all-reduce per step)"},
         "ms_forward": round(ms_fwd, 4), "ms_backward": round(ms_bwd, 4),
         "fwd_bwd_split_from": "eager instrumented replica (HIP events around forward / loss.backward())",
-        "fwd_frames_per_s": round(world * 1e3 / ms_fwd, 2), "kernels": kern, "roofline": roof,
+        "fwd_frames_per_s": round(world * B * 1e3 / ms_fwd, 2), "kernels": kern, "roofline": roof,
     }
     if note:
         out["note"] = note
-    if rank == 0 and not args.no_dense:
+    if rank == 0 and not args.no_dense and headline:
         out["roofline_dense"] = dense_roofline(device)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
         threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
         os.environ.setdefault("OMP_NUM_THREADS", str(threads))
         v, dt = cpu_baseline(args.cpu_frames, threads)

@@ -13,6 +13,15 @@ from .. import _native as nat
 F32 = torch.float32
 
 
+def _per_mesh(m, N, name):
+    """(N,4,4) float32 contiguous matrices, one per mesh (the kernels index mesh n's matrix at
+    n*16): one camera broadcast over a batch of meshes, as PyTorch3D does."""
+    m = m.detach().to(F32)
+    if m.dim() != 3 or m.shape[1:] != (4, 4) or m.shape[0] not in (1, N):
+        raise ValueError(f"{name} matrices must be (1,4,4) or (N={N},4,4), got {tuple(m.shape)}")
+    return (m.expand(N, 4, 4) if m.shape[0] != N else m).contiguous()
+
+
 class _ProjectFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, verts, faces, first, nfaces, w2v, proj):
@@ -22,9 +31,10 @@ class _ProjectFn(torch.autograd.Function):
         f = faces.detach().to(torch.int64).contiguous()
         a = nat.PRProjectArgs()
         a.verts, a.faces, a.mesh_first_face, a.mesh_num_faces = nat.ptr(v), nat.ptr(f), nat.ptr(first), nat.ptr(nfaces)
-        m1, m2 = w2v.detach().to(F32).contiguous(), proj.detach().to(F32).contiguous()
+        N = first.shape[0]
+        m1, m2 = _per_mesh(w2v, N, "world_to_view"), _per_mesh(proj, N, "projection")
         a.world_to_view, a.proj = nat.ptr(m1), nat.ptr(m2)
-        a.V, a.F, a.N = v.shape[0], f.shape[0], first.shape[0]
+        a.V, a.F, a.N = v.shape[0], f.shape[0], N
         fv = torch.empty((f.shape[0], 3, 3), dtype=F32, device=v.device)
         a.face_verts = nat.ptr(fv)
         nat.check(lib.pr_project_fwd(a, nat.stream_of(fv)), "pr_project_fwd")
