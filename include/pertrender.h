@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 6
+#define PR_ABI_VERSION 7
 
 /* error codes */
 #define PR_OK 0
@@ -104,6 +104,9 @@ typedef struct PRBlendFwdArgs {
   const float* bary;          /* (N,H,W,K,3) */
   const int64_t* faces;       /* (F,3) packed vertex indices */
   const float* vert_colors;   /* (V,3) packed per-vertex colours */
+  /* nullable (N,H,W) valid-prefix counts of pix_to_face (pr_rast_fwd's pix_count): mask = k < */
+  /* count, and no fragment tensor is read at masked slots                                   */
+  const int32_t* pix_count;
 } PRBlendFwdArgs;
 
 typedef struct PRBlendBwdArgs {
@@ -130,6 +133,7 @@ typedef struct PRBlendBwdArgs {
   const float* vert_colors;
   float* grad_bary;           /* VERTEX out (N,H,W,K,3) (replaces grad_colors) */
   float* grad_vert_colors;    /* VERTEX out (V,3), nullable, accumulated (caller zeroes) */
+  const int32_t* pix_count;   /* nullable: as in PRBlendFwdArgs (the same tensor as the forward's) */
 } PRBlendBwdArgs;
 
 typedef struct PRHeavisideArgs {
@@ -164,6 +168,9 @@ typedef struct PRRastArgs {
   float* grad_face_verts;           /* (F,3,3), overwritten */
   void* workspace;
   size_t workspace_bytes;
+  /* nullable (N,H,W) valid-prefix counts: slots 0..count-1 of a pixel hold faces, the rest -1.  */
+  /* Forward: written.  Backward: if set (the forward's), pix_to_face is read only below it.    */
+  int32_t* pix_count;
 } PRRastArgs;
 
 typedef struct PRInterpArgs {

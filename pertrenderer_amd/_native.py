@@ -40,7 +40,8 @@ class PRBlendParams(C.Structure):
 class PRBlendFwdArgs(C.Structure):
     _fields_ = [("p", PRBlendParams), ("pix_to_face", _vp), ("mask", _vp), ("dists", _vp),
                 ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("image", _vp), ("weights", _vp),
-                ("winners", _vp), ("rast_cache", _vp), ("bary", _vp), ("faces", _vp), ("vert_colors", _vp)]
+                ("winners", _vp), ("rast_cache", _vp), ("bary", _vp), ("faces", _vp), ("vert_colors", _vp),
+                ("pix_count", _vp)]
 
 
 class PRBlendBwdArgs(C.Structure):
@@ -49,7 +50,8 @@ class PRBlendBwdArgs(C.Structure):
                 ("grad_image", _vp), ("grad_weights", _vp), ("grad_dists", _vp), ("grad_prob", _vp),
                 ("grad_zbuf", _vp), ("grad_colors", _vp), ("grad_scalars", _vp),
                 ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("rast_cache", _vp), ("bary", _vp),
-                ("faces", _vp), ("vert_colors", _vp), ("grad_bary", _vp), ("grad_vert_colors", _vp)]
+                ("faces", _vp), ("vert_colors", _vp), ("grad_bary", _vp), ("grad_vert_colors", _vp),
+                ("pix_count", _vp)]
 
 
 class PRHeavisideArgs(C.Structure):
@@ -68,7 +70,8 @@ class PRRastArgs(C.Structure):
                 ("clip_barycentric_coords", C.c_int32), ("cull_backfaces", C.c_int32),
                 ("pix_to_face", _vp), ("zbuf", _vp), ("bary", _vp), ("dists", _vp),
                 ("grad_zbuf", _vp), ("grad_bary", _vp), ("grad_dists", _vp),
-                ("grad_face_verts", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t)]
+                ("grad_face_verts", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
+                ("pix_count", _vp)]
 
 
 class PRInterpArgs(C.Structure):
@@ -117,7 +120,7 @@ EXPORTS = {
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
 }
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib = None
 

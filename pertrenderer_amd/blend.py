@@ -124,6 +124,16 @@ def _scalar_grads(gs, needs, refs):
             for i, (need, ref) in enumerate(zip(needs, refs))]
 
 
+def _counts_for(pix_to_face):
+    """The native rasterizer's valid-prefix counts of these fragments (int32 (N,H,W) on the same
+    device), or None: the kernels then read pix_to_face at every slot."""
+    from .renderer.rasterizer import valid_counts
+    c = valid_counts(pix_to_face)
+    if c is None or c.device != pix_to_face.device or tuple(c.shape) != tuple(pix_to_face.shape[:3]):
+        return None
+    return c.contiguous()
+
+
 def _timed(name, fn):
     hook = _timing.active()
     if hook is not None:
@@ -162,6 +172,7 @@ class _FusedBlendFn(torch.autograd.Function):
         a.p = p
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
+        a.pix_count = nat.ptr(cfg["counts"])
         _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
         ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, cache)
         ctx.sc_dev = sc_dev
@@ -187,6 +198,7 @@ class _FusedBlendFn(torch.autograd.Function):
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
         a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
         a.grad_dists, a.grad_zbuf, a.grad_colors, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gc), nat.ptr(gsc)
+        a.pix_count = nat.ptr(cfg["counts"])
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         _timed("blend_bwd", lambda: nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd"))
@@ -224,6 +236,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         a.pix_to_face, a.dists, a.zbuf = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c)
         a.bary, a.faces, a.vert_colors = nat.ptr(b_c), nat.ptr(f_c), nat.ptr(v_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
+        a.pix_count = nat.ptr(cfg["counts"])
         _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
         ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache)
         ctx.sc_dev = sc_dev
@@ -252,6 +265,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
         a.grad_dists, a.grad_zbuf, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gsc)
         a.grad_bary, a.grad_vert_colors = nat.ptr(gb), nat.ptr(gv)
+        a.pix_count = nat.ptr(cfg["counts"])
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         _timed("blend_bwd", lambda: nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd"))
@@ -281,7 +295,7 @@ def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, s
         noise = _merge(nr, na)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
-               bg=_background(background), noise=noise, vflags=vflags)
+               bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
     return _FusedVertexBlendFn.apply(dists, zbuf, bary, vert_colors, sigma, gamma, alpha, pix_to_face, faces,
                                      znear, zfar, cfg)
 
@@ -308,7 +322,7 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
         noise = _merge(nr, na)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
-               bg=_background(background), noise=noise, vflags=vflags)
+               bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
     return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, pix_to_face, znear, zfar, cfg)
 
 

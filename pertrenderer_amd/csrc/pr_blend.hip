@@ -266,7 +266,8 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
   float* A = smem;                 // [PB][KP1] prob, then int win counts
   float* B = A + PB * KP1;         // [PB][KP1] z_inv, then logits z
   float* PX = B + PB * KP1;        // [PB][4] z_max, alpha, max logit, candidate count
-  int* QN = reinterpret_cast<int*>(PX + PB * 4);            // rast queue length
+  int* CP = reinterpret_cast<int*>(PX + PB * 4);            // [PB] valid-prefix count (K without pix_count)
+  int* QN = CP + PB;                                        // rast queue length
   uint16_t* Q = reinterpret_cast<uint16_t*>(QN + 4);        // [PB*K] rast queue (pl << 8 | k)
   uint8_t* LC = reinterpret_cast<uint8_t*>(Q);              // [PB][KP1] argmax candidates (after 1b)
   int* CNT = reinterpret_cast<int*>(A);
@@ -277,6 +278,8 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
   const int npix = (int)min((int64_t)PB, g.P - pix0);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   if (tid == 0) *QN = 0;
+  const int32_t* pcnt = a.pix_count;
+  if (tid < npix) CP[tid] = pcnt ? pcnt[pix0 + tid] : K;
   __syncthreads();
 
   // ---- 1a: slots, kU per thread in flight: mask, z_inv, and the probability wherever
@@ -298,9 +301,12 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
         dd[u] = zb[u] = 0.f;
         if (bt.ok[u]) {
           const int64_t gs = (pix0 + bt.pl[u]) * K + bt.k[u];
-          mk[u] = slot_mask(a.pix_to_face, a.mask, gs);
-          dd[u] = RAST ? a.dists[gs] : a.prob[gs];
-          zb[u] = a.zbuf[gs];
+          // with valid-prefix counts nothing is read at a masked slot
+          mk[u] = pcnt ? bt.k[u] < CP[bt.pl[u]] : slot_mask(a.pix_to_face, a.mask, gs);
+          if (mk[u] || !pcnt) {
+            dd[u] = RAST ? a.dists[gs] : a.prob[gs];
+            zb[u] = a.zbuf[gs];
+          }
         }
       }
 #pragma unroll
@@ -321,7 +327,8 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
             } else {          // count Sr (saturated inside) or 0: prob Sr/Sr * 1 = 1, or 0
               const float prob = sat < 0 ? 1.f : 0.f;
               A[li] = prob;
-              if (a.rast_cache) reinterpret_cast<float2*>(a.rast_cache)[gs] = make_float2(prob, 0.f);
+              // (with pix_count the cache is defined at valid slots only: the backward reads no more)
+              if (a.rast_cache && (m || !pcnt)) reinterpret_cast<float2*>(a.rast_cache)[gs] = make_float2(prob, 0.f);
             }
           } else {
             A[li] = dd[u];
@@ -536,10 +543,14 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
   int* CN = reinterpret_cast<int*>(DW + PB * KP1);      // [PB][KP1] win counts
   float* AS = reinterpret_cast<float*>(CN + PB * KP1);  // [PB][Sa] a_s
   float* PX = AS + PB * Sa;            // [PB][8] per-pixel scalars
+  int* CP = reinterpret_cast<int*>(PX + PB * 8);        // [PB] valid-prefix count (K without pix_count)
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
   const int64_t pix0 = (int64_t)blockIdx.x * PB;
   const int npix = (int)min((int64_t)PB, g.P - pix0);
+  const int32_t* pcnt = a.pix_count;
+  if (tid < npix) CP[tid] = pcnt ? pcnt[pix0 + tid] : K;
+  __syncthreads();
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   const float gal = sc.gamma / sc.alpha;
   float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
@@ -564,7 +575,9 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
         const int64_t gp = pix0 + pl;
         if (k < K) {
           const int64_t gs = gp * K + k;
-          mk[u] = slot_mask(a.pix_to_face, a.mask, gs);
+          // with valid-prefix counts nothing is read at a masked slot (prob, score, z_inv are 0)
+          mk[u] = pcnt ? k < CP[pl] : slot_mask(a.pix_to_face, a.mask, gs);
+          if (!mk[u] && pcnt) continue;
           if constexpr (RAST) {
             if (a.rast_cache) pg[u] = reinterpret_cast<const float2*>(a.rast_cache)[gs];
             else pg[u].x = a.dists[gs];
@@ -795,7 +808,9 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
       gik[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (!bt.ok[u]) continue;
       const int64_t gp = pix0 + bt.pl[u], gs = gp * K + bt.k[u];
-      if (a.pix_to_face) {
+      if (pcnt) {  // the face id is read below, for the (few) slots that won a sample
+        mk[u] = bt.k[u] < CP[bt.pl[u]];
+      } else if (a.pix_to_face) {
         fk[u] = a.pix_to_face[gs];
         mk[u] = fk[u] >= 0;
       } else {
@@ -842,8 +857,8 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
       // d colour = w * g_rgb, pushed through the interpolation (interp_bwd_kernel's order)
       const int cnt = CN[pl * KP1 + k];
       float gb[3] = {0.f, 0.f, 0.f};
-      const int64_t f = m ? fk[u] : -1;
-      if (cnt != 0 && f >= 0) {
+      const int64_t f = (cnt != 0 && m) ? (pcnt ? a.pix_to_face[gs] : fk[u]) : -1;
+      if (f >= 0) {
         const float w = (float)cnt / (float)Sa;
         const float dc[3] = {w * gi.x, w * gi.y, w * gi.z};
         const int64_t v[3] = {a.faces[f * 3], a.faces[f * 3 + 1], a.faces[f * 3 + 2]};
@@ -994,13 +1009,13 @@ __global__ void seed_advance_kernel(uint64_t* seeds, int n) {
 }
 
 // ================================================================== host side
-// A, B, PX, queue length (+pad), then the uint16 rast queue [PB*K] (which also holds the
+// A, B, PX, CP, queue length (+pad), then the uint16 rast queue [PB*K] (which also holds the
 // uint8 candidate lists [PB][KP1]: 2K >= K+1)
 size_t fwd_lds(int PB, int KP1) {
-  return (size_t)(2 * PB * KP1 + 4 * PB + 4) * sizeof(float) + (size_t)PB * (KP1 - 1) * sizeof(uint16_t);
+  return (size_t)(2 * PB * KP1 + 5 * PB + 4) * sizeof(float) + (size_t)PB * (KP1 - 1) * sizeof(uint16_t);
 }
 size_t bwd_lds(int PB, int KP1, int Sa) {
-  const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + 8 * PB) * sizeof(float);
+  const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + 9 * PB) * sizeof(float);
   return b < 16 * sizeof(float) ? 16 * sizeof(float) : b;
 }
 constexpr size_t kLdsBudget = 48 * 1024;  // forward: >= 3 workgroups (12 waves) per CU

@@ -610,7 +610,10 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
     __syncthreads();
     PR_STAMP(4);
   }
-  if (slice == 0) qsz[pix] = inimg ? qs : 0;
+  if (slice == 0) {
+    qsz[pix] = inimg ? qs : 0;
+    if (inimg && a.pix_count) a.pix_count[((int64_t)n * H + row) * W + col] = qs;
+  }
   __syncthreads();
   // ---- coalesced output: each tile row's pixels own a contiguous ncols*K slot range;
   //      the wave walks the tile's rows as one flat index (4 slots per lane in flight)
@@ -893,6 +896,7 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a) {
   __shared__ int2 clist[kBwdEnt];                 // (pixel << 16 | k, face id)
   __shared__ int ccount, nface;
   __shared__ float pxs[kBwdTile], pys[ROWS];
+  __shared__ int pcnt[kBwdTile * ROWS];           // valid-prefix counts of the tile's pixels (or K)
   const int tid = threadIdx.x, lane = tid & 63;
   const int K = a.K, H = a.H, W = a.W;
   const int n = blockIdx.z, row0 = blockIdx.y * tile_rows, col0 = blockIdx.x * kBwdTile;
@@ -907,20 +911,28 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a) {
   if (tid < kBwdTile) pxs[tid] = ndc(W - 1 - min(col0 + tid, W - 1), W, H);
   if (tid >= 64 && tid < 64 + ROWS) pys[tid - 64] = ndc(H - 1 - min(row0 + tid - 64, H - 1), H, W);
   if (tid == 0) nface = 0;
+  if (tid < TP) {
+    const int r = tid / kBwdTile, c = tid - r * kBwdTile;
+    pcnt[tid] = (r < nrows && c < ncols) ? (a.pix_count ? a.pix_count[((int64_t)n * H + row0 + r) * W + col0 + c] : K) : 0;
+  }
   float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // owner lane tid < kBwdFaces
   for (int c0 = 0; c0 < total; c0 += kBwdEnt) {
     if (tid == 0) ccount = 0;
     __syncthreads();  // also: the previous round's transpose is done (M reset, gbuf free)
     // ---- 1. scan + compaction + face registration
     int64_t f[kBwdEnt / kBwdThreads];
+    int pk[kBwdEnt / kBwdThreads];  // (pixel << 16) | k
 #pragma unroll
     for (int u = 0; u < kBwdEnt / kBwdThreads; ++u) {
       const int i = c0 + u * kBwdThreads + tid;
       f[u] = -1;
+      pk[u] = 0;
       if (i < total) {
-        int rem;
+        int rem, k;
         const int r = divmod_small(i, per_row, inv_row, rem);
-        f[u] = a.pix_to_face[tile_o + r * row_stride + rem];
+        const int c = divmod_small(rem, K, inv_k, k);
+        pk[u] = ((r * kBwdTile + c) << 16) | k;
+        if (k < pcnt[r * kBwdTile + c]) f[u] = a.pix_to_face[tile_o + r * row_stride + rem];
       }
     }
 #pragma unroll
@@ -932,12 +944,8 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a) {
       if (lane == 0) off = atomicAdd(&ccount, __popcll(bal));
       off = __shfl(off, 0);
       if (!keep) continue;
-      const int i = c0 + u * kBwdThreads + tid;
-      int rem, k;
-      const int r = divmod_small(i, per_row, inv_row, rem);
-      const int c = divmod_small(rem, K, inv_k, k);
       const int fi = (int)f[u];
-      clist[off + __popcll(bal & ((1ull << lane) - 1ull))] = make_int2(((r * kBwdTile + c) << 16) | k, fi);
+      clist[off + __popcll(bal & ((1ull << lane) - 1ull))] = make_int2(pk[u], fi);
       uint32_t h = ((uint32_t)fi * 2654435761u) & (kHash - 1);
       for (int probe = 0; probe < 32; ++probe) {
         const int cur = atomicCAS(&hkey[h], -1, fi);

@@ -49,6 +49,21 @@ def _hw(image_size):
     return int(image_size), int(image_size)
 
 
+def attach_valid_counts(pix_to_face, counts):
+    """Remember the rasterizer's per-pixel valid-prefix counts on its pix_to_face tensor (the
+    valid slots of a pixel are 0..count-1, PyTorch3D's -1 padding after them).  Native ops on
+    these fragments then read no fragment data at padded slots.  Tied to the tensor's version:
+    an in-place change of pix_to_face drops them."""
+    pix_to_face._pr_valid_counts = (pix_to_face._version, counts)
+    return pix_to_face
+
+
+def valid_counts(pix_to_face):
+    """The (N,H,W) int32 counts attached by the native rasterizer, or None."""
+    e = getattr(pix_to_face, "_pr_valid_counts", None)
+    return e[1] if e is not None and e[0] == pix_to_face._version else None
+
+
 class _RasterizeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, face_verts, first, nfaces, H, W, K, blur, persp, clip, cull):
@@ -66,7 +81,9 @@ class _RasterizeFn(torch.autograd.Function):
         zbuf = torch.empty((N, H, W, K), dtype=F32, device=dev)
         bary = torch.empty((N, H, W, K, 3), dtype=F32, device=dev)
         dists = torch.empty((N, H, W, K), dtype=F32, device=dev)
+        counts = torch.empty((N, H, W), dtype=torch.int32, device=dev)
         a.pix_to_face, a.zbuf, a.bary, a.dists = nat.ptr(p2f), nat.ptr(zbuf), nat.ptr(bary), nat.ptr(dists)
+        a.pix_count = nat.ptr(counts)
         ws = torch.empty(max(1, lib.pr_rast_fwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         timing = _timing.active()
@@ -75,22 +92,22 @@ class _RasterizeFn(torch.autograd.Function):
         nat.check(lib.pr_rast_fwd(a, nat.stream_of(fv)), "pr_rast_fwd")
         if timing is not None:
             timing.stop("rast_fwd")
-        ctx.save_for_backward(fv, first, nfaces, p2f)
+        ctx.save_for_backward(fv, first, nfaces, p2f, counts)
         ctx.cfg = (H, W, K, float(blur), int(persp), int(clip), int(cull))
-        ctx.mark_non_differentiable(p2f)
+        ctx.mark_non_differentiable(p2f, counts)
         ctx.set_materialize_grads(False)  # no zero-filled int64 grad for pix_to_face
-        return p2f, zbuf, bary, dists
+        return p2f, zbuf, bary, dists, counts
 
     @staticmethod
-    def backward(ctx, gp2f, gzbuf, gbary, gdists):
-        fv, first, nfaces, p2f = ctx.saved_tensors
+    def backward(ctx, gp2f, gzbuf, gbary, gdists, gcounts):
+        fv, first, nfaces, p2f, counts = ctx.saved_tensors
         H, W, K, blur, persp, clip, cull = ctx.cfg
         lib = nat.load()
         a = nat.PRRastArgs()
         a.face_verts, a.mesh_first_face, a.mesh_num_faces = nat.ptr(fv), nat.ptr(first), nat.ptr(nfaces)
         a.F, a.N, a.H, a.W, a.K = fv.shape[0], first.shape[0], H, W, K
         a.blur_radius, a.perspective_correct, a.clip_barycentric_coords, a.cull_backfaces = blur, persp, clip, cull
-        a.pix_to_face = nat.ptr(p2f)
+        a.pix_to_face, a.pix_count = nat.ptr(p2f), nat.ptr(counts)
         keep = []
         for name, g in (("grad_zbuf", gzbuf), ("grad_bary", gbary), ("grad_dists", gdists)):
             if g is not None:
@@ -117,8 +134,13 @@ def rasterize_meshes(meshes, image_size=256, blur_radius=0.0, faces_per_pixel=8,
     first = meshes.mesh_to_faces_packed_first_idx().to(verts.device)
     nfaces = meshes.num_faces_per_mesh().to(verts.device)
     H, W = _hw(image_size)
-    return _RasterizeFn.apply(face_verts, first, nfaces, H, W, int(faces_per_pixel), float(blur_radius),
-                              bool(perspective_correct), bool(clip_barycentric_coords), bool(cull_backfaces))
+    return _rasterize(face_verts, first, nfaces, H, W, int(faces_per_pixel), float(blur_radius),
+                      bool(perspective_correct), bool(clip_barycentric_coords), bool(cull_backfaces))
+
+
+def _rasterize(face_verts, first, nfaces, H, W, K, blur, persp, clip, cull):
+    p2f, zbuf, bary, dists, counts = _RasterizeFn.apply(face_verts, first, nfaces, H, W, K, blur, persp, clip, cull)
+    return attach_valid_counts(p2f, counts), zbuf, bary, dists
 
 
 class MeshRasterizer(torch.nn.Module):
@@ -158,9 +180,9 @@ class MeshRasterizer(torch.nn.Module):
             fv = project_faces(meshes_world.verts_packed(), meshes_world.faces_packed(), first, nfaces,
                                cameras.world_to_view_matrix(), cameras.projection_matrix())
             H, W = _hw(rs.image_size)
-            p2f, zbuf, bary, dists = _RasterizeFn.apply(fv, first, nfaces, H, W, int(rs.faces_per_pixel),
-                                                        float(rs.blur_radius), bool(rs.perspective_correct),
-                                                        bool(clip), bool(rs.cull_backfaces))
+            p2f, zbuf, bary, dists = _rasterize(fv, first, nfaces, H, W, int(rs.faces_per_pixel),
+                                                float(rs.blur_radius), bool(rs.perspective_correct),
+                                                bool(clip), bool(rs.cull_backfaces))
             return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)
         meshes_screen = self.transform(meshes_world, **kwargs)
         p2f, zbuf, bary, dists = rasterize_meshes(

@@ -66,9 +66,9 @@ def _soup(F, seed, zmin=0.5, spread=1.2, size=0.4):
 
 
 def _run_native(fv, first, nf, H, W, K, blur, persp, clip, cull, dev):
-    from pertrenderer_amd.renderer.rasterizer import _RasterizeFn
+    from pertrenderer_amd.renderer.rasterizer import _rasterize
     fvt = torch.tensor(fv, device=dev, requires_grad=True)
-    out = _RasterizeFn.apply(fvt, torch.tensor(first, device=dev), torch.tensor(nf, device=dev), H, W, K, blur,
+    out = _rasterize(fvt, torch.tensor(first, device=dev), torch.tensor(nf, device=dev), H, W, K, blur,
                              persp, clip, cull)
     return fvt, out
 
@@ -88,6 +88,9 @@ def test_rasterizer_forward_matches_oracle_bitwise(cfg, device):
                                        cfg["clip"], cfg["cull"])
     assert (rp >= 0).sum() > 100
     np.testing.assert_array_equal(p2f.cpu().numpy(), rp)
+    # the attached valid-prefix counts
+    from pertrenderer_amd.renderer.rasterizer import valid_counts
+    np.testing.assert_array_equal(valid_counts(p2f).cpu().numpy(), (rp >= 0).sum(-1))
     np.testing.assert_array_equal(zbuf.detach().cpu().numpy(), rz)
     np.testing.assert_array_equal(dists.detach().cpu().numpy(), rd)
     np.testing.assert_array_equal(bary.detach().cpu().numpy(), rb)
@@ -180,3 +183,26 @@ def test_mesh_rasterizer_sphere_matches_oracle(size, K, dist_cam, device):
     np.testing.assert_array_equal(frag.dists.cpu().numpy(), rd)
     np.testing.assert_array_equal(frag.bary_coords.cpu().numpy(), rb)
     assert (rp >= 0).sum(-1).max() == min(K, 56)  # the blur radius fills all K slots somewhere (<= 56 here)
+
+
+def test_mesh_batch_with_one_camera_matches_single_meshes(device):
+    """One camera broadcast over a batch of different meshes (PyTorch3D semantics): each image of
+    the batch equals the single-mesh render, with pix_to_face offset by the mesh's first face."""
+    sph, sf, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
+    cub, cf, _ = load_obj(os.path.join(ROOT, "tests", "golden", "cube2.obj"))
+    vl = [sph.to(device), cub.to(device) * 0.5, sph.to(device) * 0.8]
+    fl = [sf.verts_idx.to(device), cf.verts_idx.to(device), sf.verts_idx.to(device)]
+    R, T = look_at_view_transform(2.7, 30.0, 120.0, device=device)
+    cams = FoVPerspectiveCameras(R=R, T=T, device=device)
+    rs = RasterizationSettings(image_size=40, blur_radius=9.2e-3, faces_per_pixel=12)
+    rast = MeshRasterizer(cameras=cams, raster_settings=rs)
+    batch = rast(Meshes(vl, fl))
+    first = 0
+    for i in range(3):
+        single = rast(Meshes([vl[i]], [fl[i]]))
+        p = single.pix_to_face[0]
+        np.testing.assert_array_equal(batch.pix_to_face[i].cpu().numpy(), torch.where(p >= 0, p + first, p).cpu().numpy())
+        np.testing.assert_array_equal(batch.zbuf[i].cpu().numpy(), single.zbuf[0].cpu().numpy())
+        np.testing.assert_array_equal(batch.dists[i].cpu().numpy(), single.dists[0].cpu().numpy())
+        first += fl[i].shape[0]
+    assert (batch.pix_to_face >= 0).sum() > 100
