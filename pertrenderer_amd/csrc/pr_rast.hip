@@ -207,6 +207,80 @@ PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, float& pz) {
   return inbox && !(pz < 0.f) && (inside || d < blur);
 }
 
+// ---- two-stage test (no perspective correction): a cheap stage that only ever REJECTS
+// with certainty, then the exact face_test for the survivors.
+//  * inside: b_i = e_i / area > 0  <=>  e_i != 0 and sign(e_i) == sign(area) (area != 0 for
+//    every uncull'd face).  So "not inside by signs" implies "not inside" exactly.
+//  * edge distance with t = dot * rcp(l2) instead of dot / l2: the squared distance differs
+//    from the exact one by a few ulp of its terms (it is stationary in t at interior
+//    optima, continuous at the clamps); 1e-3 relative is a wide safety band.
+// A lane is rejected only if it is outside its box, or outside the face by signs and
+// farther than blur * (1 + 1e-3).  Everything else runs the exact test, so every decision
+// and every value equals face_test's.
+constexpr float kDistBand = 1e-3f;
+
+PR_DEV float seg_dist2_fast(V2 p, V2 a, float bax, float bay, float l2, V2 b) {
+  const float bx = p.x - b.x, by = p.y - b.y;
+  const float db = bx * bx + by * by;
+  float t = (bax * (p.x - a.x) + bay * (p.y - a.y)) * __builtin_amdgcn_rcpf(l2);
+  t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+  const float qx = a.x + t * bax, qy = a.y + t * bay;
+  const float dx = p.x - qx, dy = p.y - qy;
+  const float ds = dx * dx + dy * dy;
+  return l2 <= kEps ? db : ds;
+}
+
+PR_DEV bool face_maybe(const FaceRec& r, V2 p, float blur, float& dfast) {
+  const bool inbox = !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
+  const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
+  const float e0 = (p.x - v1.x) * r.e.w - (p.y - v1.y) * r.e.z;
+  const float e1 = (p.x - v2.x) * r.f.y - (p.y - v2.y) * r.f.x;
+  const float e2 = (p.x - v0.x) * r.e.y - (p.y - v0.y) * r.e.x;
+  const bool pos = r.d.y > 0.f;
+  const bool ins = e0 != 0.f && e1 != 0.f && e2 != 0.f && (e0 > 0.f) == pos && (e1 > 0.f) == pos &&
+                   (e2 > 0.f) == pos;
+  const float d01 = seg_dist2_fast(p, v0, r.e.x, r.e.y, r.d.z, v1);
+  const float d02 = seg_dist2_fast(p, v0, -r.f.x, -r.f.y, r.f.z, v2);
+  const float d12 = seg_dist2_fast(p, v1, r.e.z, r.e.w, r.d.w, v2);
+  float d = d01 < d02 ? d01 : d02;
+  d = d < d12 ? d : d12;
+  dfast = d;
+  return inbox && (ins || !(d > blur * (1.f + kDistBand)));
+}
+
+// The exact test for a lane that face_maybe kept (no perspective correction): barycentrics,
+// clipping, pz and the inside flag with face_test's operations; the exact edge distance
+// only where the fast one is inside the safety band around blur (a branch that is rarely
+// taken by any lane of the wave).
+template <bool CLIP>
+PR_DEV bool face_test_kept(const FaceRec& r, V2 p, float blur, float dfast, float& pz) {
+  const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
+  const float z0 = r.a.z, z1 = r.b.y, z2 = r.c.x;
+  const float area = r.d.y;
+  const float e0 = (p.x - v1.x) * r.e.w - (p.y - v1.y) * r.e.z;
+  const float e1 = (p.x - v2.x) * r.f.y - (p.y - v2.y) * r.f.x;
+  const float e2 = (p.x - v0.x) * r.e.y - (p.y - v0.y) * r.e.x;
+  const float b[3] = {e0 / area, e1 / area, e2 / area};
+  float bc[3];
+  if constexpr (CLIP) {
+    clip_fwd(b, bc);
+  } else {
+    bc[0] = b[0]; bc[1] = b[1]; bc[2] = b[2];
+  }
+  pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
+  const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
+  bool near = dfast < blur * (1.f - kDistBand);
+  if (!inside && !near && !(dfast > blur * (1.f + kDistBand))) {  // in the band: exact distance
+    const float d01 = seg_dist2_d(p, v0, r.e.x, r.e.y, r.d.z, v1);
+    const float d02 = seg_dist2_d(p, v0, -r.f.x, -r.f.y, r.f.z, v2);
+    const float d12 = seg_dist2_d(p, v1, r.e.z, r.e.w, r.d.w, v2);
+    float d = d01 < d02 ? d01 : d02;
+    d = d < d12 ? d : d12;
+    near = d < blur;
+  }
+  return !(pz < 0.f) && (inside || near);
+}
+
 PR_DEV bool in_bbox(const FaceRec& r, V2 p) {
   return !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
 }
@@ -533,14 +607,25 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
           ok[j] = idx[j] < cnt;
           rr[j] = lrec[min(idx[j], cnt - 1)];  // one LDS wait per group
         }
+        bool maybe[kGroup];
+        float dfast[kGroup];
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j) any |= __ballot(ok[j] && in_bbox(rr[j], p)) != 0;
+        for (int j = 0; j < kGroup; ++j) {
+          // the cheap certain-reject stage (non-perspective; the box test otherwise)
+          dfast[j] = 0.f;
+          if constexpr (PERSP) maybe[j] = ok[j] && in_bbox(rr[j], p);
+          else maybe[j] = ok[j] && face_maybe(rr[j], p, blur, dfast[j]);
+          any |= __ballot(maybe[j]) != 0;
+        }
         if (!any) continue;
 #ifdef PR_RAST_PROFILE
         const int ins_before = n_ins;
 #endif
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j) cand[j] = face_test<PERSP, CLIP>(rr[j], p, blur, pzv[j]) && ok[j];
+        for (int j = 0; j < kGroup; ++j) {
+          if constexpr (PERSP) cand[j] = face_test<PERSP, CLIP>(rr[j], p, blur, pzv[j]) && maybe[j];
+          else cand[j] = face_test_kept<CLIP>(rr[j], p, blur, dfast[j], pzv[j]) && maybe[j];
+        }
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           // clipped barycentrics make pz a convex combination of the vertex depths, so
@@ -1168,10 +1253,11 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
     face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr, fbox);
     if (int e = check_launch("rast_face_prep")) return e;
   }
-  // face slices per pixel (tile 8x8 / 8x4 / 4x4): 2 measured fastest on the bench frame
-  // (113 us vs 117 at 4 and 157 at 1); PR_RAST_SLICES=1|2|4 overrides (sweeps).  FRAG: barycentrics / distances written by the rasterizer itself
+  // face slices per pixel (tile 8x8 / 8x4 / 4x4): 4 measured fastest on the bench frame
+  // with the two-stage face test (107 us vs 118-123 at 2 and 157 at 1); PR_RAST_SLICES=1|2|4
+  // overrides (sweeps).  FRAG: barycentrics / distances written by the rasterizer itself
   // (no second pass over pix_to_face); PR_RAST_FRAG=0 selects the separate pass.
-  int sl = 2;
+  int sl = 4;
   if (const char* e = getenv("PR_RAST_SLICES")) {
     const int v = atoi(e);
     if (v == 1 || v == 2 || v == 4) sl = v;
