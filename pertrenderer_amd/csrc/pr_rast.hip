@@ -635,11 +635,14 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
           const int fid = lcf[min(idx[j], cnt - 1)];
 #pragma unroll
           for (int sl = 0; sl < SL; ++sl) {
-            if (slice == sl && ok[j]) {
-              if (clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
-              const float pz = pzv[j];
-              // (qlast_z, qlast_f) = the queue's last (largest) key
-              if (!done && cand[j] && (qs < K || key_less(pz, fid, qlast_z, qlast_f))) {
+            const bool mine = slice == sl && ok[j];
+            if (mine && clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
+            const float pz = pzv[j];
+            // (qlast_z, qlast_f) = the queue's last (largest) key
+            const bool enter = mine && !done && cand[j] && (qs < K || key_less(pz, fid, qlast_z, qlast_f));
+            if (__ballot(enter) == 0) continue;  // no queue of the wave changes: no state exchange
+            {
+              if (enter) {
                 if (qs == 0 || key_less(qlast_z, qlast_f, pz, fid)) {
                   // append (the common case: faces arrive roughly in depth order)
                   q[qs * TP + pix] = make_float2(pz, __int_as_float(fid));
