@@ -34,7 +34,21 @@ constexpr float kNegInf = -__builtin_inff();
 constexpr float kEpsMaxBM = 5.8f;               // > sqrt(-2 ln 2^-24) = 5.7683
 
 #ifdef PR_BLEND_PROFILE
-#define PR_BPROF_DECL long long bst_[6] = {0, 0, 0, 0, 0, 0}, bt_ = __builtin_amdgcn_s_memtime()
+// diagnostic build: per block [start, end (100 MHz), phases (shader clock) x6, hw id]; fwd
+// blocks at [0, 1<<16), bwd blocks at [1<<16, 2<<16)
+constexpr unsigned kBProfBlocks = 1 << 16;
+__device__ long long g_blend_prof[2 * kBProfBlocks * 10];
+#define PR_BPROF_DECL long long bst_[6] = {0, 0, 0, 0, 0, 0}, bt_ = __builtin_amdgcn_s_memtime(), \
+                      brt_ = __builtin_amdgcn_s_memrealtime()
+#define PR_BPROF_DUMP(which)                                                                   \
+  if (threadIdx.x == 0 && blockIdx.x < kBProfBlocks) {                                         \
+    unsigned hw_;                                                                              \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                          \
+    long long* r_ = g_blend_prof + ((size_t)(which) * kBProfBlocks + blockIdx.x) * 10;         \
+    r_[0] = brt_; r_[1] = (long long)__builtin_amdgcn_s_memrealtime();                          \
+    for (int i_ = 0; i_ < 6; ++i_) r_[2 + i_] = bst_[i_];                                       \
+    r_[8] = hw_; r_[9] = 1;                                                                    \
+  }
 #define PR_BSTAMP(i) (bst_[i] = __builtin_amdgcn_s_memtime() - bt_, bt_ = __builtin_amdgcn_s_memtime())
 #else
 #define PR_BPROF_DECL (void)0
@@ -522,8 +536,7 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
 #ifdef PR_BLEND_PROFILE
   __syncthreads();
   PR_BSTAMP(3);
-  if (tid == 0 && (blockIdx.x % 97) == 0)
-    printf("fwd blk %d | p1 %lld p2 %lld p3 %lld p4 %lld\n", blockIdx.x, bst_[0], bst_[1], bst_[2], bst_[3]);
+  PR_BPROF_DUMP(0);
 #endif
 }
 
@@ -901,9 +914,7 @@ __global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, G
   }
 #ifdef PR_BLEND_PROFILE
   PR_BSTAMP(5);
-  if (tid == 0 && (blockIdx.x % 97) == 0)
-    printf("bwd blk %d | B1 %lld B2 %lld B5 %lld B6 %lld B7 %lld B8+red %lld\n", blockIdx.x, bst_[0], bst_[1], bst_[2],
-           bst_[3], bst_[4], bst_[5]);
+  PR_BPROF_DUMP(1);
 #endif
 }
 
@@ -1109,6 +1120,13 @@ int64_t bwd_blocks(const PRBlendParams& p) {
 }  // namespace pr
 
 using namespace pr;
+
+#ifdef PR_BLEND_PROFILE
+extern "C" int pr_blend_prof_dump(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_blend_prof), bytes < sizeof(g_blend_prof) ? bytes : sizeof(g_blend_prof),
+                             0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "blend_fwd: null args");

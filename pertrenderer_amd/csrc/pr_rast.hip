@@ -411,6 +411,21 @@ PR_DEV int from_slice(int v, int s) {
   }
 }
 
+// v from the lane r places further along the pixel's SL lanes (cyclically): DPP quad
+// rotations, so every lane sees its pixel's other slices
+template <int SL>
+PR_DEV int quad_rot(int v, int r) {
+  if constexpr (SL == 2) {
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  } else {
+    switch (r) {
+      case 1: return __builtin_amdgcn_update_dpp(0, v, 0x39, 0xf, 0xf, false);  // quad_perm [1,2,3,0]
+      case 2: return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+      default: return __builtin_amdgcn_update_dpp(0, v, 0x93, 0xf, 0xf, false); // quad_perm [3,0,1,2]
+    }
+  }
+}
+
 // Forward: per-pixel K nearest (z, face) keys -> pix_to_face, zbuf (+ barycentrics and
 // signed distances with FRAG).  One wave per tile of TP = 64 / SL pixels (8x8, 8x4 or
 // 4x4); lane = pixel * SL + slice.  The SL lanes of a pixel (one DPP quad) split the
@@ -633,6 +648,49 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
           // 1e-6 margin)
           const float zk = lcs[min(idx[j], cnt - 1)];
           const int fid = lcf[min(idx[j], cnt - 1)];
+          if constexpr (SL > 1) {
+            // ---- batch path: when every candidate of the wave is an append (the common
+            //      case, faces arrive in depth order), a pixel's SL candidates enter its
+            //      queue together, each at qs + its rank among them; else the slices insert
+            //      in turn below.  Same queue either way (the K smallest keys, sorted).
+            if (ok[j] && clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
+            const float pz = pzv[j];
+            const bool enter = ok[j] && !done && cand[j] && (qs < K || key_less(pz, fid, qlast_z, qlast_f));
+            const bool app = enter && (qs == 0 || key_less(qlast_z, qlast_f, pz, fid));
+            if (__ballot(enter && !app) == 0) {
+              if (__ballot(enter) == 0) continue;
+              bool oe[SL - 1];
+              float oz[SL - 1];
+              int of[SL - 1];
+              int rank = 0, nq = enter ? 1 : 0;
+#pragma unroll
+              for (int r = 1; r < SL; ++r) {
+                oe[r - 1] = quad_rot<SL>((int)enter, r) != 0;
+                oz[r - 1] = __int_as_float(quad_rot<SL>(__float_as_int(pz), r));
+                of[r - 1] = quad_rot<SL>(fid, r);
+                nq += oe[r - 1] ? 1 : 0;
+                rank += (enter && oe[r - 1] && key_less(oz[r - 1], of[r - 1], pz, fid)) ? 1 : 0;
+              }
+              const int nkept = min(nq, K - qs);  // the largest ones drop off a full queue
+              if (enter && rank < nkept) q[(qs + rank) * TP + pix] = make_float2(pz, __int_as_float(fid));
+              if (nkept > 0) {  // new last key: the entered one of rank nkept - 1
+                const bool last = enter && rank == nkept - 1;
+                float lz = pz;
+                int lf = fid;
+#pragma unroll
+                for (int r = 1; r < SL; ++r) {
+                  if (quad_rot<SL>((int)last, r) != 0) { lz = oz[r - 1]; lf = of[r - 1]; }
+                }
+                qlast_z = lz;
+                qlast_f = lf;
+                qs += nkept;
+              }
+#ifdef PR_RAST_PROFILE
+              n_app += enter && rank < nkept ? 1 : 0;
+#endif
+              continue;
+            }
+          }
 #pragma unroll
           for (int sl = 0; sl < SL; ++sl) {
             const bool mine = slice == sl && ok[j];
