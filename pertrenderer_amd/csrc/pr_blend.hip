@@ -55,6 +55,15 @@ __device__ long long g_blend_prof[2 * kBProfBlocks * 10];
 #define PR_BSTAMP(i) (void)0
 #endif
 
+// minimum waves per SIMD the blend kernels are compiled for (caps their VGPRs); sweeps
+// override with -DPR_BLEND_FWD_WPE=... / -DPR_BLEND_BWD_WPE=...
+#ifndef PR_BLEND_FWD_WPE
+#define PR_BLEND_FWD_WPE 1
+#endif
+#ifndef PR_BLEND_BWD_WPE
+#define PR_BLEND_BWD_WPE 1
+#endif
+
 struct Geo {
   int64_t P, PK;  // pixels, slots
   int K, KP1, PB, HW;
@@ -272,7 +281,7 @@ PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
 // ================================================================== forward
 // CM: colour mode, 0 = weights out (no colour), 1 = texel colours, 2 = vertex colours
 template <int NOISE, bool RAST, int CM>
-__global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, Geo g, int NC) {
+__global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(PRBlendFwdArgs a, Geo g, int NC) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
   const Sc sc = resolve(p);
@@ -542,7 +551,7 @@ __global__ void __launch_bounds__(kThreads) blend_fwd_kernel(PRBlendFwdArgs a, G
 
 // ================================================================= backward
 template <int NOISE, bool RAST, int CM>
-__global__ void __launch_bounds__(kThreads) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
+__global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
   const Sc sc = resolve(p);
