@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 7
+#define PR_ABI_VERSION 8
 
 /* error codes */
 #define PR_OK 0
@@ -171,6 +171,7 @@ typedef struct PRRastArgs {
   /* nullable (N,H,W) valid-prefix counts: slots 0..count-1 of a pixel hold faces, the rest -1.  */
   /* Forward: written.  Backward: if set (the forward's), pix_to_face is read only below it.    */
   int32_t* pix_count;
+  int32_t flags;                    /* PR_GRAD_PREZEROED: pr_rast_bwd does not zero grad_face_verts */
 } PRRastArgs;
 
 typedef struct PRInterpArgs {
@@ -204,9 +205,19 @@ typedef struct PRProjectArgs {
   float* face_verts;           /* fwd out (F,3,3) */
   const float* grad_face_verts;/* bwd in (F,3,3) */
   float* grad_verts;           /* bwd out (V,3), overwritten */
+  int32_t flags;               /* PR_GRAD_PREZEROED: pr_project_bwd does not zero grad_verts */
 } PRProjectArgs;
 
+/* the backward's gradient accumulator was zeroed by the forward (pr_project_rast_fwd) */
+#define PR_GRAD_PREZEROED 1
+
 int pr_project_fwd(const PRProjectArgs* args, void* stream);
+/* MeshRasterizer.forward's projection (eval.py:165-168: world -> view -> NDC with view z, face
+   gather) fused with pr_rast_fwd: one face pass instead of pr_project_fwd + the rasterizer's
+   face preparation.  pa->face_verts receives the projected corners and must equal
+   ra->face_verts.  Non-null ra->grad_face_verts / pa->grad_verts are zeroed here, for a
+   pr_rast_bwd / pr_project_bwd with flags PR_GRAD_PREZEROED. */
+int pr_project_rast_fwd(const PRProjectArgs* pa, const PRRastArgs* ra, void* stream);
 int pr_project_bwd(const PRProjectArgs* args, void* stream);
 
 /* Pose of the pose-optimisation loop (experiments/eval.py:343-346; PyTorch3D 0.4.0

@@ -22,6 +22,7 @@ PR_BLEND_RAST_CAUCHY = 8
 PR_BLEND_AGG_CAUCHY = 16
 PR_BLEND_RAST_WOVR = 32
 PR_BLEND_AGG_WOVR = 64
+PR_GRAD_PREZEROED = 1
 
 _vp = C.c_void_p
 
@@ -71,7 +72,7 @@ class PRRastArgs(C.Structure):
                 ("pix_to_face", _vp), ("zbuf", _vp), ("bary", _vp), ("dists", _vp),
                 ("grad_zbuf", _vp), ("grad_bary", _vp), ("grad_dists", _vp),
                 ("grad_face_verts", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
-                ("pix_count", _vp)]
+                ("pix_count", _vp), ("flags", C.c_int32)]
 
 
 class PRInterpArgs(C.Structure):
@@ -83,7 +84,7 @@ class PRInterpArgs(C.Structure):
 class PRProjectArgs(C.Structure):
     _fields_ = [("verts", _vp), ("faces", _vp), ("mesh_first_face", _vp), ("mesh_num_faces", _vp),
                 ("world_to_view", _vp), ("proj", _vp), ("V", C.c_int64), ("F", C.c_int64), ("N", C.c_int32),
-                ("face_verts", _vp), ("grad_face_verts", _vp), ("grad_verts", _vp)]
+                ("face_verts", _vp), ("grad_face_verts", _vp), ("grad_verts", _vp), ("flags", C.c_int32)]
 
 
 class PRSO3Args(C.Structure):
@@ -115,12 +116,13 @@ EXPORTS = {
     "pr_seed_advance": (C.c_int, [_vp, C.c_int32, _vp]),
     "pr_project_fwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
     "pr_project_bwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
+    "pr_project_rast_fwd": (C.c_int, [C.POINTER(PRProjectArgs), C.POINTER(PRRastArgs), _vp]),
     "pr_so3_exp_fwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
     "pr_so3_exp_bwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
 }
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lib = None
 

@@ -108,31 +108,38 @@ struct FaceRec {
   float4 f;  // D20.x D20.y l2_20 z_min   (D20 = v0 - v2)
 };
 
+// the face record and cull box of one face from its projected corners
+PR_DEV void write_face_rec(const float v[9], float blur, int cull_backfaces, FaceRec* out, float4* bbox) {
+  const float x0 = v[0], y0 = v[1], z0 = v[2], x1 = v[3], y1 = v[4], z1 = v[5], x2 = v[6], y2 = v[7], z2 = v[8];
+  const float r = sqrtf(blur);
+  float xmin = fminf(x0, fminf(x1, x2)) - r, xmax = fmaxf(x0, fmaxf(x1, x2)) + r;
+  float ymin = fminf(y0, fminf(y1, y2)) - r, ymax = fmaxf(y0, fmaxf(y1, y2)) + r;
+  const float zmax = fmaxf(z0, fmaxf(z1, z2));
+  const float area = edge_fn(V2{x0, y0}, V2{x1, y1}, V2{x2, y2});
+  const bool back = area < 0.f;
+  const bool zero_area = area <= kEps && area >= -kEps;
+  const bool valid = !(zmax < 0.f || (cull_backfaces && back) || zero_area);
+  if (!valid) { xmin = ymin = __builtin_inff(); xmax = ymax = -__builtin_inff(); }
+  const float d01x = x1 - x0, d01y = y1 - y0, d12x = x2 - x1, d12y = y2 - y1, d20x = x0 - x2, d20y = y0 - y2;
+  FaceRec rec;
+  rec.a = make_float4(x0, y0, z0, x1);
+  rec.b = make_float4(y1, z1, x2, y2);
+  rec.c = make_float4(z2, xmin, xmax, ymin);
+  rec.d = make_float4(ymax, edge_fn(V2{x2, y2}, V2{x0, y0}, V2{x1, y1}) + kEps, d01x * d01x + d01y * d01y,
+                      d12x * d12x + d12y * d12y);
+  rec.e = make_float4(d01x, d01y, d12x, d12y);
+  rec.f = make_float4(d20x, d20y, d20x * d20x + d20y * d20y, fminf(z0, fminf(z1, z2)));
+  *out = rec;
+  *bbox = make_float4(xmin, xmax, ymin, ymax);
+}
+
 __global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cull_backfaces, FaceRec* out,
                                  float4* bbox) {
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < F; f += (int64_t)gridDim.x * blockDim.x) {
-    const float* v = fv + f * 9;
-    const float x0 = v[0], y0 = v[1], z0 = v[2], x1 = v[3], y1 = v[4], z1 = v[5], x2 = v[6], y2 = v[7], z2 = v[8];
-    const float r = sqrtf(blur);
-    float xmin = fminf(x0, fminf(x1, x2)) - r, xmax = fmaxf(x0, fmaxf(x1, x2)) + r;
-    float ymin = fminf(y0, fminf(y1, y2)) - r, ymax = fmaxf(y0, fmaxf(y1, y2)) + r;
-    const float zmax = fmaxf(z0, fmaxf(z1, z2));
-    const float area = edge_fn(V2{x0, y0}, V2{x1, y1}, V2{x2, y2});
-    const bool back = area < 0.f;
-    const bool zero_area = area <= kEps && area >= -kEps;
-    const bool valid = !(zmax < 0.f || (cull_backfaces && back) || zero_area);
-    if (!valid) { xmin = ymin = __builtin_inff(); xmax = ymax = -__builtin_inff(); }
-    const float d01x = x1 - x0, d01y = y1 - y0, d12x = x2 - x1, d12y = y2 - y1, d20x = x0 - x2, d20y = y0 - y2;
-    FaceRec rec;
-    rec.a = make_float4(x0, y0, z0, x1);
-    rec.b = make_float4(y1, z1, x2, y2);
-    rec.c = make_float4(z2, xmin, xmax, ymin);
-    rec.d = make_float4(ymax, edge_fn(V2{x2, y2}, V2{x0, y0}, V2{x1, y1}) + kEps, d01x * d01x + d01y * d01y,
-                        d12x * d12x + d12y * d12y);
-    rec.e = make_float4(d01x, d01y, d12x, d12y);
-    rec.f = make_float4(d20x, d20y, d20x * d20x + d20y * d20y, fminf(z0, fminf(z1, z2)));
-    out[f] = rec;
-    bbox[f] = make_float4(xmin, xmax, ymin, ymax);
+    float v[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) v[i] = fv[f * 9 + i];
+    write_face_rec(v, blur, cull_backfaces, out + f, bbox + f);
   }
 }
 
@@ -1239,6 +1246,36 @@ __global__ void project_fwd_kernel(PRProjectArgs a) {
   }
 }
 
+// MeshRasterizer's projection and the rasterizer's face preparation in one pass (one
+// thread per face, project_fwd_kernel's operations per corner), plus the zeroing of the
+// backward's accumulators (grad_face_verts, grad_verts) so the backward needs no memset.
+__global__ void project_prep_kernel(PRProjectArgs a, float blur, int cull_backfaces, FaceRec* recs, float4* bbox,
+                                    float* zero_fv, float* zero_v) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.F; f += stride) {
+    const int n = mesh_of(a.mesh_first_face, a.mesh_num_faces, a.N, f);
+    float fv[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float* v = a.verts + a.faces[f * 3 + i] * 3;
+      float o[4], c[4];
+      xform(a.world_to_view + n * 16, v[0], v[1], v[2], o);
+      const float vx = o[0] / o[3], vy = o[1] / o[3], vz = o[2] / o[3];
+      xform(a.proj + n * 16, vx, vy, vz, c);
+      fv[i * 3 + 0] = c[0] / c[3];
+      fv[i * 3 + 1] = c[1] / c[3];
+      fv[i * 3 + 2] = vz;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) a.face_verts[f * 9 + i] = fv[i];
+    write_face_rec(fv, blur, cull_backfaces, recs + f, bbox + f);
+  }
+  if (zero_fv)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.F * 9; i += stride) zero_fv[i] = 0.f;
+  if (zero_v)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.V * 3; i += stride) zero_v[i] = 0.f;
+}
+
 __global__ void project_bwd_kernel(PRProjectArgs a) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.F * 3; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t f = t / 3;
@@ -1299,6 +1336,8 @@ extern "C" size_t pr_rast_fwd_workspace_size(const PRRastArgs* a) {
   return (size_t)(a->F > 0 ? a->F : 1) * (sizeof(FaceRec) + sizeof(float4));  // records + compact boxes
 }
 
+static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const float4* fbox, hipStream_t st);
+
 extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "rast_fwd: null args");
   const PRRastArgs& a = *args;
@@ -1314,6 +1353,10 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
     face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr, fbox);
     if (int e = check_launch("rast_face_prep")) return e;
   }
+  return rast_fwd_prepared(a, fr, fbox, st);
+}
+
+static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const float4* fbox, hipStream_t st) {
   // face slices per pixel (tile 8x8 / 8x4 / 4x4): 4 measured fastest on the bench frame
   // with the two-stage face test (107 us vs 118-123 at 2 and 157 at 1); PR_RAST_SLICES=1|2|4
   // overrides (sweeps).  FRAG: barycentrics / distances written by the rasterizer itself
@@ -1345,7 +1388,7 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
   if (int e = rast_check(a)) return e;
   if (!a.pix_to_face || !a.grad_face_verts) return set_error(PR_ERR_ARG, "rast_bwd: buffer missing");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (a.F > 0) {
+  if (a.F > 0 && !(a.flags & PR_GRAD_PREZEROED)) {
     if (hipMemsetAsync(a.grad_face_verts, 0, (size_t)a.F * 9 * sizeof(float), st) != hipSuccess)
       return set_error(PR_ERR_HIP, "rast_bwd: memset failed");
   }
@@ -1406,10 +1449,35 @@ extern "C" int pr_project_bwd(const PRProjectArgs* args, void* stream) {
   if (int e = project_check(args)) return e;
   if (!args->grad_face_verts || !args->grad_verts) return set_error(PR_ERR_ARG, "project_bwd: buffers missing");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (args->V > 0 && hipMemsetAsync(args->grad_verts, 0, (size_t)args->V * 3 * sizeof(float), st) != hipSuccess)
+  if (args->V > 0 && !(args->flags & PR_GRAD_PREZEROED) &&
+      hipMemsetAsync(args->grad_verts, 0, (size_t)args->V * 3 * sizeof(float), st) != hipSuccess)
     return set_error(PR_ERR_HIP, "project_bwd: memset failed");
   if (args->F == 0) return PR_OK;
   const int nb = (int)std::min<int64_t>((args->F * 3 + kThreads - 1) / kThreads, 4096);
   project_bwd_kernel<<<nb, kThreads, 0, st>>>(*args);
   return check_launch("project_bwd");
+}
+
+extern "C" int pr_project_rast_fwd(const PRProjectArgs* pa, const PRRastArgs* ra, void* stream) {
+  if (int e = project_check(pa)) return e;
+  if (!ra) return set_error(PR_ERR_ARG, "project_rast_fwd: null rast args");
+  const PRRastArgs& a = *ra;
+  if (int e = rast_check(a)) return e;
+  if (!pa->face_verts || pa->face_verts != a.face_verts || pa->F != a.F || pa->N != a.N)
+    return set_error(PR_ERR_ARG, "project_rast_fwd: projection and rasterizer face buffers / counts differ");
+  if (!a.pix_to_face || !a.zbuf || !a.bary || !a.dists) return set_error(PR_ERR_ARG, "rast_fwd: output missing");
+  if (!a.workspace || a.workspace_bytes < pr_rast_fwd_workspace_size(ra))
+    return set_error(PR_ERR_WORKSPACE, "rast_fwd: workspace too small");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  FaceRec* fr = reinterpret_cast<FaceRec*>(a.workspace);
+  float4* fbox = reinterpret_cast<float4*>(fr + (a.F > 0 ? a.F : 1));
+  const int64_t work = std::max<int64_t>(std::max<int64_t>(a.F, a.grad_face_verts ? a.F * 9 : 0),
+                                         pa->grad_verts ? pa->V * 3 : 0);
+  if (work > 0) {
+    const int nb = (int)std::min<int64_t>((work + kThreads - 1) / kThreads, 1024);
+    project_prep_kernel<<<nb, kThreads, 0, st>>>(*pa, a.blur_radius, a.cull_backfaces, fr, fbox, a.grad_face_verts,
+                                                 pa->grad_verts);
+    if (int e = check_launch("project_prep")) return e;
+  }
+  return rast_fwd_prepared(a, fr, fbox, st);
 }

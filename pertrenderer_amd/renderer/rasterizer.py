@@ -125,6 +125,94 @@ class _RasterizeFn(torch.autograd.Function):
         return gfv, None, None, None, None, None, None, None, None, None
 
 
+class _ProjectRasterizeFn(torch.autograd.Function):
+    """MeshRasterizer.forward's fast path as one op: world verts -> (projection + face gather +
+    rasterization) -> fragments (pr_project_rast_fwd: one face pass, then the rasterizer);
+    backward: pr_rast_bwd then pr_project_bwd into d verts, their accumulators zeroed by the
+    forward kernel (no memsets).  Same values as project_faces followed by _RasterizeFn."""
+
+    @staticmethod
+    def forward(ctx, verts, faces, first, nfaces, w2v, proj, H, W, K, blur, persp, clip, cull):
+        from .project import _per_mesh
+        nat.require_device(verts, faces, first, nfaces, w2v, proj)
+        lib = nat.load()
+        v = verts.detach().to(F32).contiguous()
+        f = faces.detach().to(torch.int64).contiguous()
+        N, F, dev = first.shape[0], f.shape[0], v.device
+        m1, m2 = _per_mesh(w2v, N, "world_to_view"), _per_mesh(proj, N, "projection")
+        fv = torch.empty((F, 3, 3), dtype=F32, device=dev)
+        need = ctx.needs_input_grad[0]
+        gfv = torch.empty((F, 3, 3), dtype=F32, device=dev) if need else None
+        gv = torch.empty_like(v) if need else None
+        pa = nat.PRProjectArgs()
+        pa.verts, pa.faces, pa.mesh_first_face, pa.mesh_num_faces = nat.ptr(v), nat.ptr(f), nat.ptr(first), nat.ptr(nfaces)
+        pa.world_to_view, pa.proj = nat.ptr(m1), nat.ptr(m2)
+        pa.V, pa.F, pa.N = v.shape[0], F, N
+        pa.face_verts, pa.grad_verts = nat.ptr(fv), nat.ptr(gv)
+        a = nat.PRRastArgs()
+        a.face_verts, a.mesh_first_face, a.mesh_num_faces = nat.ptr(fv), nat.ptr(first), nat.ptr(nfaces)
+        a.F, a.N, a.H, a.W, a.K = F, N, H, W, K
+        a.blur_radius, a.perspective_correct = float(blur), int(persp)
+        a.clip_barycentric_coords, a.cull_backfaces = int(clip), int(cull)
+        p2f = torch.empty((N, H, W, K), dtype=torch.int64, device=dev)
+        zbuf = torch.empty((N, H, W, K), dtype=F32, device=dev)
+        bary = torch.empty((N, H, W, K, 3), dtype=F32, device=dev)
+        dists = torch.empty((N, H, W, K), dtype=F32, device=dev)
+        counts = torch.empty((N, H, W), dtype=torch.int32, device=dev)
+        a.pix_to_face, a.zbuf, a.bary, a.dists = nat.ptr(p2f), nat.ptr(zbuf), nat.ptr(bary), nat.ptr(dists)
+        a.pix_count, a.grad_face_verts = nat.ptr(counts), nat.ptr(gfv)
+        ws = torch.empty(max(1, lib.pr_rast_fwd_workspace_size(a)), dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
+        timing = _timing.active()
+        if timing is not None:
+            timing.start("rast_fwd")
+        nat.check(lib.pr_project_rast_fwd(pa, a, nat.stream_of(fv)), "pr_project_rast_fwd")
+        if timing is not None:
+            timing.stop("rast_fwd")
+        ctx.save_for_backward(v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv)
+        ctx.cfg = (H, W, K, float(blur), int(persp), int(clip), int(cull))
+        ctx.prezeroed = True
+        ctx.mark_non_differentiable(p2f, counts)
+        ctx.set_materialize_grads(False)
+        return p2f, zbuf, bary, dists, counts
+
+    @staticmethod
+    def backward(ctx, gp2f, gzbuf, gbary, gdists, gcounts):
+        v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv = ctx.saved_tensors
+        if gfv is None:
+            return (None,) * 13
+        H, W, K, blur, persp, clip, cull = ctx.cfg
+        # a second backward (retain_graph) finds the accumulators used: zero them again
+        flags = nat.PR_GRAD_PREZEROED if ctx.prezeroed else 0
+        ctx.prezeroed = False
+        lib = nat.load()
+        a = nat.PRRastArgs()
+        a.face_verts, a.mesh_first_face, a.mesh_num_faces = nat.ptr(fv), nat.ptr(first), nat.ptr(nfaces)
+        a.F, a.N, a.H, a.W, a.K = fv.shape[0], first.shape[0], H, W, K
+        a.blur_radius, a.perspective_correct, a.clip_barycentric_coords, a.cull_backfaces = blur, persp, clip, cull
+        a.pix_to_face, a.pix_count, a.flags = nat.ptr(p2f), nat.ptr(counts), flags
+        keep = []
+        for name, g in (("grad_zbuf", gzbuf), ("grad_bary", gbary), ("grad_dists", gdists)):
+            if g is not None:
+                g = g.detach().to(F32).contiguous()
+                keep.append(g)
+                setattr(a, name, nat.ptr(g))
+        a.grad_face_verts = nat.ptr(gfv)
+        timing = _timing.active()
+        if timing is not None:
+            timing.start("rast_bwd")
+        nat.check(lib.pr_rast_bwd(a, nat.stream_of(fv)), "pr_rast_bwd")
+        if timing is not None:
+            timing.stop("rast_bwd")
+        pa = nat.PRProjectArgs()
+        pa.verts, pa.faces, pa.mesh_first_face, pa.mesh_num_faces = nat.ptr(v), nat.ptr(f), nat.ptr(first), nat.ptr(nfaces)
+        pa.world_to_view, pa.proj = nat.ptr(m1), nat.ptr(m2)
+        pa.V, pa.F, pa.N = v.shape[0], f.shape[0], first.shape[0]
+        pa.grad_face_verts, pa.grad_verts, pa.flags = nat.ptr(gfv), nat.ptr(gv), flags
+        nat.check(lib.pr_project_bwd(pa, nat.stream_of(gv)), "pr_project_bwd")
+        return (gv,) + (None,) * 12
+
+
 def rasterize_meshes(meshes, image_size=256, blur_radius=0.0, faces_per_pixel=8, bin_size=None,
                      max_faces_per_bin=None, perspective_correct=False, clip_barycentric_coords=False,
                      cull_backfaces=False):
@@ -177,13 +265,12 @@ class MeshRasterizer(torch.nn.Module):
             # fused native projection + face gather (pr_project_*), then the rasterizer
             first = meshes_world.mesh_to_faces_packed_first_idx()
             nfaces = meshes_world.num_faces_per_mesh()
-            fv = project_faces(meshes_world.verts_packed(), meshes_world.faces_packed(), first, nfaces,
-                               cameras.world_to_view_matrix(), cameras.projection_matrix())
             H, W = _hw(rs.image_size)
-            p2f, zbuf, bary, dists = _rasterize(fv, first, nfaces, H, W, int(rs.faces_per_pixel),
-                                                float(rs.blur_radius), bool(rs.perspective_correct),
-                                                bool(clip), bool(rs.cull_backfaces))
-            return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)
+            p2f, zbuf, bary, dists, counts = _ProjectRasterizeFn.apply(
+                meshes_world.verts_packed(), meshes_world.faces_packed(), first, nfaces,
+                cameras.world_to_view_matrix(), cameras.projection_matrix(), H, W, int(rs.faces_per_pixel),
+                float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces))
+            return Fragments(pix_to_face=attach_valid_counts(p2f, counts), zbuf=zbuf, bary_coords=bary, dists=dists)
         meshes_screen = self.transform(meshes_world, **kwargs)
         p2f, zbuf, bary, dists = rasterize_meshes(
             meshes_screen, image_size=rs.image_size, blur_radius=rs.blur_radius,

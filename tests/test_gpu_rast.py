@@ -206,3 +206,36 @@ def test_mesh_batch_with_one_camera_matches_single_meshes(device):
         np.testing.assert_array_equal(batch.dists[i].cpu().numpy(), single.dists[0].cpu().numpy())
         first += fl[i].shape[0]
     assert (batch.pix_to_face >= 0).sum() > 100
+
+
+def test_fused_projection_rasterizer_matches_separate_ops(device):
+    """pr_project_rast_fwd (MeshRasterizer's fast path) == pr_project_fwd + pr_rast_fwd: fragments
+    bit for bit; d verts through the pre-zeroed accumulators == through the memset path (float
+    atomics: summation order), including a second backward (retain_graph)."""
+    from pertrenderer_amd.renderer.rasterizer import _rasterize
+    verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
+    R, T = look_at_view_transform(2.7, 30.0, 120.0, device=device)
+    cams = FoVPerspectiveCameras(R=R, T=T, device=device)
+    rs = RasterizationSettings(image_size=48, blur_radius=9.2e-3, faces_per_pixel=20)
+    g = torch.Generator().manual_seed(5)
+    gz, gb, gd = (torch.randn(s, generator=g).to(device) for s in ((1, 48, 48, 20), (1, 48, 48, 20, 3), (1, 48, 48, 20)))
+    v1 = verts.to(device).requires_grad_(True)
+    m1 = Meshes([v1], [faces.verts_idx.to(device)])
+    fr = MeshRasterizer(cameras=cams, raster_settings=rs)(m1)
+    loss1 = (fr.zbuf * gz).sum() + (fr.bary_coords * gb).sum() + (fr.dists * gd).sum()
+    loss1.backward(retain_graph=True)
+    g1 = v1.grad.clone()
+    v1.grad = None
+    loss1.backward()
+    g1b = v1.grad.clone()
+    v2 = verts.to(device).requires_grad_(True)
+    m2 = Meshes([v2], [faces.verts_idx.to(device)])
+    fv = project_faces(m2.verts_packed(), m2.faces_packed(), m2.mesh_to_faces_packed_first_idx(),
+                       m2.num_faces_per_mesh(), cams.world_to_view_matrix(), cams.projection_matrix())
+    p2f, zbuf, bary, dists = _rasterize(fv, m2.mesh_to_faces_packed_first_idx(), m2.num_faces_per_mesh(), 48, 48, 20,
+                                        9.2e-3, False, True, False)
+    for a, b in ((fr.pix_to_face, p2f), (fr.zbuf, zbuf), (fr.bary_coords, bary), (fr.dists, dists)):
+        assert torch.equal(a, b)
+    ((zbuf * gz).sum() + (bary * gb).sum() + (dists * gd).sum()).backward()
+    assert_close(g1, v2.grad, rtol=1e-4, atol_rel=1e-5, name="d verts")
+    assert_close(g1b, v2.grad, rtol=1e-4, atol_rel=1e-5, name="d verts (second backward)")
