@@ -1,6 +1,6 @@
 """Benchmark of the perturbed-renderer hot path (BASELINE.json configs[1]).
 
-One step = one pose-optimisation iteration of experiments/eval.py:343-370: rotate
+One step = one pose-optimisation iteration of experiments/eval.py:343-376: rotate
 the mesh (so3 exp map), MeshRasterizer (native K-nearest rasterizer, 256x256,
 faces_per_pixel=50, blur = ln(1/1e-4 - 1)*sigma), RandomSimpleShader with
 GaussianRast(nb_samples=8) + GaussianAgg(nb_samples=8) (fused native blend with
@@ -251,7 +251,8 @@ def build_step(wl, world, mode, device):
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    # thread_local: CUDA calls of other threads (the RCCL watchdog at N>1) must not void the capture
+    with torch.cuda.graph(graph, capture_error_mode="thread_local"):
         ds.advance()
         wl.forward().backward()
         if world == 1:
@@ -260,7 +261,7 @@ def build_step(wl, world, mode, device):
     if world == 1:
         return graph.replay
     opt_graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(opt_graph):
+    with torch.cuda.graph(opt_graph, capture_error_mode="thread_local"):
         wl.opt.step()
     wl.opt_graph = opt_graph
 
