@@ -4,21 +4,22 @@
 // MeshRasterizer at experiments/eval.py:165-168).  Semantics restated in
 // SURVEY.md §8 a10/a11 and oracle/rast_oracle.c.
 //
-// Forward (MI355X layout): one wave per 8x8 pixel tile, one lane per pixel.
-// The mesh's faces stream through LDS in 64-face chunks; a chunk is culled
-// against the tile's NDC rectangle (expanded face bbox) and compacted with a
-// wave ballot, then every lane tests the surviving faces against its pixel
-// (LDS broadcast reads).  Each lane keeps its K nearest (z, face) keys in a
-// per-lane column of an LDS queue kept sorted by (z, face id), which is exactly
-// PyTorch3D's ordering; barycentrics/distances of the K winners are recomputed
-// once at the end.
+// Forward (MI355X layout): one wave per tile (4x4 pixels by default), lane = (pixel,
+// face slice).  The tile's faces are culled (fp16 boxes, ballot compaction), sorted by
+// depth near the tile centre and staged through LDS in chunks; the slices of a pixel test
+// interleaved sorted positions with a two-stage (certain-reject, then exact) face test and
+// share one K-queue per pixel in LDS, sorted by (z, face id) -- PyTorch3D's ordering.  The
+// output pass writes p2f/zbuf, the winners' barycentrics / distances and the per-pixel
+// valid-prefix counts.  MeshRasterizer's projection can run in the same face pass
+// (pr_project_rast_fwd).
 //
-// Backward: flat slot loop; each workgroup pre-reduces its face-gradient
-// contributions in an LDS hash table keyed by face id before one global
-// atomic per (face, component), so hot faces shared by neighbouring pixels
-// do not serialise on global atomics.
+// Backward: per tile, the valid slots are compacted, each face gets a tile-local index,
+// the per-slot gradients go to LDS without atomics and are summed per face by a
+// face x pixel transpose; one global atomic per (face, component) per tile.
 #include <cstdlib>
 #include <type_traits>
+
+#include <hip/hip_fp16.h>
 
 #include "pr_common.h"
 
@@ -109,7 +110,22 @@ struct FaceRec {
 };
 
 // the face record and cull box of one face from its projected corners
-PR_DEV void write_face_rec(const float v[9], float blur, int cull_backfaces, FaceRec* out, float4* bbox) {
+// Cull boxes in fp16, rounded outward (never smaller than the exact box): 8 B per face of
+// L2 traffic per tile instead of 16.  The cull only selects a superset; the per-pixel test
+// re-checks the exact box from the face record, so results do not change.
+PR_DEV uint32_t half_bits(__half h) { return (uint32_t)__half_as_ushort(h); }
+PR_DEV uint2 pack_box(float xmin, float xmax, float ymin, float ymax) {
+  return make_uint2(half_bits(__float2half_rd(xmin)) | (half_bits(__float2half_ru(xmax)) << 16),
+                    half_bits(__float2half_rd(ymin)) | (half_bits(__float2half_ru(ymax)) << 16));
+}
+PR_DEV float4 unpack_box(uint2 b) {
+  return make_float4(__half2float(__ushort_as_half((unsigned short)(b.x & 0xffffu))),
+                     __half2float(__ushort_as_half((unsigned short)(b.x >> 16))),
+                     __half2float(__ushort_as_half((unsigned short)(b.y & 0xffffu))),
+                     __half2float(__ushort_as_half((unsigned short)(b.y >> 16))));
+}
+
+PR_DEV void write_face_rec(const float v[9], float blur, int cull_backfaces, FaceRec* out, uint2* bbox) {
   const float x0 = v[0], y0 = v[1], z0 = v[2], x1 = v[3], y1 = v[4], z1 = v[5], x2 = v[6], y2 = v[7], z2 = v[8];
   const float r = sqrtf(blur);
   float xmin = fminf(x0, fminf(x1, x2)) - r, xmax = fmaxf(x0, fmaxf(x1, x2)) + r;
@@ -130,11 +146,11 @@ PR_DEV void write_face_rec(const float v[9], float blur, int cull_backfaces, Fac
   rec.e = make_float4(d01x, d01y, d12x, d12y);
   rec.f = make_float4(d20x, d20y, d20x * d20x + d20y * d20y, fminf(z0, fminf(z1, z2)));
   *out = rec;
-  *bbox = make_float4(xmin, xmax, ymin, ymax);
+  *bbox = pack_box(xmin, xmax, ymin, ymax);
 }
 
 __global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cull_backfaces, FaceRec* out,
-                                 float4* bbox) {
+                                 uint2* bbox) {
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < F; f += (int64_t)gridDim.x * blockDim.x) {
     float v[9];
 #pragma unroll
@@ -449,7 +465,7 @@ PR_DEV int quad_rot(int v, int r) {
 // neither on SL nor on the traversal order.
 template <int SL, bool PERSP, bool CLIP, bool FRAG>
 __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces,
-                                                      const float4* __restrict__ fbox) {
+                                                      const uint2* __restrict__ fbox) {
   constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
   constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
   extern __shared__ float smem[];
@@ -498,7 +514,7 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
 #pragma unroll
       for (int u = 0; u < kCullU; ++u) {
         const int64_t f = base + u * 64 + lane;
-        bb[u] = fbox[f < fe ? f : fe - 1];
+        bb[u] = unpack_box(fbox[f < fe ? f : fe - 1]);
       }
       int64_t next = base + 64 * kCullU;
       bool stop = false;  // wave-uniform; no break, so bb[] stays in registers
@@ -838,7 +854,7 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
 }
 
 template <int SL, bool PERSP, bool CLIP>
-void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const float4* fb, bool frag, size_t lds,
+void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, bool frag, size_t lds,
                         hipStream_t st) {
   constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW;
   dim3 grid((a.W + TW - 1) / TW, (a.H + TH - 1) / TH, a.N);
@@ -847,14 +863,14 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const float4* fb
 }
 
 template <bool PERSP, bool CLIP>
-void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, const float4* fb, int sl, bool frag, size_t lds,
+void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, int sl, bool frag, size_t lds,
                         hipStream_t st) {
   if (sl == 4) launch_rast_fwd_sl<4, PERSP, CLIP>(a, fr, fb, frag, lds, st);
   else if (sl == 2) launch_rast_fwd_sl<2, PERSP, CLIP>(a, fr, fb, frag, lds, st);
   else launch_rast_fwd_sl<1, PERSP, CLIP>(a, fr, fb, frag, lds, st);
 }
 
-void launch_rast_fwd(const PRRastArgs& a, const FaceRec* fr, const float4* fb, int sl, bool frag, size_t lds,
+void launch_rast_fwd(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, int sl, bool frag, size_t lds,
                      hipStream_t st) {
   const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
   if (persp && clip) launch_rast_fwd_pc<true, true>(a, fr, fb, sl, frag, lds, st);
@@ -1249,7 +1265,7 @@ __global__ void project_fwd_kernel(PRProjectArgs a) {
 // MeshRasterizer's projection and the rasterizer's face preparation in one pass (one
 // thread per face, project_fwd_kernel's operations per corner), plus the zeroing of the
 // backward's accumulators (grad_face_verts, grad_verts) so the backward needs no memset.
-__global__ void project_prep_kernel(PRProjectArgs a, float blur, int cull_backfaces, FaceRec* recs, float4* bbox,
+__global__ void project_prep_kernel(PRProjectArgs a, float blur, int cull_backfaces, FaceRec* recs, uint2* bbox,
                                     float* zero_fv, float* zero_v) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.F; f += stride) {
@@ -1333,10 +1349,10 @@ extern "C" int pr_rast_prof_dump(void* dst, size_t bytes) {
 
 extern "C" size_t pr_rast_fwd_workspace_size(const PRRastArgs* a) {
   if (!a) return 0;
-  return (size_t)(a->F > 0 ? a->F : 1) * (sizeof(FaceRec) + sizeof(float4));  // records + compact boxes
+  return (size_t)(a->F > 0 ? a->F : 1) * (sizeof(FaceRec) + sizeof(uint2));  // records + fp16 cull boxes
 }
 
-static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const float4* fbox, hipStream_t st);
+static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2* fbox, hipStream_t st);
 
 extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "rast_fwd: null args");
@@ -1347,7 +1363,7 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
     return set_error(PR_ERR_WORKSPACE, "rast_fwd: workspace too small");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   FaceRec* fr = reinterpret_cast<FaceRec*>(a.workspace);
-  float4* fbox = reinterpret_cast<float4*>(fr + (a.F > 0 ? a.F : 1));
+  uint2* fbox = reinterpret_cast<uint2*>(fr + (a.F > 0 ? a.F : 1));
   if (a.F > 0) {
     const int nb = (int)std::min<int64_t>((a.F + kThreads - 1) / kThreads, 1024);
     face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr, fbox);
@@ -1356,7 +1372,7 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
   return rast_fwd_prepared(a, fr, fbox, st);
 }
 
-static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const float4* fbox, hipStream_t st) {
+static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2* fbox, hipStream_t st) {
   // face slices per pixel (tile 8x8 / 8x4 / 4x4): 4 measured fastest on the bench frame
   // with the two-stage face test (107 us vs 118-123 at 2 and 157 at 1); PR_RAST_SLICES=1|2|4
   // overrides (sweeps).  FRAG: barycentrics / distances written by the rasterizer itself
@@ -1470,7 +1486,7 @@ extern "C" int pr_project_rast_fwd(const PRProjectArgs* pa, const PRRastArgs* ra
     return set_error(PR_ERR_WORKSPACE, "rast_fwd: workspace too small");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   FaceRec* fr = reinterpret_cast<FaceRec*>(a.workspace);
-  float4* fbox = reinterpret_cast<float4*>(fr + (a.F > 0 ? a.F : 1));
+  uint2* fbox = reinterpret_cast<uint2*>(fr + (a.F > 0 ? a.F : 1));
   const int64_t work = std::max<int64_t>(std::max<int64_t>(a.F, a.grad_face_verts ? a.F * 9 : 0),
                                          pa->grad_verts ? pa->V * 3 : 0);
   if (work > 0) {
