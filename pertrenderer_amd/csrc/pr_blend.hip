@@ -68,7 +68,8 @@ struct Geo {
   int64_t P, PK;  // pixels, slots
   int K, KP1, PB, HW;
   int qK, rK, qK1, rK1, qS, rS;  // 256 / {K, K+1, Sa} and remainders
-  int ck;                        // contiguous per-lane chunk for 8-lane pixel phases: ceil((K+1)/8)
+  int lpp, lsh;                  // lanes per pixel in the pixel phases (256 / PB, 8..64) and log2
+  int ck;                        // contiguous per-lane chunk of the pixel phases: ceil((K+1)/lpp)
 };
 
 struct Sc {
@@ -391,7 +392,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   // ---- 2: per pixel (8 lanes): alpha, z_max, logits, largest logit, and the list of
   //         argmax candidates (ascending j)
   {
-    const int pl = tid >> 3, l = tid & 7;
+    const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
     const int j0 = l * g.ck, j1 = min(KP1, j0 + g.ck), k1 = min(K, j1);
     float al = 1.f, zm = kNegInf;
@@ -400,8 +401,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         al *= (1.f - A[pl * KP1 + k]);
         zm = fmaxf(zm, B[pl * KP1 + k]);
       }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
+    for (int m = 1; m < g.lpp; m <<= 1) {
       al *= __shfl_xor(al, m);
       zm = fmaxf(zm, __shfl_xor(zm, m));
     }
@@ -415,8 +415,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         CNT[pl * KP1 + j] = 0;
         zl = fmaxf(zl, z);
       }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) zl = fmaxf(zl, __shfl_xor(zl, m));
+    for (int m = 1; m < g.lpp; m <<= 1) zl = fmaxf(zl, __shfl_xor(zl, m));
     // candidates: finite logits not below zl - skipm (bounded Box-Muller noise only: a
     // logit further below the best can never win); lane chunks are contiguous, so an
     // exclusive scan of the lane counts gives each lane its output offset
@@ -430,9 +429,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         nc += (z > kNegInf && z >= zfloor) ? 1 : 0;
       }
     int off = 0, tot = 0;
-    const int lane8 = (tid & 63) & ~7;
-#pragma unroll
-    for (int o = 0; o < 8; ++o) {
+    const int lane8 = (tid & 63) & ~(g.lpp - 1);  // the pixel's first lane
+    for (int o = 0; o < g.lpp; ++o) {
       const int t = __shfl(nc, lane8 + o);
       off += o < l ? t : 0;
       tot += t;
@@ -507,11 +505,11 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   // ---- 4: outputs
   const float fSa = (float)p.Sa;
   if constexpr (CM != 0) {
-    // 8 lanes per pixel sweep the pixel's slots; only slots that won a sample are read
-    const int pl = tid >> 3, l = tid & 7;
+    // the pixel's lanes sweep its slots; only slots that won a sample are read
+    const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
     if (pl < npix) {
-      for (int k = l; k < K; k += 8) {
+      for (int k = l; k < K; k += g.lpp) {
         const int cw = CNT[pl * KP1 + k];
         if (cw == 0) continue;
         const float w = (float)cw / fSa;
@@ -522,8 +520,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         acc2 += w * c[2];
       }
     }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
+    for (int m = 1; m < g.lpp; m <<= 1) {
       acc0 += __shfl_xor(acc0, m);
       acc1 += __shfl_xor(acc1, m);
       acc2 += __shfl_xor(acc2, m);
@@ -661,7 +658,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   // ---- B2: per pixel (8 lanes, contiguous chunks): z_max + first argmax, exclusive
   //          products for the alpha gradient, logits, unperturbed argmax j0
   {
-    const int pl = tid >> 3, l = tid & 7;
+    const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
     const int j0c = l * g.ck, j1c = min(KP1, j0c + g.ck), k1c = min(K, j1c);
     float zm = kNegInf, tp = 1.f;
@@ -672,8 +669,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         if (zi > zm) { zm = zi; km = k; }
         tp *= (1.f - PR[pl * KP1 + k]);
       }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
+    for (int m = 1; m < g.lpp; m <<= 1) {
       const float oz = __shfl_xor(zm, m);
       const int ok = __shfl_xor(km, m);
       if (oz > zm || (oz == zm && ok < km)) { zm = oz; km = ok; }
@@ -683,9 +679,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     if constexpr (CM != 0) {
       // exclusive products across the 8 lane chunks, then within the chunk
       float pre = 1.f, suf = 1.f;
-      const int lane8 = (tid & 63) & ~7;
-#pragma unroll
-      for (int o = 0; o < 8; ++o) {
+      const int lane8 = (tid & 63) & ~(g.lpp - 1);  // the pixel's first lane
+      for (int o = 0; o < g.lpp; ++o) {
         const float t = __shfl(tp, lane8 + o);
         if (o < l) pre *= t;
         if (o > l) suf *= t;
@@ -708,8 +703,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         const float z = j < K ? gal * logf(PR[pl * KP1 + j]) + ZZ[pl * KP1 + j] - zmax : p.eps - zmax;
         if (z > zb || jb == (1 << 30)) { zb = z; jb = j; }
       }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
+    for (int m = 1; m < g.lpp; m <<= 1) {
       const float oz = __shfl_xor(zb, m);
       const int oj = __shfl_xor(jb, m);
       if (oj != (1 << 30) && (jb == (1 << 30) || oz > zb || (oz == zb && oj < jb))) { zb = oz; jb = oj; }
@@ -798,14 +792,13 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
 
   // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps
   {
-    const int pl = tid >> 3, l = tid & 7;
+    const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
     const int j0c = l * g.ck, k1c = min(K, j0c + g.ck);
     float s = 0.f;
     if (act)
       for (int k = j0c; k < k1c; ++k) s += ZZ[pl * KP1 + k];
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) s += __shfl_xor(s, m);
+    for (int m = 1; m < g.lpp; m <<= 1) s += __shfl_xor(s, m);
     if (act && l == 0) {
       float dzm = -s - ZZ[pl * KP1 + K];
       dzm = dzm * (PX[pl * 8 + 0] >= p.eps ? 1.f : 0.f);
@@ -1115,7 +1108,10 @@ Geo make_geo(const PRBlendParams& p, int PB) {
   g.qK = kThreads / g.K; g.rK = kThreads % g.K;
   g.qK1 = kThreads / g.KP1; g.rK1 = kThreads % g.KP1;
   g.qS = kThreads / p.Sa; g.rS = kThreads % p.Sa;
-  g.ck = (g.KP1 + 7) / 8;
+  // all 256 threads work in the pixel phases: 256 / PB lanes per pixel (one wave at most)
+  g.lpp = std::min(64, std::max(8, kThreads / PB));
+  g.lsh = 31 - __builtin_clz(g.lpp);
+  g.ck = (g.KP1 + g.lpp - 1) / g.lpp;
   return g;
 }
 
