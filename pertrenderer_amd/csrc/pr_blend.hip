@@ -1108,8 +1108,9 @@ Geo make_geo(const PRBlendParams& p, int PB) {
   g.qK = kThreads / g.K; g.rK = kThreads % g.K;
   g.qK1 = kThreads / g.KP1; g.rK1 = kThreads % g.KP1;
   g.qS = kThreads / p.Sa; g.rS = kThreads % p.Sa;
-  // all 256 threads work in the pixel phases: 256 / PB lanes per pixel (one wave at most)
-  g.lpp = std::min(64, std::max(8, kThreads / PB));
+  // lanes per pixel in the pixel phases: 8 (measured: 16 lanes for the backward's 16-pixel
+  // blocks made its pixel phase slower -- longer shuffle prefixes outweigh shorter chunks)
+  g.lpp = 8;
   g.lsh = 31 - __builtin_clz(g.lpp);
   g.ck = (g.KP1 + g.lpp - 1) / g.lpp;
   return g;
