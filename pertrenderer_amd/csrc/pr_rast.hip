@@ -463,9 +463,25 @@ PR_DEV int quad_rot(int v, int r) {
 // at once (independent chains).  The queue is an LDS column sorted by (z, face id),
 // PyTorch3D's order, and ends as the K smallest keys of all candidates: it depends
 // neither on SL nor on the traversal order.
+//
+// Tile order (ring = 1, square grids of even side): block b takes the b-th tile of the
+// Chebyshev rings around the image centre, so the tiles of a centred object -- the heavy
+// ones -- are dispatched first and the cheap empty border tiles fill the tail (row-major
+// order started the bottom quarter's heavy tiles only when the first tiles retired).
+PR_DEV void ring_tile(int b, int m, int& tx, int& ty) {
+  int r = (int)(__builtin_sqrtf((float)b) * 0.5f);
+  while (4 * (r + 1) * (r + 1) <= b) ++r;
+  while (4 * r * r > b) --r;
+  const int k = b - 4 * r * r, s = 2 * r + 2, c0 = m / 2 - r - 1;  // ring r: side s, corner (c0, c0)
+  if (k < s) { tx = c0 + k; ty = c0; }
+  else if (k < 2 * s - 2) { tx = c0 + s - 1; ty = c0 + 1 + (k - s); }
+  else if (k < 3 * s - 2) { tx = c0 + s - 1 - (k - (2 * s - 2)); ty = c0 + s - 1; }
+  else { tx = c0; ty = c0 + s - 2 - (k - (3 * s - 2)); }
+}
+
 template <int SL, bool PERSP, bool CLIP, bool FRAG>
 __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces,
-                                                      const uint2* __restrict__ fbox) {
+                                                      const uint2* __restrict__ fbox, int ring) {
   constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
   constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
   extern __shared__ float smem[];
@@ -482,7 +498,9 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
   float* lcs = reinterpret_cast<float*>(lcf + CH);                  // [CH] staged chunk suffix mins
   const int n = blockIdx.z;
   const int H = a.H, W = a.W;
-  const int row0 = blockIdx.y * TH, col0 = blockIdx.x * TW;
+  int tile_x = blockIdx.x, tile_y = blockIdx.y;
+  if (ring) ring_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x, tile_x, tile_y);
+  const int row0 = tile_y * TH, col0 = tile_x * TW;
   const int row = row0 + pix / TW, col = col0 + pix % TW;
   const bool inimg = row < H && col < W;
   const V2 p{ndc(W - 1 - min(col, W - 1), W, H), ndc(H - 1 - min(row, H - 1), H, W)};
@@ -842,7 +860,7 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
     const unsigned t = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     if (t < kProfTiles) {
       long long* rec = g_rast_prof + (size_t)t * 16;
-      rec[0] = blockIdx.x; rec[1] = blockIdx.y; rec[2] = blockIdx.z; rec[3] = nlist;
+      rec[0] = tile_x; rec[1] = tile_y; rec[2] = blockIdx.z; rec[3] = nlist;
       rec[4] = rt0; rec[5] = (long long)__builtin_amdgcn_s_memrealtime(); rec[6] = hw;
       for (int i = 0; i < 6; ++i) rec[7 + i] = stamp[i];
       rec[13] = SL;
@@ -858,8 +876,11 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb,
                         hipStream_t st) {
   constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW;
   dim3 grid((a.W + TW - 1) / TW, (a.H + TH - 1) / TH, a.N);
-  if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb);
-  else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb);
+  // centre-out tile order on square grids of even side (PR_RAST_ORDER=0: row-major)
+  static const bool ring_env = !getenv("PR_RAST_ORDER") || atoi(getenv("PR_RAST_ORDER")) != 0;
+  const int ring = ring_env && grid.x == grid.y && grid.x % 2 == 0;
+  if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring);
+  else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring);
 }
 
 template <bool PERSP, bool CLIP>
