@@ -70,7 +70,15 @@ struct Geo {
   int qK, rK, qK1, rK1, qS, rS;  // 256 / {K, K+1, Sa} and remainders
   int lpp, lsh;                  // lanes per pixel in the pixel phases (256 / PB, 8..64) and log2
   int ck;                        // contiguous per-lane chunk of the pixel phases: ceil((K+1)/lpp)
+  int bpi;                       // blocks per image for the centre-out block order (0: linear)
 };
+
+// pixel block of this workgroup: centre-out within each image when blocks tile images
+PR_DEV int64_t pixel_block(const Geo& g) {
+  if (g.bpi == 0) return blockIdx.x;
+  const int64_t n = blockIdx.x / g.bpi;
+  return n * g.bpi + centre_out((int)(blockIdx.x - n * g.bpi), g.bpi);
+}
 
 struct Sc {
   float sigma, gamma, alpha;
@@ -298,7 +306,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   int* PXI = reinterpret_cast<int*>(PX);
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
-  const int64_t pix0 = (int64_t)blockIdx.x * PB;
+  const int64_t blk = pixel_block(g), pix0 = blk * PB;
   const int npix = (int)min((int64_t)PB, g.P - pix0);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   if (tid == 0) *QN = 0;
@@ -565,7 +573,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   int* CP = reinterpret_cast<int*>(PX + PB * 8);        // [PB] valid-prefix count (K without pix_count)
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
-  const int64_t pix0 = (int64_t)blockIdx.x * PB;
+  const int64_t blk = pixel_block(g), pix0 = blk * PB;
   const int npix = (int)min((int64_t)PB, g.P - pix0);
   const int32_t* pcnt = a.pix_count;
   if (tid < npix) CP[tid] = pcnt ? pcnt[pix0 + tid] : K;
@@ -912,7 +920,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   }
   __syncthreads();
   if (tid < 4) {
-    partials[(int64_t)blockIdx.x * 4 + tid] = (RED[tid] + RED[4 + tid]) + (RED[8 + tid] + RED[12 + tid]);
+    partials[blk * 4 + tid] = (RED[tid] + RED[4 + tid]) + (RED[8 + tid] + RED[12 + tid]);
   }
 #ifdef PR_BLEND_PROFILE
   PR_BSTAMP(5);
@@ -1097,7 +1105,7 @@ void launch_bwd(const PRBlendBwdArgs& a, Geo geo, hipStream_t st, size_t lds, in
   else blend_bwd_kernel<NOISE, false, 0><<<nblk, kThreads, lds, st>>>(a, geo, part);
 }
 
-Geo make_geo(const PRBlendParams& p, int PB) {
+Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   Geo g;
   g.P = (int64_t)p.N * p.H * p.W;
   g.PK = g.P * p.K;
@@ -1113,6 +1121,9 @@ Geo make_geo(const PRBlendParams& p, int PB) {
   g.lpp = 8;
   g.lsh = 31 - __builtin_clz(g.lpp);
   g.ck = (g.KP1 + g.lpp - 1) / g.lpp;
+  // centre-out block order (PR_BLEND_ORDER bit 0: forward, bit 1: backward; 0 = linear)
+  static const int order = getenv("PR_BLEND_ORDER") ? atoi(getenv("PR_BLEND_ORDER")) : 1;
+  g.bpi = (order >> (bwd ? 1 : 0) & 1) && g.HW % PB == 0 ? g.HW / PB : 0;
   return g;
 }
 
@@ -1147,7 +1158,7 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
     return set_error(PR_ERR_ARG, "blend_fwd: missing buffer");
   const int KP1 = a.p.K + 1;
   const int PB = pick_pb(KP1, a.p.Sa, false);
-  const Geo geo = make_geo(a.p, PB);
+  const Geo geo = make_geo(a.p, PB, false);
   // slot chunks per (pixel, sample group) so that ~256 threads share the MC loop
   const int ng = ((a.p.sample_offset_a + a.p.Sa - 1) >> 2) - (a.p.sample_offset_a >> 2) + 1;
   int NC = 1;
@@ -1182,7 +1193,7 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
   if (!a.workspace || a.workspace_bytes < need) return set_error(PR_ERR_WORKSPACE, "blend_bwd: workspace too small");
   const int KP1 = a.p.K + 1;
   const int PB = pick_pb(KP1, a.p.Sa, true);
-  const Geo geo = make_geo(a.p, PB);
+  const Geo geo = make_geo(a.p, PB, true);
   const int64_t nblk = (geo.P + PB - 1) / PB;
   const size_t lds = bwd_lds(PB, KP1, a.p.Sa);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

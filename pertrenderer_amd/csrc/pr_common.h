@@ -82,6 +82,11 @@ PR_DEV U4 philox_block(uint64_t seed, uint32_t pixel, uint32_t slot, uint32_t gr
   return philox4x32_10(U4{pixel, slot, group, tag}, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// k-th index of [0, n) in centre-out order (n/2, n/2-1, n/2+1, ...): workgroups over
+// image rows are dispatched from the middle outwards, so the rows of a centred object
+// (the expensive ones) start first and the cheap border rows fill the tail.
+PR_DEV int centre_out(int k, int n) { return (k & 1) ? n / 2 - 1 - (k >> 1) : n / 2 + (k >> 1); }
+
 // --------------------------------------------------------------------- math
 PR_DEV float heaviside1(float x) { return x >= 0.f ? 1.f : 0.f; }  // torch.heaviside(x, 1)
 

@@ -876,8 +876,8 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb,
                         hipStream_t st) {
   constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW;
   dim3 grid((a.W + TW - 1) / TW, (a.H + TH - 1) / TH, a.N);
-  // centre-out tile order on square grids of even side (PR_RAST_ORDER=0: row-major)
-  static const bool ring_env = !getenv("PR_RAST_ORDER") || atoi(getenv("PR_RAST_ORDER")) != 0;
+  // centre-out tile order on square grids of even side (PR_RAST_ORDER bit 0; 0: row-major)
+  static const bool ring_env = (getenv("PR_RAST_ORDER") ? atoi(getenv("PR_RAST_ORDER")) : 3) & 1;
   const int ring = ring_env && grid.x == grid.y && grid.x % 2 == 0;
   if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring);
   else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring);
@@ -1076,7 +1076,7 @@ constexpr int kBwdFaces = 128;  // faces per tile reduced by the transpose; late
 // Faces past the first kBwdFaces of a tile, and hash overflow, add their slots straight
 // to global memory (correct, slower; dense meshes under large tiles only).
 template <int ROWS>
-__global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a) {
+__global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int order) {
   constexpr int tile_rows = ROWS, TP = kBwdTile * ROWS;  // tile pixels
   __shared__ int hkey[kHash];
   __shared__ int hfl[kHash];                      // tile-local face index of a hash entry
@@ -1089,7 +1089,8 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a) {
   __shared__ int pcnt[kBwdTile * ROWS];           // valid-prefix counts of the tile's pixels (or K)
   const int tid = threadIdx.x, lane = tid & 63;
   const int K = a.K, H = a.H, W = a.W;
-  const int n = blockIdx.z, row0 = blockIdx.y * tile_rows, col0 = blockIdx.x * kBwdTile;
+  const int n = blockIdx.z, col0 = blockIdx.x * kBwdTile;
+  const int row0 = (order ? centre_out(blockIdx.y, gridDim.y) : (int)blockIdx.y) * tile_rows;
   const int ncols = min(kBwdTile, W - col0), nrows = min(tile_rows, H - row0);
   const int per_row = ncols * K;
   const int total = nrows * per_row;
@@ -1434,10 +1435,12 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
   const char* er = getenv("PR_RAST_BWD_ROWS");
   const int rows = er && (atoi(er) == 1 || atoi(er) == 4 || atoi(er) == 8) ? atoi(er) : 2;
   dim3 grid((a.W + kBwdTile - 1) / kBwdTile, (a.H + rows - 1) / rows, a.N);
-  if (rows == 8) rast_bwd_kernel<8><<<grid, kBwdThreads, 0, st>>>(a);
-  else if (rows == 4) rast_bwd_kernel<4><<<grid, kBwdThreads, 0, st>>>(a);
-  else if (rows == 1) rast_bwd_kernel<1><<<grid, kBwdThreads, 0, st>>>(a);
-  else rast_bwd_kernel<2><<<grid, kBwdThreads, 0, st>>>(a);
+  // tile rows dispatched centre-out (PR_RAST_ORDER bit 1; 0: row-major)
+  static const int order = (getenv("PR_RAST_ORDER") ? atoi(getenv("PR_RAST_ORDER")) : 3) >> 1 & 1;
+  if (rows == 8) rast_bwd_kernel<8><<<grid, kBwdThreads, 0, st>>>(a, order);
+  else if (rows == 4) rast_bwd_kernel<4><<<grid, kBwdThreads, 0, st>>>(a, order);
+  else if (rows == 1) rast_bwd_kernel<1><<<grid, kBwdThreads, 0, st>>>(a, order);
+  else rast_bwd_kernel<2><<<grid, kBwdThreads, 0, st>>>(a, order);
   return check_launch("rast_bwd");
 }
 
