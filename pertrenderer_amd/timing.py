@@ -4,6 +4,12 @@ When a :class:`KernelTimer` is active (``with KernelTimer() as t``), every nativ
 launch site brackets its kernel with two events recorded on the SAME stream the
 kernel is enqueued on (torch's current stream of the tensors' device), so the
 elapsed time is the kernel's own duration on that stream.
+
+In an eager (uncaptured) pass the GPU is usually AHEAD of the host: it would reach the
+start event before the host has submitted the launch, and the interval would include
+host time (Python, argument packing).  ``lead_cycles`` enqueues a device-side spin
+(``torch.cuda._sleep``) before the start event, long enough for the host to submit the
+launch behind it, so start event -> kernels -> stop event run back to back on the GPU.
 """
 import collections
 
@@ -20,10 +26,11 @@ class KernelTimer:
     """external=True creates events that become record nodes when the launches are
     captured into a HIP graph; after a replay they time that replay's kernels."""
 
-    def __init__(self, external=False):
+    def __init__(self, external=False, lead_cycles=0):
         self._open = {}
         self.events = collections.defaultdict(list)
         self.external = external
+        self.lead_cycles = lead_cycles
 
     def __enter__(self):
         global _ACTIVE
@@ -36,6 +43,8 @@ class KernelTimer:
         return False
 
     def start(self, name):
+        if self.lead_cycles:
+            torch.cuda._sleep(self.lead_cycles)
         ev = torch.cuda.Event(enable_timing=True, external=self.external)
         ev.record(torch.cuda.current_stream())
         self._open[name] = ev

@@ -14,7 +14,7 @@ import os
 import sys
 
 # C-ABI call (bench.py's timed unit) -> the kernels it launches
-CALLS = {"rast_fwd": ["face_prep_kernel", "rast_fwd_kernel", "rast_frag_kernel"],
+CALLS = {"rast_fwd": ["face_prep_kernel", "project_prep_kernel", "rast_fwd_kernel", "rast_frag_kernel"],
          "rast_bwd": ["rast_bwd_kernel"],
          "blend_fwd": ["blend_fwd_kernel"],
          "blend_bwd": ["blend_bwd_kernel", "blend_finalize_kernel"],
