@@ -853,12 +853,14 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     const int n = image_of(n0, rem0, pl, g.HW);
     a.grad_zbuf[gs] = -((dzinv * mf) / (p.zfar[n] - p.znear[n]));
     const float prob = PR[pl * KP1 + k];
-    const float L = logf(prob);
+    // L and 1/prob feed only gradients (tolerance, not winners): hardware log2 / rcp
+    // (prob = count / Sr: never denormal; log2(1) = 0 and rcp(0) = inf exactly)
+    const float L = __builtin_amdgcn_logf(prob) * 0.693147180559945f;
     float dL = gal * dzk;
     if (dL != dL) dL = 0.f;
     const float lp = __builtin_isinf(L) ? 0.f : L * dzk;
     if (lp == lp) part_gal += lp;
-    float r = 1.f / prob;
+    float r = __builtin_amdgcn_rcpf(prob);
     if (__builtin_isinf(r)) r = 0.f;
     float dprob = r * dL;
     const float4 gi = gik[u];
