@@ -938,7 +938,21 @@ __global__ void __launch_bounds__(kThreads) blend_finalize_kernel(const float* p
   const int tid = threadIdx.x;
   const Sc sc = resolve(p);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int b = tid; b < nblk; b += kThreads) {
+  // blocks b, b+256, ... in order; four blocks' loads in flight per step (the latency chain
+  // of one load per step made this kernel ~6 us)
+  int b = tid;
+  for (; b + 3 * kThreads < nblk; b += 4 * kThreads) {
+    float v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[u][c] = partials[(int64_t)(b + u * kThreads) * 4 + c];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] += v[u][c];
+  }
+  for (; b < nblk; b += kThreads) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[c] += partials[(int64_t)b * 4 + c];
   }
