@@ -1087,14 +1087,12 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int
   __shared__ int ccount, nface;
   __shared__ float pxs[kBwdTile], pys[ROWS];
   __shared__ int pcnt[kBwdTile * ROWS];           // valid-prefix counts of the tile's pixels (or K)
+  __shared__ int pstart[kBwdTile * ROWS + 1];     // exclusive prefix sum of pcnt
   const int tid = threadIdx.x, lane = tid & 63;
   const int K = a.K, H = a.H, W = a.W;
   const int n = blockIdx.z, col0 = blockIdx.x * kBwdTile;
   const int row0 = (order ? centre_out(blockIdx.y, gridDim.y) : (int)blockIdx.y) * tile_rows;
   const int ncols = min(kBwdTile, W - col0), nrows = min(tile_rows, H - row0);
-  const int per_row = ncols * K;
-  const int total = nrows * per_row;
-  const float inv_row = 1.f / (float)per_row, inv_k = 1.f / (float)K;
   const int64_t tile_o = (((int64_t)n * H + row0) * W + col0) * K;  // slot offset of the tile's first row
   const int64_t row_stride = (int64_t)W * K;
   for (int i = tid; i < kHash; i += kBwdThreads) hkey[i] = -1;
@@ -1106,6 +1104,16 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int
     const int r = tid / kBwdTile, c = tid - r * kBwdTile;
     pcnt[tid] = (r < nrows && c < ncols) ? (a.pix_count ? a.pix_count[((int64_t)n * H + row0 + r) * W + col0 + c] : K) : 0;
   }
+  __syncthreads();
+  if (tid == 0) {
+    int acc_s = 0;
+    for (int q = 0; q < TP; ++q) { pstart[q] = acc_s; acc_s += pcnt[q]; }
+    pstart[TP] = acc_s;
+  }
+  __syncthreads();
+  // the rounds walk the tile's valid-prefix slots only (pixel q's slots 0..pcnt[q]-1 are
+  // entries pstart[q].. of the walk): a tile with <= kBwdEnt valid slots is one round
+  const int total = pstart[TP];
   float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // owner lane tid < kBwdFaces
   for (int c0 = 0; c0 < total; c0 += kBwdEnt) {
     if (tid == 0) ccount = 0;
@@ -1119,11 +1127,13 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int
       f[u] = -1;
       pk[u] = 0;
       if (i < total) {
-        int rem, k;
-        const int r = divmod_small(i, per_row, inv_row, rem);
-        const int c = divmod_small(rem, K, inv_k, k);
-        pk[u] = ((r * kBwdTile + c) << 16) | k;
-        if (k < pcnt[r * kBwdTile + c]) f[u] = a.pix_to_face[tile_o + r * row_stride + rem];
+        int q = 0;  // the pixel: last q with pstart[q] <= i (binary search over TP entries)
+#pragma unroll
+        for (int step = TP / 2; step > 0; step >>= 1)
+          if (pstart[q + step] <= i) q += step;
+        const int k = i - pstart[q], r = q / kBwdTile, c = q - r * kBwdTile;
+        pk[u] = (q << 16) | k;
+        f[u] = a.pix_to_face[tile_o + r * row_stride + c * K + k];
       }
     }
 #pragma unroll
