@@ -1054,7 +1054,10 @@ PR_DEV void slot_grad(const PRRastArgs& a, V2 p, const float* v, int64_t o, floa
 constexpr int kHash = 512;      // LDS hash entries per workgroup (distinct faces of one tile)
 constexpr int kBwdTile = 8;     // tile width; rows per tile (<= 8) chosen at launch
 constexpr int kBwdThreads = 256;
-constexpr int kBwdEnt = 512;    // slots scanned (and at most valid) per round: 2 per thread
+#ifndef PR_BWD_ENT  // sweeps: -DPR_BWD_ENT=256 / 1024 measured 46.8 / 77 us vs 44 us at 512
+#define PR_BWD_ENT 512
+#endif
+constexpr int kBwdEnt = PR_BWD_ENT;  // slots scanned (and at most valid) per round: 2 per thread
 constexpr int kBwdFaces = 128;  // faces per tile reduced by the transpose; later ones use global atomics
 
 // One 256-thread workgroup per 8 x tile_rows pixel tile (tile_rows <= 8), rounds of
