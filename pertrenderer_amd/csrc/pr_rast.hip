@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
   const int n = blockIdx.z;
   const int H = a.H, W = a.W;
   int tile_x = blockIdx.x, tile_y = blockIdx.y;
-  if (ring) ring_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x, tile_x, tile_y);
+  if (ring & 1) ring_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x, tile_x, tile_y);
   const int row0 = tile_y * TH, col0 = tile_x * TW;
   const int row = row0 + pix / TW, col = col0 + pix % TW;
   const bool inimg = row < H && col < W;
@@ -556,6 +556,11 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
     nlist += nl;
 #endif
     if (nl == 0) continue;
+    if (ring & 2) {  // critical-path priority: the tiles with the longest face lists bound the kernel
+      if (nl >= 72) __builtin_amdgcn_s_setprio(3);
+      else if (nl >= 56) __builtin_amdgcn_s_setprio(2);
+      else if (nl >= 40) __builtin_amdgcn_s_setprio(1);
+    }
     bool done = !inimg;  // the early exit below is only valid inside one sorted round
     // ---- sort key: the face plane's depth at the tile centre, clamped to the face's
     //      z range (an ordering heuristic only: it makes the per-pixel inserts mostly
@@ -878,7 +883,9 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb,
   dim3 grid((a.W + TW - 1) / TW, (a.H + TH - 1) / TH, a.N);
   // centre-out tile order on square grids of even side (PR_RAST_ORDER bit 0; 0: row-major)
   static const bool ring_env = (getenv("PR_RAST_ORDER") ? atoi(getenv("PR_RAST_ORDER")) : 3) & 1;
-  const int ring = ring_env && grid.x == grid.y && grid.x % 2 == 0;
+  // wave priority raised for long face lists (PR_RAST_PRIO=0: off)
+  static const bool prio_env = getenv("PR_RAST_PRIO") ? atoi(getenv("PR_RAST_PRIO")) != 0 : true;
+  const int ring = (ring_env && grid.x == grid.y && grid.x % 2 == 0 ? 1 : 0) | (prio_env ? 2 : 0);
   if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring);
   else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring);
 }
