@@ -1,0 +1,46 @@
+"""Host-side profile of the eager bench step (eval.py's execution mode): cProfile over N
+steps, top functions by own time and by cumulative time.
+
+    python tools/eager_host_prof.py [steps]
+"""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import pertrenderer_amd as pa  # noqa: E402
+
+
+def main():
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    dev = torch.device("cuda:0")
+    pa.native_library()
+    wl = bench.Workload(dev)
+    step = bench.build_step(wl, 1, "eager", dev)
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    print(f"eager: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/step")
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    pr.disable()
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(25)
+    st.sort_stats("cumulative").print_stats(40)
+
+
+if __name__ == "__main__":
+    main()
