@@ -764,6 +764,9 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   {
     const int ng = agg_num_groups(p), g0 = agg_first_group(p);
     const bool cauchy = p.flags & PR_BLEND_AGG_CAUCHY;
+    // the reference divides each sample's a_s * score by gamma (smoothagg.py:52); one
+    // reciprocal here instead of an IEEE division per (slot, sample): within 1 ulp
+    const float inv_gamma = 1.f / sc.gamma;
     PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
       const int j = k;
       const int64_t gp = pix0 + pl;
@@ -786,7 +789,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         for (int r = 0; r < 4; ++r) {
           if (av[r] != 0.f) {
             const float scr = noise_score(e[r], cauchy);
-            dz += (av[r] * scr) / sc.gamma;
+            dz += (av[r] * scr) * inv_gamma;
             q += av[r] * (e[r] * scr);
           }
         }
@@ -851,7 +854,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     const float dzk = ZZ[pl * KP1 + k];
     const float dzinv = dzk + (k == (int)PX[pl * 8 + 2] ? PX[pl * 8 + 4] : 0.f);
     const int n = image_of(n0, rem0, pl, g.HW);
-    a.grad_zbuf[gs] = -((dzinv * mf) / (p.zfar[n] - p.znear[n]));
+    // gradient only: hardware reciprocal of (zfar - znear) instead of an IEEE division
+    a.grad_zbuf[gs] = -((dzinv * mf) * __builtin_amdgcn_rcpf(p.zfar[n] - p.znear[n]));
     const float prob = PR[pl * KP1 + k];
     // L and 1/prob feed only gradients (tolerance, not winners): hardware log2 / rcp
     // (prob = count / Sr: never denormal; log2(1) = 0 and rcp(0) = inf exactly)
