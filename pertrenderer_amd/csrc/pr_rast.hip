@@ -323,7 +323,7 @@ __device__ long long g_rast_prof[kProfTiles * 16];  // per tile: x y z list t0 t
 template <int SL> struct RastCfg {
   static constexpr int CAP = SL == 1 ? 512 : (SL == 2 ? 256 : 128);
   static constexpr int G = SL == 1 ? 4 : 2;
-  static constexpr int CH = SL == 4 ? 32 : 64;
+  static constexpr int CH = SL >= 4 ? 32 : 64;
   static_assert(CAP <= 8 * 64, "suffix-min pass holds CAP / 64 <= 8 entries per lane");
 };
 constexpr int kCullU = 16;   // 64-face cull chunks whose boxes are in flight together
@@ -410,7 +410,8 @@ size_t rast_fwd_lds_sl(int K) {
 }
 
 size_t rast_fwd_lds(int K, int SL) {
-  return SL == 4 ? rast_fwd_lds_sl<4>(K) : (SL == 2 ? rast_fwd_lds_sl<2>(K) : rast_fwd_lds_sl<1>(K));
+  return SL == 8 ? rast_fwd_lds_sl<8>(K)
+                 : SL == 4 ? rast_fwd_lds_sl<4>(K) : (SL == 2 ? rast_fwd_lds_sl<2>(K) : rast_fwd_lds_sl<1>(K));
 }
 
 // v from the lane of the same pixel that holds slice s (lane = pixel * SL + slice):
@@ -424,6 +425,8 @@ PR_DEV int from_slice(int v, int s) {
       case 0: return __builtin_amdgcn_update_dpp(0, v, 0xA0, 0xf, 0xf, false);  // quad_perm [0,0,2,2]
       default: return __builtin_amdgcn_update_dpp(0, v, 0xF5, 0xf, 0xf, false); // quad_perm [1,1,3,3]
     }
+  } else if constexpr (SL == 8) {  // beyond a DPP quad: a lane permute
+    return __shfl(v, (int)(__lane_id() & ~7u) | s);
   } else {
     switch (s) {
       case 0: return __builtin_amdgcn_update_dpp(0, v, 0x00, 0xf, 0xf, false);  // quad_perm [0,0,0,0]
@@ -440,6 +443,9 @@ template <int SL>
 PR_DEV int quad_rot(int v, int r) {
   if constexpr (SL == 2) {
     return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (SL == 8) {
+    const unsigned l = __lane_id();
+    return __shfl(v, (int)((l & ~7u) | ((l + (unsigned)r) & 7u)));
   } else {
     switch (r) {
       case 1: return __builtin_amdgcn_update_dpp(0, v, 0x39, 0xf, 0xf, false);  // quad_perm [1,2,3,0]
@@ -482,7 +488,7 @@ PR_DEV void ring_tile(int b, int m, int& tx, int& ty) {
 template <int SL, bool PERSP, bool CLIP, bool FRAG>
 __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces,
                                                       const uint2* __restrict__ fbox, int ring) {
-  constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
+  constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
   constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
   extern __shared__ float smem[];
   const int K = a.K;
@@ -499,7 +505,15 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
   const int n = blockIdx.z;
   const int H = a.H, W = a.W;
   int tile_x = blockIdx.x, tile_y = blockIdx.y;
-  if (ring & 1) ring_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x, tile_x, tile_y);
+  if (ring & 1) {
+    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+    if (gridDim.y == gridDim.x) {
+      ring_tile(b, gridDim.x, tile_x, tile_y);
+    } else {  // gridDim.y == 2 gridDim.x: rings over 1x2 super-tiles
+      ring_tile(b >> 1, gridDim.x, tile_x, tile_y);
+      tile_y = 2 * tile_y + (b & 1);
+    }
+  }
   const int row0 = tile_y * TH, col0 = tile_x * TW;
   const int row = row0 + pix / TW, col = col0 + pix % TW;
   const bool inimg = row < H && col < W;
@@ -879,13 +893,14 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
 template <int SL, bool PERSP, bool CLIP>
 void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, bool frag, size_t lds,
                         hipStream_t st) {
-  constexpr int TW = SL == 4 ? 4 : 8, TH = 64 / SL / TW;
+  constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW;
   dim3 grid((a.W + TW - 1) / TW, (a.H + TH - 1) / TH, a.N);
   // centre-out tile order on square grids of even side (PR_RAST_ORDER bit 0; 0: row-major)
   static const bool ring_env = (getenv("PR_RAST_ORDER") ? atoi(getenv("PR_RAST_ORDER")) : 3) & 1;
   // wave priority raised for long face lists (PR_RAST_PRIO=0: off)
   static const bool prio_env = getenv("PR_RAST_PRIO") ? atoi(getenv("PR_RAST_PRIO")) != 0 : true;
-  const int ring = (ring_env && grid.x == grid.y && grid.x % 2 == 0 ? 1 : 0) | (prio_env ? 2 : 0);
+  const bool sq = grid.x % 2 == 0 && (grid.y == grid.x || grid.y == 2 * grid.x);
+  const int ring = (ring_env && sq ? 1 : 0) | (prio_env ? 2 : 0);
   if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring);
   else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring);
 }
@@ -893,7 +908,8 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb,
 template <bool PERSP, bool CLIP>
 void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, int sl, bool frag, size_t lds,
                         hipStream_t st) {
-  if (sl == 4) launch_rast_fwd_sl<4, PERSP, CLIP>(a, fr, fb, frag, lds, st);
+  if (sl == 8) launch_rast_fwd_sl<8, PERSP, CLIP>(a, fr, fb, frag, lds, st);
+  else if (sl == 4) launch_rast_fwd_sl<4, PERSP, CLIP>(a, fr, fb, frag, lds, st);
   else if (sl == 2) launch_rast_fwd_sl<2, PERSP, CLIP>(a, fr, fb, frag, lds, st);
   else launch_rast_fwd_sl<1, PERSP, CLIP>(a, fr, fb, frag, lds, st);
 }
@@ -1422,7 +1438,7 @@ static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2
   int sl = 4;
   if (const char* e = getenv("PR_RAST_SLICES")) {
     const int v = atoi(e);
-    if (v == 1 || v == 2 || v == 4) sl = v;
+    if (v == 1 || v == 2 || v == 4 || v == 8) sl = v;
   }
   bool frag = true;
   if (const char* e = getenv("PR_RAST_FRAG")) frag = atoi(e) != 0;
