@@ -571,9 +571,10 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
 #endif
     if (nl == 0) continue;
     if (ring & 2) {  // critical-path priority: the tiles with the longest face lists bound the kernel
-      if (nl >= 72) __builtin_amdgcn_s_setprio(3);
-      else if (nl >= 56) __builtin_amdgcn_s_setprio(2);
-      else if (nl >= 40) __builtin_amdgcn_s_setprio(1);
+      const int t = ring >> 8;  // levels at t, t + 16, t + 32 faces
+      if (nl >= t + 32) __builtin_amdgcn_s_setprio(3);
+      else if (nl >= t + 16) __builtin_amdgcn_s_setprio(2);
+      else if (nl >= t) __builtin_amdgcn_s_setprio(1);
     }
     bool done = !inimg;  // the early exit below is only valid inside one sorted round
     // ---- sort key: the face plane's depth at the tile centre, clamped to the face's
@@ -899,8 +900,9 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb,
   static const bool ring_env = (getenv("PR_RAST_ORDER") ? atoi(getenv("PR_RAST_ORDER")) : 3) & 1;
   // wave priority raised for long face lists (PR_RAST_PRIO=0: off)
   static const bool prio_env = getenv("PR_RAST_PRIO") ? atoi(getenv("PR_RAST_PRIO")) != 0 : true;
+  static const int prio_t = getenv("PR_RAST_PRIO_T") ? atoi(getenv("PR_RAST_PRIO_T")) & 255 : 40;
   const bool sq = grid.x % 2 == 0 && (grid.y == grid.x || grid.y == 2 * grid.x);
-  const int ring = (ring_env && sq ? 1 : 0) | (prio_env ? 2 : 0);
+  const int ring = (ring_env && sq ? 1 : 0) | (prio_env ? 2 : 0) | (prio_t << 8);
   if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring);
   else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring);
 }
