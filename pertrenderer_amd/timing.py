@@ -57,10 +57,18 @@ class KernelTimer:
     def reset(self):
         self.events.clear()
 
-    def summary(self):
-        """{name: (launches, mean ms)} — call after torch.cuda.synchronize()."""
+    def summary(self, stat="mean"):
+        """{name: (launches, ms)} with ms the mean or the median over launches — call after
+        torch.cuda.synchronize()."""
         out = {}
         for name, pairs in self.events.items():
-            ms = [a.elapsed_time(b) for a, b in pairs]
-            out[name] = (len(ms), sum(ms) / max(1, len(ms)))
+            ms = sorted(a.elapsed_time(b) for a, b in pairs)
+            if not ms:
+                continue
+            if stat == "median":
+                m = len(ms) // 2
+                v = ms[m] if len(ms) % 2 else 0.5 * (ms[m - 1] + ms[m])
+            else:
+                v = sum(ms) / len(ms)
+            out[name] = (len(ms), v)
         return out
