@@ -402,6 +402,9 @@ def main():
         tr = json.load(open(pmc)).get(dom)
         if tr:
             roof["traffic"] = tr.get("bytes_per_launch")
+            if tr.get("valu_issue_us"):  # the bound that applies: VALU issue
+                roof["valu_issue_us"] = tr["valu_issue_us"]
+                roof["valu_frac"] = round(tr["valu_issue_us"] / (1e3 * d["ms"]), 4)
 
     B, Hs, K, S = cfg["batch"], cfg["image_size"], cfg["K"], cfg["samples"]
     frames = args.steps * world * B

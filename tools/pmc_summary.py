@@ -46,16 +46,21 @@ def traffic(res):
     """Per C-ABI call: summed HBM bytes per launch of its kernels."""
     tr = {}
     for call, kernels in CALLS.items():
-        rd = wr = 0.0
+        rd = wr = valu = 0.0
         found = []
         for k, c in res.items():
             if k.split("<")[0] in kernels and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
                 rd += 2.0 * c["FETCH_SIZE"] * 1024
                 wr += c["WRITE_SIZE"] * 1024
+                valu += c.get("SQ_INSTS_VALU", 0.0)
                 found.append(k)
         if found:
             tr[call] = {"bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
-                        "kernels": found, "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes"}
+                        "kernels": found, "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes",
+                        # VALU issue time if the instructions were spread evenly: wave64 VALU
+                        # op = 4 cycles on a SIMD, 1024 SIMDs, 2.4 GHz
+                        "valu_insts_per_launch": int(valu),
+                        "valu_issue_us": round(valu * 4 / (1024 * 2.4e3), 2)}
     return tr
 
 
