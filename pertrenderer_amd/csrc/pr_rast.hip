@@ -323,7 +323,10 @@ __device__ long long g_rast_prof[kProfTiles * 16];  // per tile: x y z list t0 t
 template <int SL> struct RastCfg {
   static constexpr int CAP = SL == 1 ? 512 : (SL == 2 ? 256 : 128);
   static constexpr int G = SL == 1 ? 4 : 2;
-  static constexpr int CH = SL >= 4 ? 32 : 64;
+#ifndef PR_RAST_CH4  // sweeps: 16 measured equal (84 vs 86 us, noise)
+#define PR_RAST_CH4 32
+#endif
+  static constexpr int CH = SL >= 4 ? PR_RAST_CH4 : 64;
   static_assert(CAP <= 8 * 64, "suffix-min pass holds CAP / 64 <= 8 entries per lane");
 };
 constexpr int kCullU = 16;   // 64-face cull chunks whose boxes are in flight together
@@ -485,8 +488,11 @@ PR_DEV void ring_tile(int b, int m, int& tx, int& ty) {
   else { tx = c0; ty = c0 + s - 2 - (k - (3 * s - 2)); }
 }
 
+#ifndef PR_RAST_WPE  // sweeps: 4 waves/SIMD (with PR_RAST_CH4=16: 128 VGPRs, 2 spills) measured equal
+#define PR_RAST_WPE 1
+#endif
 template <int SL, bool PERSP, bool CLIP, bool FRAG>
-__global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces,
+__global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces,
                                                       const uint2* __restrict__ fbox, int ring) {
   constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
   constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
@@ -542,18 +548,19 @@ __global__ void __launch_bounds__(64) rast_fwd_kernel(PRRastArgs a, const FaceRe
     //      chunk that would overflow the round's list starts the next round
     int nl = 0;
     while (base < fe && nl <= kCap - 64) {
-      float4 bb[kCullU];
+      uint2 pb[kCullU];  // packed fp16 boxes: half the registers of unpacked ones
 #pragma unroll
       for (int u = 0; u < kCullU; ++u) {
         const int64_t f = base + u * 64 + lane;
-        bb[u] = unpack_box(fbox[f < fe ? f : fe - 1]);
+        pb[u] = fbox[f < fe ? f : fe - 1];
       }
       int64_t next = base + 64 * kCullU;
       bool stop = false;  // wave-uniform; no break, so bb[] stays in registers
 #pragma unroll
       for (int u = 0; u < kCullU; ++u) {
         const int64_t f = base + u * 64 + lane;
-        const bool keep = f < fe && !(bb[u].x > txmax || bb[u].y < txmin || bb[u].z > tymax || bb[u].w < tymin);
+        const float4 bb = unpack_box(pb[u]);
+        const bool keep = f < fe && !(bb.x > txmax || bb.y < txmin || bb.z > tymax || bb.w < tymin);
         const uint64_t bal = __ballot(keep);
         const int cnt = __popcll(bal);
         if (!stop && nl + cnt > kCap) { stop = true; next = base + u * 64; }
