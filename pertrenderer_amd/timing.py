@@ -43,7 +43,7 @@ class KernelTimer:
         return False
 
     def start(self, name):
-        if self.lead_cycles:
+        if self.lead_cycles and hasattr(torch.cuda, "_sleep"):
             torch.cuda._sleep(self.lead_cycles)
         ev = torch.cuda.Event(enable_timing=True, external=self.external)
         ev.record(torch.cuda.current_stream())
