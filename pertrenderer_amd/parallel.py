@@ -55,3 +55,98 @@ def average_gradients(params, group=None, weight=None):
         n = g.numel()
         g.copy_(flat[off:off + n].reshape(g.shape).to(g.device, g.dtype))
         off += n
+
+
+# ------------------------------------------------------ exact sample-sharded mode
+# SURVEY.md §8(e) "exact mode": every rank renders the same frame with its shard of the
+# Monte-Carlo samples, and the collectives make the result the full-S estimator (the same
+# values as one GPU up to fp summation order), not an average of per-rank estimators:
+#   forward : all-reduce of the rast probabilities P (counts) and of the agg weights W;
+#   backward: all-reduce of dL/dP (the agg shards' contributions) and of dL/d dists and
+#             dL/d zbuf; the smoothing scalars' gradients are per-rank partial sums
+#             (reduce_scalar_grads).
+# Built from the standalone native ops (perturbed_heaviside / perturbed_aggregate), the
+# colour blend in torch: it serves the large-S configurations, where the messages
+# (N,H,W,K) are small against the per-rank RNG work.
+
+def _all_reduce_sum(t, group):
+    """In-place SUM all-reduce; gloo reduces CUDA tensors through a host copy."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        c = t.detach().cpu()
+        dist.all_reduce(c, group=group)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, group=group)
+    return t
+
+
+class _SumForward(torch.autograd.Function):
+    """y = sum over ranks of weight_r * x_r.  The gradient arriving at y is the same on
+    every rank, so x_r's gradient is weight_r * dy (no collective)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, group):
+        ctx.weight = weight
+        return _all_reduce_sum(x.detach() * weight, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g * ctx.weight, None, None
+
+
+class _SumBackward(torch.autograd.Function):
+    """Identity forward; the backward sums the rank-local gradients (each rank's shard
+    contributes its own part of dL/dx)."""
+
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _all_reduce_sum(g.detach().clone(memory_format=torch.contiguous_format), ctx.group), None
+
+
+def exact_sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_samples_rast, nb_samples_agg,
+                        seed_r, seed_a, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0, zfar=100.0,
+                        group=None):
+    """smooth_rgb_blend (random_rasterizer.py:34-56) with GaussianRast / GaussianAgg over
+    `nb_samples_*` GLOBAL samples split across the ranks of `group` (sample_shard): the
+    image and the gradients of colors, dists and zbuf equal the single-process full-S
+    result up to fp summation order (P and W are exact: counts).  Call reduce_scalar_grads
+    after backward for sigma / gamma / alpha."""
+    from .blend import perturbed_aggregate, perturbed_heaviside
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    off_r, n_r = sample_shard(nb_samples_rast, rank, world)
+    off_a, n_a = sample_shard(nb_samples_agg, rank, world)
+    if n_r == 0 or n_a == 0:
+        raise ValueError(f"exact sharding needs >= 1 sample per rank (Sr={nb_samples_rast}, "
+                         f"Sa={nb_samples_agg}, world={world})")
+    K = dists.shape[-1]
+    mask = pix_to_face >= 0
+    d_in = _SumBackward.apply(dists, group)
+    z_in = _SumBackward.apply(zbuf, group)
+    P_r = perturbed_heaviside(d_in, sigma, n_r, noise=Noise.philox(seed_r=seed_r, offset_r=off_r))
+    P = _SumForward.apply(P_r * mask, n_r / nb_samples_rast, group)  # smooth_rgb_blend :47
+    P_in = _SumBackward.apply(P, group)
+    W_r = perturbed_aggregate(z_in, zfar, znear, P_in, mask, gamma, alpha, n_a, eps=eps,
+                              noise=Noise.philox(seed_a=seed_a, offset_a=off_a))
+    W = _SumForward.apply(W_r, n_a / nb_samples_agg, group)
+    bg = torch.as_tensor(background, dtype=colors.dtype, device=colors.device)
+    rgb = (W[..., :K, None] * colors).sum(dim=-2) + W[..., K:K + 1] * bg  # :50-53
+    a = 1.0 - torch.prod(1.0 - P, dim=-1, keepdim=True)  # :48, :54
+    return torch.cat([rgb, a], dim=-1)
+
+
+def reduce_scalar_grads(params, group=None):
+    """Exact mode: the smoothing scalars' gradients are per-rank partial sums over the
+    sample shards; one SUM all-reduce completes them."""
+    grads = [p.grad for p in params if p is not None and p.grad is not None]
+    if not grads:
+        return
+    flat = torch.stack([g.detach().reshape(()).to(torch.float32) for g in grads])
+    _all_reduce_sum(flat, group)
+    for g, v in zip(grads, flat):
+        g.copy_(v.to(g.dtype))

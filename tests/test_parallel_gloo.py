@@ -1,6 +1,7 @@
 """Multi-process (gloo, world size 2, CPU) tests of the data-parallel logic:
-shard arithmetic, the single flattened gradient all-reduce, and that Monte-Carlo
-sample shards recombine exactly (counts are additive) using the CPU oracle."""
+shard arithmetic, the single flattened gradient all-reduce, that Monte-Carlo
+sample shards recombine exactly (counts are additive) using the CPU oracle, and the
+exact mode's collective autograd pair."""
 import os
 import socket
 
@@ -68,7 +69,19 @@ def _worker(rank, world, port, q):
         dist.all_gather(allk, keys)
         ok3 = (nr.offset_r == 8 * rank and na.offset_a == 8 * rank and all(torch.equal(k, allk[0]) for k in allk))
         nz.set_sample_shard(0)
-        q.put((rank, bool(ok1), bool(ok2 and ok3)))
+        # 4) exact mode's collective autograd pair (parallel.exact_sharded_blend): a
+        #    rank-specific shard function between _SumBackward and _SumForward gives the
+        #    full function's value and gradient on every rank
+        from pertrenderer_amd.parallel import _SumBackward, _SumForward
+        x = torch.tensor([0.3, -0.7, 1.1], requires_grad=True)
+        c = torch.tensor([1.0, 2.0, 3.0])
+        P = _SumForward.apply(_SumBackward.apply(x, None) ** (rank + 2), 0.5, None)
+        (torch.sin(P) * c).sum().backward()
+        xr = x.detach()
+        P_ref = 0.5 * (xr ** 2 + xr ** 3)
+        g_ref = torch.cos(P_ref) * c * 0.5 * (2 * xr + 3 * xr ** 2)
+        ok4 = torch.allclose(P.detach(), P_ref, atol=1e-6) and torch.allclose(x.grad, g_ref, atol=1e-6)
+        q.put((rank, bool(ok1), bool(ok2 and ok3 and ok4)))
     finally:
         dist.destroy_process_group()
 
