@@ -344,9 +344,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PR_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks on fewer GPUs
+    # (rank -> GPU local % device_count); the measured configuration is nccl (RCCL)
+    backend = os.environ.get("PR_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     torch.manual_seed(1234)  # same Philox keys on every rank ...
