@@ -1140,7 +1140,12 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   g.qS = kThreads / p.Sa; g.rS = kThreads % p.Sa;
   // lanes per pixel in the pixel phases: 8 (measured: 16 lanes for the backward's 16-pixel
   // blocks made its pixel phase slower -- longer shuffle prefixes outweigh shorter chunks)
-  g.lpp = 8;
+  // PR_BLEND_LPP=16|32|64 (sweeps; capped at 256 / PB so every pixel keeps its lanes):
+  // 8 / 16 / 32 measured within 1 % at cfg2 and cfg3
+  static const int lpp_env = getenv("PR_BLEND_LPP") ? atoi(getenv("PR_BLEND_LPP")) : 8;
+  int lpp = (lpp_env == 16 || lpp_env == 32 || lpp_env == 64) ? lpp_env : 8;
+  while (lpp > 8 && lpp * PB > kThreads) lpp >>= 1;
+  g.lpp = lpp;
   g.lsh = 31 - __builtin_clz(g.lpp);
   g.ck = (g.KP1 + g.lpp - 1) / g.lpp;
   // centre-out block order (PR_BLEND_ORDER bit 0: forward, bit 1: backward; 0 = linear)
