@@ -11,9 +11,11 @@
 // share one K-queue per pixel in LDS, sorted by (z, face id) -- PyTorch3D's ordering.  The
 // output pass writes p2f/zbuf, the winners' barycentrics / distances and the per-pixel
 // valid-prefix counts.  MeshRasterizer's projection can run in the same face pass
-// (pr_project_rast_fwd).
+// (pr_project_rast_fwd).  Scheduling: tiles are dispatched centre-out (Chebyshev rings)
+// so a centred object's heavy tiles start first, and waves with long face lists raise
+// their priority (the kernel's span is its heaviest tiles).
 //
-// Backward: per tile, the valid slots are compacted, each face gets a tile-local index,
+// Backward: per tile, the valid-prefix slots are compacted, each face gets a tile-local index,
 // the per-slot gradients go to LDS without atomics and are summed per face by a
 // face x pixel transpose; one global atomic per (face, component) per tile.
 #include <cstdlib>
