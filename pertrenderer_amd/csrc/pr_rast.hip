@@ -324,14 +324,20 @@ __device__ long long g_rast_prof[kProfTiles * 16];  // per tile: x y z list t0 t
 // (LDS, VGPRs) rather than per-wave ILP.
 template <int SL> struct RastCfg {
   static constexpr int CAP = SL == 1 ? 512 : (SL == 2 ? 256 : 128);
-  static constexpr int G = SL == 1 ? 4 : 2;
+#ifndef PR_RAST_G4  // sweeps: 3 / 4 faces per lane measured equal or slower
+#define PR_RAST_G4 2
+#endif
+  static constexpr int G = SL == 1 ? 4 : (SL >= 4 ? PR_RAST_G4 : 2);
 #ifndef PR_RAST_CH4  // sweeps: 16 measured equal (84 vs 86 us, noise)
 #define PR_RAST_CH4 32
 #endif
   static constexpr int CH = SL >= 4 ? PR_RAST_CH4 : 64;
   static_assert(CAP <= 8 * 64, "suffix-min pass holds CAP / 64 <= 8 entries per lane");
 };
-constexpr int kCullU = 16;   // 64-face cull chunks whose boxes are in flight together
+#ifndef PR_RAST_CULLU  // sweeps: 8 measured equal, 4 slower (+10 us)
+#define PR_RAST_CULLU 16
+#endif
+constexpr int kCullU = PR_RAST_CULLU;  // 64-face cull chunks whose boxes are in flight together
 
 // Bitonic sort (ascending key) of n2 (power of two) LDS entries by NT threads.
 template <int NT>
