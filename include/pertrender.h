@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 8
+#define PR_ABI_VERSION 9
 
 /* error codes */
 #define PR_OK 0
@@ -270,6 +270,14 @@ int pr_interp_bwd(const PRInterpArgs* args, void* stream);
 
 /* seeds[i] <- splitmix64(seeds[i]) for i < n, on the stream (capturable). */
 int pr_seed_advance(uint64_t* seeds, int32_t n, void* stream);
+
+/* The kernels' own noise generator on explicit counters (diagnostic / known-answer entry):
+ * block i = Philox4x32-10(counters[4i..4i+3], key = keys[i] (lo word, hi word)).
+ * words (n,4) u32 receives the raw block; normals (n,4) f32 its Box-Muller N(0,1) samples
+ * (pr_common.h gauss4), cauchy (n,4) f32 its clamped Cauchy samples (cauchy4).  Each output
+ * is nullable.  This is exactly the per-(pixel, slot, sample-group) draw of PR_NOISE_PHILOX. */
+int pr_philox(const uint32_t* counters, const uint64_t* keys, int64_t n, uint32_t* words, float* normals,
+              float* cauchy, void* stream);
 
 #ifdef __cplusplus
 }

@@ -121,8 +121,9 @@ EXPORTS = {
     "pr_so3_exp_bwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
+    "pr_philox": (C.c_int, [_vp, _vp, C.c_int64, _vp, _vp, _vp, _vp]),
 }
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lib = None
 

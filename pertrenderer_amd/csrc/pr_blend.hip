@@ -1051,6 +1051,26 @@ __global__ void seed_advance_kernel(uint64_t* seeds, int n) {
   if (i < n) seeds[i] = mix64(seeds[i] + 0x9E3779B97F4A7C15ull);
 }
 
+// pr_philox: the generator of PR_NOISE_PHILOX on caller-given counters (known-answer tests)
+__global__ void __launch_bounds__(kThreads) philox_kernel(const uint4* ctr, const uint64_t* keys, int64_t n,
+                                                          uint4* words, float4* normals, float4* cauchy) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint4 c = ctr[i];
+  const uint64_t k = keys[i];
+  const U4 u = philox4x32_10(U4{c.x, c.y, c.z, c.w}, (uint32_t)k, (uint32_t)(k >> 32));
+  if (words) words[i] = make_uint4(u.x, u.y, u.z, u.w);
+  float e[4];
+  if (normals) {
+    gauss4(u, e);
+    normals[i] = make_float4(e[0], e[1], e[2], e[3]);
+  }
+  if (cauchy) {
+    cauchy4(u, e);
+    cauchy[i] = make_float4(e[0], e[1], e[2], e[3]);
+  }
+}
+
 // ================================================================== host side
 // A, B, PX, CP, queue length (+pad), then the uint16 rast queue [PB*K] (which also holds the
 // uint8 candidate lists [PB][KP1]: 2K >= K+1)
@@ -1289,4 +1309,14 @@ extern "C" int pr_seed_advance(uint64_t* seeds, int32_t n, void* stream) {
   if (!seeds || n <= 0) return set_error(PR_ERR_ARG, "seed_advance: bad args");
   seed_advance_kernel<<<(n + 63) / 64, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(seeds, n);
   return check_launch("seed_advance");
+}
+
+extern "C" int pr_philox(const uint32_t* counters, const uint64_t* keys, int64_t n, uint32_t* words, float* normals,
+                         float* cauchy, void* stream) {
+  if (!counters || !keys || n <= 0 || n > (int64_t(1) << 40)) return set_error(PR_ERR_ARG, "philox: bad args");
+  const int64_t nb = (n + kThreads - 1) / kThreads;
+  philox_kernel<<<(unsigned)nb, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<const uint4*>(counters), keys, n, reinterpret_cast<uint4*>(words),
+      reinterpret_cast<float4*>(normals), reinterpret_cast<float4*>(cauchy));
+  return check_launch("philox");
 }

@@ -85,20 +85,32 @@ def test_device_seed_keys_and_graph_replay(device):
 
 
 def test_fixed_noise_ignores_device_seed(device):
-    fr = _frags(device, seed=2)
+    """GaussianAgg(fixed_noise=True) reseeds the global generator with 1 before its draw
+    (smoothagg.py:18-19), so its noise is the same on every call even while a DeviceSeed base
+    advances; without fixed_noise the same calls draw fresh noise."""
+    from pertrenderer_amd.random_rasterizer import smooth_rgb_blend
+    from pertrenderer_amd.renderer import BlendParams, Fragments
+    p2f, dists, zbuf, cols = _frags(device, seed=2)
+    mask = p2f >= 0
+    prob = torch.rand(p2f.shape, generator=torch.Generator().manual_seed(3)).to(device) * mask
+    frag = Fragments(p2f, zbuf, None, dists)
     ds = DeviceSeed(device, seed=99)
     use_device_seed(ds)
     try:
-        agg = pa.GaussianAgg(nb_samples=8, gamma=1e-2, fixed_noise=True)
-        rast = pa.GaussianRast(nb_samples=8, sigma=1e-3)
-        from pertrenderer_amd.random_rasterizer import smooth_rgb_blend
-        from pertrenderer_amd.renderer import BlendParams, Fragments
-        frag = Fragments(fr[0], fr[2], None, fr[1])
-        outs = []
-        for _ in range(2):
-            ds.advance()
-            outs.append(smooth_rgb_blend(fr[3], frag, rast, agg, BlendParams(1e-3, 1e-2, (0, 0, 0))).detach())
-        # rast noise changes with the base; agg noise is fixed -> images differ only through P
-        assert outs[0].shape == outs[1].shape
+        for fixed in (True, False):
+            agg = pa.GaussianAgg(nb_samples=8, gamma=2e-2, fixed_noise=fixed)
+            # sigma so small that the Heaviside never flips: the image depends on the agg noise only
+            rast = pa.GaussianRast(nb_samples=8, sigma=1e-12)
+            ws, imgs = [], []
+            for _ in range(3):
+                ds.advance()
+                ws.append(agg.aggregate(zbuf, 100.0, 1.0, prob, mask).detach())
+                imgs.append(smooth_rgb_blend(cols, frag, rast, agg, BlendParams(1e-3, 2e-2, (0, 0, 0))).detach())
+            if fixed:
+                assert all(torch.equal(ws[0], w) for w in ws[1:])
+                assert all(torch.equal(imgs[0], i) for i in imgs[1:])
+            else:
+                assert not torch.equal(ws[0], ws[1]) and not torch.equal(ws[1], ws[2])
+                assert not torch.equal(imgs[0], imgs[1])
     finally:
         use_device_seed(None)
