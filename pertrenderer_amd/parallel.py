@@ -14,11 +14,14 @@ from .noise import Noise
 
 
 def sample_shard(S, rank, world, align=4):
-    """(offset, count) of `rank`'s share of S samples.  Shards are contiguous, cover
-    [0, S) exactly, and start on Philox-group boundaries (multiples of `align`) when
-    S allows, so no 4-sample Philox block is split between ranks."""
+    """(offset, count) of `rank`'s share of S samples.  Shards are contiguous and cover
+    [0, S) exactly.  They start on Philox-group boundaries (multiples of `align`) when there
+    are at least `world` groups, so no 4-sample Philox block is split between ranks;
+    otherwise the split is per sample, so every rank gets >= 1 sample whenever S >= world."""
     if S <= 0 or world <= 0 or not 0 <= rank < world:
         raise ValueError("bad shard request")
+    if (S + align - 1) // align < world:
+        align = 1
     groups = (S + align - 1) // align
     g0 = (groups * rank) // world
     g1 = (groups * (rank + 1)) // world
@@ -33,6 +36,14 @@ def shard_noise(seed_r, seed_a, Sr, Sa, rank, world):
     return Noise.philox(seed_r=seed_r, seed_a=seed_a, offset_r=off_r, offset_a=off_a), n_r, n_a
 
 
+def _collective_device(group, tensors=()):
+    """Where a collective's buffer must live: a CUDA device for RCCL ("nccl" cannot reduce
+    CPU tensors, and the reference's smoothing leaves are CPU 0-d tensors), else the CPU."""
+    if dist.get_backend(group) == "gloo":
+        return torch.device("cpu")
+    return next((t.device for t in tensors if t.is_cuda), torch.device("cuda", torch.cuda.current_device()))
+
+
 def average_gradients(params, group=None, weight=None):
     """One flattened all-reduce of every gradient (the step's only collective).
 
@@ -43,7 +54,7 @@ def average_gradients(params, group=None, weight=None):
     grads = [p.grad for p in params if p.grad is not None]
     if not grads:
         return
-    dev = next((g.device for g in grads if g.device.type != "cpu"), torch.device("cpu"))
+    dev = _collective_device(group, grads)
     flat = torch.cat([g.detach().reshape(-1).to(dev, torch.float32) for g in grads])
     if weight is not None:
         flat.mul_(float(weight))
@@ -62,17 +73,19 @@ def average_gradients(params, group=None, weight=None):
 # Monte-Carlo samples, and the collectives make the result the full-S estimator (the same
 # values as one GPU up to fp summation order), not an average of per-rank estimators:
 #   forward : all-reduce of the rast probabilities P (counts) and of the agg weights W;
-#   backward: all-reduce of dL/dP (the agg shards' contributions) and of dL/d dists and
-#             dL/d zbuf; the smoothing scalars' gradients are per-rank partial sums
-#             (reduce_scalar_grads).
+#   backward: all-reduce of dL/dP (the agg shards' contributions) and of dL/d dists,
+#             dL/d zbuf and the smoothing scalars (the same _SumBackward hop, so every leaf
+#             receives the complete gradient once per backward).
 # Built from the standalone native ops (perturbed_heaviside / perturbed_aggregate), the
 # colour blend in torch: it serves the large-S configurations, where the messages
 # (N,H,W,K) are small against the per-rank RNG work.
 
 def _all_reduce_sum(t, group):
-    """In-place SUM all-reduce; gloo reduces CUDA tensors through a host copy."""
-    if t.is_cuda and dist.get_backend(group) == "gloo":
-        c = t.detach().cpu()
+    """In-place SUM all-reduce of `t`, staged through the collective's device when it lives
+    elsewhere (gloo reduces host copies of CUDA tensors; RCCL device copies of CPU tensors)."""
+    dev = _collective_device(group, (t,))
+    if t.device != dev:
+        c = t.detach().to(dev)
         dist.all_reduce(c, group=group)
         t.copy_(c)
     else:
@@ -114,8 +127,10 @@ def exact_sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, n
     """smooth_rgb_blend (random_rasterizer.py:34-56) with GaussianRast / GaussianAgg over
     `nb_samples_*` GLOBAL samples split across the ranks of `group` (sample_shard): the
     image and the gradients of colors, dists and zbuf equal the single-process full-S
-    result up to fp summation order (P and W are exact: counts).  Call reduce_scalar_grads
-    after backward for sigma / gamma / alpha."""
+    result up to fp summation order (P and W are exact: counts).  sigma / gamma / alpha pass
+    through _SumBackward too, so their gradients are completed inside autograd: each leaf
+    accumulates the full-S gradient once per backward, exactly like the single-process op
+    (the reference's eval.py never zeroes them, eval.py:382-388)."""
     from .blend import perturbed_aggregate, perturbed_heaviside
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -128,25 +143,14 @@ def exact_sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, n
     mask = pix_to_face >= 0
     d_in = _SumBackward.apply(dists, group)
     z_in = _SumBackward.apply(zbuf, group)
-    P_r = perturbed_heaviside(d_in, sigma, n_r, noise=Noise.philox(seed_r=seed_r, offset_r=off_r))
+    s_in, g_in, a_in = (_SumBackward.apply(v, group) if torch.is_tensor(v) else v for v in (sigma, gamma, alpha))
+    P_r = perturbed_heaviside(d_in, s_in, n_r, noise=Noise.philox(seed_r=seed_r, offset_r=off_r))
     P = _SumForward.apply(P_r * mask, n_r / nb_samples_rast, group)  # smooth_rgb_blend :47
     P_in = _SumBackward.apply(P, group)
-    W_r = perturbed_aggregate(z_in, zfar, znear, P_in, mask, gamma, alpha, n_a, eps=eps,
+    W_r = perturbed_aggregate(z_in, zfar, znear, P_in, mask, g_in, a_in, n_a, eps=eps,
                               noise=Noise.philox(seed_a=seed_a, offset_a=off_a))
     W = _SumForward.apply(W_r, n_a / nb_samples_agg, group)
     bg = torch.as_tensor(background, dtype=colors.dtype, device=colors.device)
     rgb = (W[..., :K, None] * colors).sum(dim=-2) + W[..., K:K + 1] * bg  # :50-53
     a = 1.0 - torch.prod(1.0 - P, dim=-1, keepdim=True)  # :48, :54
     return torch.cat([rgb, a], dim=-1)
-
-
-def reduce_scalar_grads(params, group=None):
-    """Exact mode: the smoothing scalars' gradients are per-rank partial sums over the
-    sample shards; one SUM all-reduce completes them."""
-    grads = [p.grad for p in params if p is not None and p.grad is not None]
-    if not grads:
-        return
-    flat = torch.stack([g.detach().reshape(()).to(torch.float32) for g in grads])
-    _all_reduce_sum(flat, group)
-    for g, v in zip(grads, flat):
-        g.copy_(v.to(g.dtype))

@@ -1,0 +1,334 @@
+"""BASELINE cfg5: experiments/eval.py's pose-optimisation benchmark on this package.
+
+Mirrors, call for call, the reference's experiment driver:
+  * ``load_cube``       eval.py:727-757  (textured rubiks cube, TexturesUV)
+  * ``init_target``     eval.py:183-292  (cube centred / scaled, camera dist 6.7 elev 30 azim 120,
+                                         PointLights at (0,2,-2), HardPhongShader K=1 target of a
+                                         random_rotations pose)
+  * ``init_renderers``  eval.py:124-180  (20 deg perturbation of the true pose; MeshRasterizer with
+                                         blur = ln(1e4-1)*sigma, faces_per_pixel=50; RandomPhongShader
+                                         with GaussianRast(sigma) [Sr = 16, its default] +
+                                         GaussianAgg(nb_samples=MC), or SoftRast + SoftAgg)
+  * ``optimize_pose``   eval.py:320-409  (Adam lr 5e-2, best-loss tracking, the grad-norm guard, and
+                                         the adaptive schedule of :382-394: EMA of the smoothing
+                                         gradients, every 50 iterations after 100 while v_gamma > 0:
+                                         blur_radius / sigma / gamma / 1.1, nb_samples x2 up to 128,
+                                         lr / 1.5 and a fresh Adam)
+  * ``compare_pose_opt`` eval.py:576-661 (NUM_PROB problems x noise types; angle errors, solved
+                                         fractions per threshold, the seven json tables)
+
+Execution modes (``--mode``):
+  * ``eager``:  the reference loop as written, including its per-iteration host reads (loss value,
+                gradient norm, best-loss test).  This is what ``python eval.py`` does.
+  * ``graph``:  the same iteration as a captured HIP graph (fwd + bwd + guard + Adam + best-loss
+                tracking + the smoothing-gradient EMA, all on the device); the host only decides the
+                adaptive schedule every 50 iterations and re-captures when it changes S or blur.
+                Numerically the same algorithm (same Philox noise stream per iteration).
+
+Multi-GPU (``torchrun --nproc-per-node G -m pertrenderer_amd.pose_opt``): the independent problems
+are dealt round-robin to the ranks (one process per GPU), results are gathered on rank 0; no
+collective on the data path.  Wall-clock = the slowest rank.
+"""
+import argparse
+import json
+import math
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import random_rasterizer as rr
+from .renderer import (BlendParams, HardPhongShader, Meshes, MeshRasterizer, MeshRenderer, OpenGLPerspectiveCameras,
+                       PointLights, RasterizationSettings, Textures, load_obj, look_at_view_transform)
+from .renderer.transforms import Rotate, random_rotations, so3_exponential_map, so3_log_map, so3_relative_angle
+from .smoothagg import CauchyAgg, GaussianAgg, GaussianAgg_wovr, HardAgg, SoftAgg
+from .smoothrast import AffineRast, ArctanRast, GaussianRast, GaussianRast_wovr, HardRast, SoftRast
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DATA = os.path.join(ROOT, "tests", "golden")  # the reference's data/objs/rubiks files
+THRESHOLDS = (1, 2, 5, 10, 15, 20, 25, 35, 45)  # eval.py:603
+BLUR_FACTOR = math.log(1.0 / 1e-4 - 1.0)  # eval.py:137
+
+
+def load_cube(device, data_dir=DATA):
+    """eval.py:727-757: cube2.obj with its texture strip recoloured face by face from cube_p.npz."""
+    with np.load(os.path.join(data_dir, "cube_p.npz")) as f:
+        _, _, _, col = f.values()
+    vtx_col = torch.from_numpy(col.astype(np.float32))
+    green = vtx_col[3, :].clone()  # "reorder color to have same cube as softras"
+    vtx_col[3, :] = vtx_col[0, :]
+    vtx_col[0, :] = green
+    verts, faces, aux = load_obj(os.path.join(data_dir, "cube2.obj"))
+    img = aux.texture_images["cube"]
+    band = img.size()[1] // 6
+    for i in range(6):
+        img[:, i * band:(i + 1) * band, :] = vtx_col[i, :][None, None].repeat(img.size()[0], band, 1)
+    tex = Textures(verts_uvs=aux.verts_uvs[None], faces_uvs=faces.textures_idx[None], maps=img[None])
+    return Meshes(verts=[verts], faces=[faces.verts_idx], textures=tex).to(device)
+
+
+class Scene:
+    """init_target's fixed part (eval.py:239-263): normalised cube, cameras, lights."""
+
+    def __init__(self, device, imsize):
+        mesh = load_cube(device)
+        v = mesh.verts_packed()
+        center = v.mean(0)
+        scale = max((v - center).abs().max(0)[0])
+        mesh.offset_verts_(-center.expand(v.shape[0], 3))
+        mesh.scale_verts_(1.0 / float(scale))
+        self.meshes = mesh.extend(1)
+        R, T = look_at_view_transform(dist=6.7, elev=torch.linspace(30, 240, 1), azim=torch.linspace(120, 150, 1))
+        R, T = R.to(device), T.to(device)
+        self.cameras = [OpenGLPerspectiveCameras(device=device, R=R[None, 0], T=T[None, 0], fov=60)]
+        self.camera = OpenGLPerspectiveCameras(device=device, R=R[None, 0], T=T[None, 0])
+        self.lights = PointLights(device=device, location=[[0.0, 2.0, -2.0]])
+        self.device, self.imsize = device, imsize
+        self.hard = MeshRenderer(
+            MeshRasterizer(cameras=self.camera, raster_settings=RasterizationSettings(
+                image_size=imsize, blur_radius=0.0, faces_per_pixel=1, max_faces_per_bin=100000)),
+            HardPhongShader(device=device, blend_params=BlendParams(background_color=(0.0, 0.0, 0.0))))
+
+    def target(self):
+        """One test problem's target (eval.py:284-292): a random_rotations pose, hard render."""
+        R_true = random_rotations(1).to(self.device)
+        m = self.meshes.update_padded(Rotate(R_true).transform_points(self.meshes.verts_padded()))
+        img = self.hard(m, cameras=self.cameras[0], lights=self.lights)
+        return [img[0, ..., :3].detach()], R_true
+
+
+def init_renderers(scene, R_true, pert_init_intensity=20.0, sigma=1e-3, gamma=1e-2, alpha=1.0, nb_samples=8,
+                   noise_type=("softras", "gaussian")):
+    """eval.py:124-180 -> (log_rot_init, [MeshRenderer per noise type])."""
+    dev = scene.device
+    if pert_init_intensity == 0.0:
+        R_init = random_rotations(1).to(dev)
+    else:
+        R_pert = torch.normal(torch.zeros((1, 3), device=dev))
+        R_pert = so3_exponential_map((pert_init_intensity * np.pi / 180.0) * R_pert / R_pert.norm(dim=1))
+        R_init = torch.bmm(R_true.clone(), R_pert).detach().clone()
+    log_rot_init = so3_log_map(R_init)
+    blend = BlendParams(sigma=sigma, gamma=gamma, background_color=(0.0, 0.0, 0.0))
+    renderers = []
+    for nt in noise_type:
+        settings = RasterizationSettings(image_size=scene.imsize, blur_radius=BLUR_FACTOR * blend.sigma,
+                                         faces_per_pixel=50, max_faces_per_bin=50000, perspective_correct=False)
+        rast, agg = {
+            "cauchy": lambda: (ArctanRast(sigma=sigma), CauchyAgg(gamma=gamma, alpha=1.0, nb_samples=nb_samples)),
+            "gaussian": lambda: (GaussianRast(sigma=sigma), GaussianAgg(gamma=gamma, alpha=1.0, nb_samples=nb_samples)),
+            "gaussian_wovr": lambda: (GaussianRast_wovr(sigma=sigma),
+                                      GaussianAgg_wovr(gamma=gamma, alpha=1.0, nb_samples=nb_samples)),
+            "uniform": lambda: (AffineRast(sigma=sigma), HardAgg()),
+            "hard": lambda: (HardRast(), HardAgg()),
+            "softras": lambda: (SoftRast(sigma=sigma), SoftAgg(gamma=gamma, alpha=1.0)),
+        }[nt]()
+        renderers.append(MeshRenderer(
+            MeshRasterizer(cameras=scene.camera, raster_settings=settings),
+            rr.RandomPhongShader(device=dev, cameras=scene.camera, lights=scene.lights, blend_params=blend,
+                                 smoothrast=rast, smoothagg=agg)))
+    return log_rot_init, renderers
+
+
+def _adapt(renderer, i, v, adapt_params, lr, log_rot):
+    """eval.py:382-394 for iteration i (> 100); v = [v_sigma, v_gamma, v_alpha] (CPU tensors).
+    Returns (new lr or None, v)."""
+    sigma, gamma, alpha = renderer.shader.get_smoothing()
+    grads = [t.grad if t.grad is not None else torch.zeros_like(t) for t in (sigma, gamma, alpha)]
+    v = [0.9 * vi.detach().clone() + 0.1 * g.detach().clone().reshape(vi.shape).cpu() for vi, g in zip(v, grads)]
+    for t in (sigma, gamma, alpha):
+        if t.grad is not None:
+            t.grad = torch.zeros_like(t.grad)
+    new_sigma = sigma.detach().clone() / adapt_params[0]
+    new_gamma = gamma.detach().clone() / adapt_params[1]
+    nb = renderer.shader.get_nb_samples()
+    if v[1] > 0 and (i + 1) % 50 == 0:
+        s = max(float(new_sigma), 5e-5)
+        renderer.rasterizer.raster_settings.blur_radius = BLUR_FACTOR * s
+        renderer.shader.update_smoothing(sigma=s, gamma=max(float(new_gamma), 5e-4))
+        renderer.shader.update_nb_samples(nb_samples=min(2 * nb, 128))
+        return max(lr / 1.5, 1e-4), v
+    return None, v
+
+
+def optimize_pose(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Niter=800, adapt_reg=True,
+                  adapt_params=(1.1, 1.1)):
+    """eval.py:320-409 (eager, as written).  Returns (best_log_rot, info)."""
+    losses, gradient_values = [], []
+    log_rot = init_pose.clone().requires_grad_(True)
+    lr = lr_init
+    optimizer = torch.optim.Adam([log_rot], lr=lr)
+    v = [torch.zeros(1), torch.zeros(1), torch.zeros(1)]
+    best_log_rot, best_loss = log_rot.clone(), np.inf
+    mesh, cams, lights = scene.meshes, scene.cameras, scene.lights
+    runtimes = {"forward": [], "backward": []}
+    for i in range(Niter):
+        R = so3_exponential_map(log_rot)
+        predicted = mesh.update_padded(Rotate(R).transform_points(mesh.verts_padded()))
+        t1 = time.time()
+        images = renderer(predicted, cameras=cams[0], lights=lights)
+        loss_rgb = ((images[..., :3] - target_rgb[0]) ** 2).mean()
+        t2 = time.time()
+        losses.append(loss_rgb.detach().cpu().item())
+        optimizer.zero_grad()
+        t3 = time.time()
+        loss_rgb.backward()
+        t4 = time.time()
+        lv = loss_rgb.detach().cpu().numpy()
+        if lv < best_loss:
+            best_loss, best_log_rot = lv, log_rot.clone()
+        gradient_values.append(torch.norm(log_rot.grad).detach().cpu().item())
+        if gradient_values[-1] > 1000.0:
+            log_rot.grad = 1e-5 * torch.normal(torch.zeros_like(log_rot.grad))
+        optimizer.step()
+        runtimes["forward"].append(t2 - t1)
+        runtimes["backward"].append(t4 - t3)
+        if adapt_reg and i > 100:
+            new_lr, v = _adapt(renderer, i, v, adapt_params, lr, log_rot)
+            if new_lr is not None:
+                lr = new_lr
+                optimizer = torch.optim.Adam([log_rot], lr=lr)
+    return best_log_rot, dict(loss_values=losses, gradient_values=gradient_values, runtimes=runtimes,
+                              nb_samples=renderer.shader.get_nb_samples())
+
+
+def angle_deg(log_rot, R_true):
+    return so3_relative_angle(so3_exponential_map(log_rot), R_true).detach().cpu().item() * 180.0 / np.pi
+
+
+def make_problems(scene, num_prob, noise_type, pert):
+    """compare_pose_opt's test problems (eval.py:605-609): targets and initial poses."""
+    problems = []
+    for _ in range(num_prob):
+        target_rgb, R_true = scene.target()
+        log_rot_init, _ = init_renderers(scene, R_true, pert_init_intensity=pert, sigma=0.1, gamma=0.1, nb_samples=1,
+                                         noise_type=noise_type)
+        problems.append(([t.clone() for t in target_rgb], R_true.clone(), log_rot_init.detach().clone()))
+    return problems
+
+
+def run_problem(scene, problem, noise_type, sigma, gamma, nb_mc, pert, niter, adapt_reg, adapt_params, mode):
+    target_rgb, R_true, log_rot_init = problem
+    _, renderers = init_renderers(scene, R_true, pert_init_intensity=pert, sigma=sigma, gamma=gamma,
+                                  nb_samples=nb_mc, noise_type=noise_type)
+    out = {}
+    for nt, renderer in zip(noise_type, renderers):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if mode == "graph" and nt != "softras":
+            from .pose_graph import optimize_pose_graph
+            log_rot, info = optimize_pose_graph(scene, log_rot_init, renderer, target_rgb, Niter=niter,
+                                                adapt_reg=adapt_reg, adapt_params=adapt_params)
+        else:
+            log_rot, info = optimize_pose(scene, log_rot_init, renderer, target_rgb, Niter=niter, adapt_reg=adapt_reg,
+                                          adapt_params=adapt_params)
+        torch.cuda.synchronize()
+        out[nt] = dict(seconds=time.perf_counter() - t0, init_error=angle_deg(log_rot_init, R_true),
+                       final_error=angle_deg(log_rot, R_true), final_nb_samples=info["nb_samples"],
+                       final_loss=info["loss_values"][-1], iterations=niter)
+    return out
+
+
+def tables(per_problem, noise_type, params, exp_setup):
+    """compare_pose_opt's json tables (eval.py:632-661) for one parameter setting."""
+    mean_errors, var_errors, init_errors, final_errors = {}, {}, {}, {}
+    mean_solved = {}
+    for nt in noise_type:
+        err = [p[nt]["final_error"] for p in per_problem]
+        mean_errors[nt] = [sum(err) / len(err)]
+        var_errors[nt] = [float(np.std(err))]
+        init_errors[nt] = [[p[nt]["init_error"] for p in per_problem]]
+        final_errors[nt] = [err]
+        mean_solved[nt] = {th: [sum(1 if a < th else 0 for a in err) / len(err)] for th in THRESHOLDS}
+    return dict(mean_errors=mean_errors, final_errors=final_errors, init_errors=init_errors, var_errors=var_errors,
+                mean_solved=mean_solved, params=params, exp_setup=exp_setup)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="eval.py compare_pose_opt (BASELINE cfg5) on pertrenderer_amd")
+    ap.add_argument("-np", "--num-prob", type=int, default=100)
+    ap.add_argument("-ni", "--num-iterations", type=int, default=800)
+    ap.add_argument("-is", "--image-size", type=int, default=256)
+    ap.add_argument("-sn", "--smoothing-noise", nargs="+", default=["softras", "gaussian"])
+    ap.add_argument("-mc", "--mc-samples", type=int, default=8)
+    ap.add_argument("-sv", "--smoothing", type=float, nargs=2, default=(1e-3, 1e-2))
+    ap.add_argument("-ip", "--initial-perturbation", type=float, default=20.0)
+    ap.add_argument("-ar", "--adaptive-regularization", type=int, default=1)
+    ap.add_argument("-s", "--seed", type=int, default=1)
+    ap.add_argument("--mode", choices=["eager", "graph"], default="eager")
+    ap.add_argument("--out", default=None, help="directory for eval.py's tables + summary.json")
+    args = ap.parse_args(argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")  # results only: a handful of floats per problem
+    torch.manual_seed(args.seed)
+    t_setup = time.perf_counter()
+    scene = Scene(device, args.image_size)
+    noise_type = list(args.smoothing_noise)
+    problems = make_problems(scene, args.num_prob, noise_type, args.initial_perturbation)
+    sigma, gamma = args.smoothing
+    adapt_params = (1.1, 1.1)
+    mine = list(range(rank, args.num_prob, world))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    results = {}
+    for i in mine:
+        results[i] = run_problem(scene, problems[i], noise_type, sigma, gamma, args.mc_samples,
+                                 args.initial_perturbation, args.num_iterations, bool(args.adaptive_regularization),
+                                 adapt_params, args.mode)
+        if rank == 0:
+            print(json.dumps({"problem": i, **{nt: {k: round(v, 4) if isinstance(v, float) else v
+                                                    for k, v in r.items()} for nt, r in results[i].items()}}),
+                  flush=True)
+    wall = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (results, wall))
+        results = {k: v for res, _ in gathered for k, v in res.items()}
+        wall = max(w for _, w in gathered)
+        dist.destroy_process_group()
+    if rank != 0:
+        return 0
+    per_problem = [results[i] for i in sorted(results)]
+    params = {"lr-smoothing-MC": [(5e-2, sigma, gamma, args.mc_samples)], "lr": [5e-2], "sigma": [sigma],
+              "gamma": [gamma], "MC": [args.mc_samples], "adapt_params": [adapt_params]}
+    exp_setup = {"perturbation": args.initial_perturbation, "Niter": args.num_iterations, "optimizer": "adam",
+                 "N_benchmark": args.num_prob, "adaptive_regularization": args.adaptive_regularization,
+                 "category": ["cube"]}
+    tab = tables(per_problem, noise_type, params, exp_setup)
+    summary = {
+        "workload": f"eval.py compare_pose_opt: cube (TexturesUV) + RandomPhongShader, {args.image_size}^2, "
+                    f"faces_per_pixel=50, {args.num_prob} problems x {args.num_iterations} iterations, "
+                    f"noise {noise_type}, MC={args.mc_samples} (GaussianRast Sr=16 default), adaptive schedule "
+                    f"{'on' if args.adaptive_regularization else 'off'}",
+        "mode": args.mode, "n_gpus": world, "wall_clock_s": round(wall, 3), "setup_s": round(t0 - t_setup, 3),
+        "per_noise": {}}
+    for nt in noise_type:
+        secs = [p[nt]["seconds"] for p in per_problem]
+        summary["per_noise"][nt] = {
+            "mean_seconds_per_problem": round(float(np.mean(secs)), 4),
+            "ms_per_iteration": round(1e3 * float(np.mean(secs)) / args.num_iterations, 4),
+            "mean_final_error_deg": round(tab["mean_errors"][nt][0], 4),
+            "std_final_error_deg": round(tab["var_errors"][nt][0], 4),
+            "mean_init_error_deg": round(float(np.mean(tab["init_errors"][nt][0])), 4),
+            "solved": {str(th): tab["mean_solved"][nt][th][0] for th in THRESHOLDS},
+            "final_nb_samples": sorted({p[nt]["final_nb_samples"] for p in per_problem}),
+        }
+    print(json.dumps(summary), flush=True)
+    if args.out:
+        from . import results as res
+        res.write_pose_results(args.out, **tab)
+        with open(os.path.join(args.out, "summary.json"), "w") as f:
+            json.dump({"summary": summary, "per_problem": per_problem}, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

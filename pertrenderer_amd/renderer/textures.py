@@ -52,12 +52,13 @@ class TexturesUV:
         uv = interpolate_face_attributes(p2f, bary, self._faces_verts_uvs_packed().to(bary.device))
         N, Ho, Wo, K = p2f.shape
         maps = self.maps_padded().to(bary.device)
-        _, Hi, Wi, C = maps.shape
-        uv = uv.permute(0, 3, 1, 2, 4).reshape(N * K, Ho, Wo, 2) * 2.0 - 1.0
-        m = maps.permute(0, 3, 1, 2)[None].expand(K, -1, -1, -1, -1).transpose(0, 1).reshape(N * K, C, Hi, Wi)
-        m = torch.flip(m, [2])  # v = 0 is the bottom row of the image
+        C = maps.shape[-1]
+        # one (Ho, Wo*K) sampling grid per mesh: every (pixel, slot) is an independent bilinear
+        # lookup, so the map is read in place instead of being replicated K times
+        uv = uv.reshape(N, Ho, Wo * K, 2) * 2.0 - 1.0
+        m = torch.flip(maps.permute(0, 3, 1, 2), [2])  # v = 0 is the bottom row of the image
         tex = F.grid_sample(m, uv, align_corners=self.align_corners, padding_mode=self.padding_mode)
-        return tex.reshape(N, K, C, Ho, Wo).permute(0, 3, 4, 1, 2)
+        return tex.reshape(N, C, Ho, Wo, K).permute(0, 2, 3, 4, 1)
 
     def extend(self, N):
         rep = lambda lst: [t for t in lst for _ in range(N)]

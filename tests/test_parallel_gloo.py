@@ -33,6 +33,8 @@ def test_sample_shard_covers_range():
             assert off == S
             if S % (4 * world) == 0:
                 assert all(o % 4 == 0 for o, _ in got)
+            if S >= world:  # every rank gets work (S=8 on 4 or 8 ranks splits per sample)
+                assert all(n >= 1 for _, n in got), (S, world, got)
 
 
 def _worker(rank, world, port, q):
@@ -81,6 +83,13 @@ def _worker(rank, world, port, q):
         P_ref = 0.5 * (xr ** 2 + xr ** 3)
         g_ref = torch.cos(P_ref) * c * 0.5 * (2 * xr + 3 * xr ** 2)
         ok4 = torch.allclose(P.detach(), P_ref, atol=1e-6) and torch.allclose(x.grad, g_ref, atol=1e-6)
+        # 5) a CPU 0-d leaf (the reference's sigma) through _SumBackward: one complete sum per
+        #    backward, accumulated like a local gradient (no re-reduction of earlier steps)
+        sg = torch.tensor(2.0, requires_grad=True)
+        for _ in range(2):
+            (_SumBackward.apply(sg, None) * float(rank + 1)).backward()
+        ok5 = sg.grad.device.type == "cpu" and abs(float(sg.grad) - 2 * 3.0) < 1e-6
+        ok4 = ok4 and ok5
         q.put((rank, bool(ok1), bool(ok2 and ok3 and ok4)))
     finally:
         dist.destroy_process_group()
