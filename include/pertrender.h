@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 9
+#define PR_ABI_VERSION 10
 
 /* error codes */
 #define PR_OK 0
@@ -207,6 +207,60 @@ typedef struct PRProjectArgs {
   float* grad_verts;           /* bwd out (V,3), overwritten */
   int32_t flags;               /* PR_GRAD_PREZEROED: pr_project_bwd does not zero grad_verts */
 } PRProjectArgs;
+
+/* Phong shading of every fragment slot: PyTorch3D 0.4.0 phong_shading (+ the texel lookup of
+ * Meshes.sample_textures), the colour producer of RandomPhongShader (random_rasterizer.py:99-110,
+ * used by experiments/eval.py:170):
+ *   p = sum_i b_i verts[f_i],  n = sum_i b_i normals[f_i],  t = texel of the slot,
+ *   d^ = normalize(light - p) (point) or normalize(light) (directional),  n^ = normalize(n),
+ *   c = n^.d^,  diffuse = diffuse_color * relu(c),
+ *   specular = specular_color * (relu(normalize(camera - p) . (2 c n^ - d^)) * [c > 0])^shininess,
+ *   colour = (ambient + mat_diffuse * diffuse) * t + mat_specular * specular
+ * (normalize(x) = x / max(|x|, 1e-6)).  Padded slots (pix_to_face < 0) shade p = n = 0 at uv = 0,
+ * exactly like the reference composition.  All per-batch parameters are (N,3) / (N,) rows. */
+#define PR_TEX_GIVEN 0   /* texels (N,H,W,K,3) given (any Textures.sample_textures output) */
+#define PR_TEX_UV 1      /* TexturesUV: bilinear map lookup at the interpolated corner UVs */
+#define PR_TEX_VERTEX 2  /* TexturesVertex: interpolated per-vertex colours */
+
+typedef struct PRShadeArgs {
+  int32_t N, H, W, K;
+  const int64_t* pix_to_face;  /* (N,H,W,K) */
+  const int32_t* pix_count;    /* nullable valid-prefix counts (N,H,W) */
+  const float* bary;           /* (N,H,W,K,3) */
+  const int64_t* faces;        /* (F,3) packed vertex indices */
+  const float* verts;          /* (V,3) world positions */
+  const float* normals;        /* (V,3) vertex normals */
+  int64_t V, F;
+  int32_t texture;             /* PR_TEX_* */
+  const float* texels;         /* GIVEN: (N,H,W,K,3) */
+  const float* vert_colors;    /* VERTEX: (V,3) */
+  const float* face_uvs;       /* UV: (F,3,2) corner UVs */
+  const float* maps;           /* UV: (N,Hm,Wm,3), v = 0 is the bottom row; grid_sample bilinear, */
+  int32_t Hm, Wm;              /*     align_corners=True, padding "border" (TexturesUV defaults)  */
+  int32_t directional;         /* 0: point lights (light = location), 1: directional (light = direction) */
+  const float* light;          /* (N,3) */
+  const float* ambient;        /* (N,3) material ambient * light ambient */
+  const float* diffuse_color;  /* (N,3) light diffuse colour */
+  const float* specular_color; /* (N,3) light specular colour */
+  const float* mat_diffuse;    /* (N,3) */
+  const float* mat_specular;   /* (N,3) */
+  const float* shininess;      /* (N,) */
+  const float* camera;         /* (N,3) camera centres */
+  float* colors;               /* fwd out (N,H,W,K,3) */
+  /* backward: every non-null output is overwritten (accumulators are zeroed by the call) */
+  const float* grad_colors;    /* (N,H,W,K,3) */
+  float* grad_bary;            /* (N,H,W,K,3) */
+  float* grad_verts;           /* (V,3) */
+  float* grad_normals;         /* (V,3) */
+  float* grad_texels;          /* GIVEN: (N,H,W,K,3) */
+  float* grad_vert_colors;     /* VERTEX: (V,3) */
+  float* grad_maps;            /* UV: (N,Hm,Wm,3) */
+  float* grad_light;           /* (N,3) */
+  float* grad_camera;          /* (N,3) */
+} PRShadeArgs;
+
+int pr_shade_fwd(const PRShadeArgs* args, void* stream);
+int pr_shade_bwd(const PRShadeArgs* args, void* stream);
 
 /* the backward's gradient accumulator was zeroed by the forward (pr_project_rast_fwd) */
 #define PR_GRAD_PREZEROED 1

@@ -97,6 +97,23 @@ class PRRotateArgs(C.Structure):
                 ("out", _vp), ("grad_out", _vp), ("grad_points", _vp), ("grad_R", _vp)]
 
 
+PR_TEX_GIVEN = 0
+PR_TEX_UV = 1
+PR_TEX_VERTEX = 2
+
+
+class PRShadeArgs(C.Structure):
+    _fields_ = [("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("K", C.c_int32),
+                ("pix_to_face", _vp), ("pix_count", _vp), ("bary", _vp), ("faces", _vp), ("verts", _vp),
+                ("normals", _vp), ("V", C.c_int64), ("F", C.c_int64), ("texture", C.c_int32), ("texels", _vp),
+                ("vert_colors", _vp), ("face_uvs", _vp), ("maps", _vp), ("Hm", C.c_int32), ("Wm", C.c_int32),
+                ("directional", C.c_int32), ("light", _vp), ("ambient", _vp), ("diffuse_color", _vp),
+                ("specular_color", _vp), ("mat_diffuse", _vp), ("mat_specular", _vp), ("shininess", _vp),
+                ("camera", _vp), ("colors", _vp), ("grad_colors", _vp), ("grad_bary", _vp), ("grad_verts", _vp),
+                ("grad_normals", _vp), ("grad_texels", _vp), ("grad_vert_colors", _vp), ("grad_maps", _vp),
+                ("grad_light", _vp), ("grad_camera", _vp)]
+
+
 # every symbol include/pertrender.h declares, with its argument struct (None = no args)
 EXPORTS = {
     "pr_abi_version": (C.c_int, []),
@@ -122,8 +139,10 @@ EXPORTS = {
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_philox": (C.c_int, [_vp, _vp, C.c_int64, _vp, _vp, _vp, _vp]),
+    "pr_shade_fwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
+    "pr_shade_bwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
 }
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib = None
 

@@ -73,9 +73,9 @@ def average_gradients(params, group=None, weight=None):
 # Monte-Carlo samples, and the collectives make the result the full-S estimator (the same
 # values as one GPU up to fp summation order), not an average of per-rank estimators:
 #   forward : all-reduce of the rast probabilities P (counts) and of the agg weights W;
-#   backward: all-reduce of dL/dP (the agg shards' contributions) and of dL/d dists,
-#             dL/d zbuf and the smoothing scalars (the same _SumBackward hop, so every leaf
-#             receives the complete gradient once per backward).
+#   backward: all-reduce of dL/dP (the agg shards' contributions) and of dL/d dists and
+#             dL/d zbuf; the smoothing scalars' per-rank partials are completed after the
+#             backward by reduce_scalar_grads (only the part accumulated since its last call).
 # Built from the standalone native ops (perturbed_heaviside / perturbed_aggregate), the
 # colour blend in torch: it serves the large-S configurations, where the messages
 # (N,H,W,K) are small against the per-rank RNG work.
@@ -127,10 +127,10 @@ def exact_sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, n
     """smooth_rgb_blend (random_rasterizer.py:34-56) with GaussianRast / GaussianAgg over
     `nb_samples_*` GLOBAL samples split across the ranks of `group` (sample_shard): the
     image and the gradients of colors, dists and zbuf equal the single-process full-S
-    result up to fp summation order (P and W are exact: counts).  sigma / gamma / alpha pass
-    through _SumBackward too, so their gradients are completed inside autograd: each leaf
-    accumulates the full-S gradient once per backward, exactly like the single-process op
-    (the reference's eval.py never zeroes them, eval.py:382-388)."""
+    result up to fp summation order (P and W are exact: counts).  Call reduce_scalar_grads
+    after each backward for sigma / gamma / alpha (their leaves are CPU tensors: a collective
+    inside their backward nodes would run on autograd's CPU thread, unordered against the
+    device-thread collectives, so the ranks could disagree on the collective order)."""
     from .blend import perturbed_aggregate, perturbed_heaviside
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -143,14 +143,38 @@ def exact_sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, n
     mask = pix_to_face >= 0
     d_in = _SumBackward.apply(dists, group)
     z_in = _SumBackward.apply(zbuf, group)
-    s_in, g_in, a_in = (_SumBackward.apply(v, group) if torch.is_tensor(v) else v for v in (sigma, gamma, alpha))
-    P_r = perturbed_heaviside(d_in, s_in, n_r, noise=Noise.philox(seed_r=seed_r, offset_r=off_r))
+    P_r = perturbed_heaviside(d_in, sigma, n_r, noise=Noise.philox(seed_r=seed_r, offset_r=off_r))
     P = _SumForward.apply(P_r * mask, n_r / nb_samples_rast, group)  # smooth_rgb_blend :47
     P_in = _SumBackward.apply(P, group)
-    W_r = perturbed_aggregate(z_in, zfar, znear, P_in, mask, g_in, a_in, n_a, eps=eps,
+    W_r = perturbed_aggregate(z_in, zfar, znear, P_in, mask, gamma, alpha, n_a, eps=eps,
                               noise=Noise.philox(seed_a=seed_a, offset_a=off_a))
     W = _SumForward.apply(W_r, n_a / nb_samples_agg, group)
     bg = torch.as_tensor(background, dtype=colors.dtype, device=colors.device)
     rgb = (W[..., :K, None] * colors).sum(dim=-2) + W[..., K:K + 1] * bg  # :50-53
     a = 1.0 - torch.prod(1.0 - P, dim=-1, keepdim=True)  # :48, :54
     return torch.cat([rgb, a], dim=-1)
+
+
+def reduce_scalar_grads(params, group=None):
+    """Exact mode: complete the smoothing scalars' gradients after a backward.  Each rank holds
+    its shard's partial sum; only what was accumulated since this function last saw the leaf is
+    all-reduced (SUM), so a leaf that is never zeroed -- the reference's sigma / gamma / alpha
+    are not, eval.py:382-388 -- accumulates exactly the single-process gradient per backward
+    instead of re-reducing its history.  One collective for all leaves, staged on the device
+    for RCCL (the leaves are CPU 0-d tensors)."""
+    leaves = [p for p in params if p is not None and p.grad is not None]
+    if not leaves:
+        return
+    deltas = []
+    for p in leaves:
+        seen = getattr(p, "_pr_reduced_grad", None)
+        g = p.grad.detach().reshape(()).to(torch.float32)
+        deltas.append(g - seen if seen is not None and seen.device == g.device else g)
+    flat = torch.stack(deltas)
+    _all_reduce_sum(flat, group)
+    for p, d in zip(leaves, flat):
+        seen = getattr(p, "_pr_reduced_grad", None)
+        base = seen if seen is not None and seen.device == p.grad.device else torch.zeros_like(d)
+        total = (base.to(d.device) + d).to(p.grad.dtype)
+        p.grad.copy_(total.reshape(p.grad.shape).to(p.grad.device))
+        p._pr_reduced_grad = p.grad.detach().reshape(()).to(torch.float32).clone()

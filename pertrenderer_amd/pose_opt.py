@@ -192,6 +192,155 @@ def optimize_pose(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Niter=80
                               nb_samples=renderer.shader.get_nb_samples())
 
 
+# ------------------------------------------------------------------ graph mode
+def _device_leaves(shader, device):
+    """The smoothing leaves as device tensors (same values, requires_grad, zero grads): the
+    captured step passes them to the kernels by pointer and accumulates their gradients in place."""
+    sr, sa = shader.smoothrast, shader.smoothagg
+    for obj, names in ((sr, ("sigma",)), (sa, ("gamma", "alpha"))):
+        for name in names:
+            t = getattr(obj, name, None)
+            if torch.is_tensor(t):
+                leaf = torch.tensor(float(t.detach()), device=device, requires_grad=True)
+                leaf.grad = torch.zeros_like(leaf)
+                setattr(obj, name, leaf)
+
+
+def _fresh_adam(log_rot, lr):
+    """torch.optim.Adam([log_rot], lr) with its state initialised up front (capturable, fused):
+    the same state a new optimizer starts from (eval.py:337, :394)."""
+    opt = torch.optim.Adam([log_rot], lr=lr, capturable=True, fused=True)
+    opt.state[log_rot] = {"step": torch.zeros((), dtype=torch.float32, device=log_rot.device),
+                          "exp_avg": torch.zeros_like(log_rot), "exp_avg_sq": torch.zeros_like(log_rot)}
+    return opt
+
+
+class _CapturedIteration:
+    """One optimize_pose iteration (eval.py:343-388) as a HIP graph for a fixed schedule state
+    (nb_samples, blur_radius, lr): noise key advance, so3 pose, render, L2 loss, backward,
+    loss / grad-norm records, best-loss tracking, the grad-norm guard, Adam, and (post) the EMA
+    of the smoothing gradients with their zeroing."""
+
+    def __init__(self, scene, renderer, target, log_rot, st, opt, post, seed, pool):
+        self.scene, self.renderer, self.target, self.log_rot = scene, renderer, target, log_rot
+        self.st, self.opt, self.post, self.seed = st, opt, post, seed
+        leaves = list(renderer.shader.get_smoothing())
+        self.leaves = leaves
+        # warm-up pass on a side stream (lazy allocations and caches outside the graph); it must
+        # not change the optimisation state: the gradients it accumulates are restored
+        saved = [l.grad.detach().clone() for l in leaves]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self.seed.advance()
+            self._forward().backward()
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.no_grad():
+            for l, g in zip(leaves, saved):
+                l.grad.copy_(g)
+            log_rot.grad.zero_()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, pool=pool):
+            self._body()
+
+    def _forward(self):
+        mesh = self.scene.meshes
+        R = so3_exponential_map(self.log_rot)
+        predicted = mesh.update_padded(Rotate(R).transform_points(mesh.verts_padded()))
+        images = self.renderer(predicted, cameras=self.scene.cameras[0], lights=self.scene.lights)
+        return ((images[..., :3] - self.target) ** 2).mean()
+
+    def _body(self):
+        st, log_rot = self.st, self.log_rot
+        self.seed.advance()
+        loss = self._forward()
+        log_rot.grad.zero_()
+        loss.backward()
+        with torch.no_grad():
+            it = st["it"].view(1)
+            st["losses"].index_copy_(0, it, loss.detach().view(1))
+            better = loss.detach() < st["best_loss"]
+            st["best_loss"].copy_(torch.where(better, loss.detach(), st["best_loss"]))
+            st["best"].copy_(torch.where(better, log_rot.detach(), st["best"]))
+            gn = torch.linalg.vector_norm(log_rot.grad)
+            st["gnorms"].index_copy_(0, it, gn.view(1))
+            log_rot.grad.copy_(torch.where(gn > 1000.0, 1e-5 * torch.randn_like(log_rot.grad), log_rot.grad))
+        self.opt.step()
+        with torch.no_grad():
+            if self.post:
+                g = torch.stack([l.grad.reshape(()) for l in self.leaves])
+                st["v"].mul_(0.9).add_(0.1 * g)
+                for l in self.leaves:
+                    l.grad.zero_()
+            st["it"].add_(1)
+
+    def replay(self, n):
+        for _ in range(n):
+            self.graph.replay()
+
+
+def optimize_pose_graph(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Niter=800, adapt_reg=True,
+                        adapt_params=(1.1, 1.1)):
+    """optimize_pose (eval.py:320-409) with every iteration a graph replay.  The host only acts at
+    the schedule's decision points (i > 100 with (i+1) % 50 == 0, eval.py:389): it reads v_gamma,
+    applies the smoothing / nb_samples / lr update and re-captures.  Returns (best_log_rot, info)."""
+    from . import noise
+    dev = scene.device
+    sh = renderer.shader
+    _device_leaves(sh, dev)
+    seed = noise.DeviceSeed(dev)
+    noise.use_device_seed(seed)
+    log_rot = init_pose.clone().detach().to(dev).requires_grad_(True)
+    log_rot.grad = torch.zeros_like(log_rot)
+    st = dict(it=torch.zeros((), dtype=torch.int64, device=dev), losses=torch.zeros(Niter, device=dev),
+              gnorms=torch.zeros(Niter, device=dev), best_loss=torch.full((), float("inf"), device=dev),
+              best=log_rot.detach().clone(), v=torch.zeros(3, device=dev))
+    target = target_rgb[0]
+    lr = lr_init
+    opt = _fresh_adam(log_rot, lr)
+    pool = torch.cuda.graph_pool_handle()
+    step, step_post = None, None
+    i = 0
+    try:
+        while i < Niter:
+            post = adapt_reg and i > 100
+            if post:
+                end = min(Niter, i + (49 - i % 50) + 1)  # through the next i with (i+1) % 50 == 0
+            else:
+                end = min(Niter, 101) if adapt_reg else Niter
+            cur = step_post if post else step
+            if cur is None:
+                cur = _CapturedIteration(scene, renderer, target, log_rot, st, opt, post, seed, pool)
+                if post:
+                    step_post = cur
+                else:
+                    step = cur
+            cur.replay(end - i)
+            i = end
+            if post and i % 50 == 0:  # the last replayed iteration had (i+1) % 50 == 0
+                v_gamma = float(st["v"][1])
+                if v_gamma > 0:
+                    sigma, gamma, _ = sh.get_smoothing()
+                    s = max(float(sigma.detach()) / adapt_params[0], 5e-5)
+                    g = max(float(gamma.detach()) / adapt_params[1], 5e-4)
+                    renderer.rasterizer.raster_settings.blur_radius = BLUR_FACTOR * s
+                    with torch.no_grad():
+                        sh.smoothrast.sigma.fill_(s)
+                        sh.smoothagg.gamma.fill_(g)
+                        sh.smoothagg.alpha.fill_(1.0)
+                    sh.update_nb_samples(nb_samples=min(2 * sh.get_nb_samples(), 128))
+                    lr = max(lr / 1.5, 1e-4)
+                    opt = _fresh_adam(log_rot, lr)
+                    step_post = None  # S, blur and the optimizer changed: capture again
+                    torch.cuda.synchronize()
+    finally:
+        noise.use_device_seed(None)
+    torch.cuda.synchronize()
+    info = dict(loss_values=st["losses"].cpu().tolist(), gradient_values=st["gnorms"].cpu().tolist(),
+                nb_samples=sh.get_nb_samples())
+    return st["best"].detach().clone(), info
+
+
 def angle_deg(log_rot, R_true):
     return so3_relative_angle(so3_exponential_map(log_rot), R_true).detach().cpu().item() * 180.0 / np.pi
 
@@ -215,8 +364,7 @@ def run_problem(scene, problem, noise_type, sigma, gamma, nb_mc, pert, niter, ad
     for nt, renderer in zip(noise_type, renderers):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if mode == "graph" and nt != "softras":
-            from .pose_graph import optimize_pose_graph
+        if mode == "graph":
             log_rot, info = optimize_pose_graph(scene, log_rot_init, renderer, target_rgb, Niter=niter,
                                                 adapt_reg=adapt_reg, adapt_params=adapt_params)
         else:

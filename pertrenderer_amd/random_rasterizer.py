@@ -15,11 +15,12 @@ import torch
 import torch.nn as nn
 
 from . import blend as _blend
+from . import variants as _variants
 from .renderer.cameras import OpenGLPerspectiveCameras, look_at_view_transform
 from .renderer.blending import hard_rgb_blend, sigmoid_alpha_blend, softmax_rgb_blend  # noqa: F401
 from .renderer.mesh import TexturesVertex
 from .renderer.renderer import BlendParams, Materials, PointLights
-from .renderer.shading import phong_shading
+from .renderer.shading import phong_shading, textured_phong_shading  # noqa: F401
 from .smoothagg import GaussianAgg, SoftAgg, _PerturbedAgg
 from .smoothrast import GaussianRast, SoftRast, _PerturbedRast
 
@@ -35,6 +36,21 @@ def _variant_kw(smoothrast, smoothagg):
                 agg_kind=smoothagg.noise_kind, agg_vr=smoothagg.variance_reduction)
 
 
+_BG_CACHE = {}
+
+
+def _background_tensor(bg, device):
+    """blend_params.background_color as a device tensor, made once per (value, device): no host
+    copy per render (and none inside a captured graph)."""
+    if torch.is_tensor(bg):
+        return bg.to(device)
+    key = (tuple(float(v) for v in bg), str(device))
+    t = _BG_CACHE.get(key)
+    if t is None:
+        t = _BG_CACHE[key] = torch.tensor(key[0], dtype=torch.float32, device=device)
+    return t
+
+
 def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, znear=1.0, zfar=100):
     """(N,H,W,K,3) colours + Fragments -> (N,H,W,4) RGBA (random_rasterizer.py:34-56)."""
     N, H, W, K = fragments.pix_to_face.shape
@@ -46,13 +62,10 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
             smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
             eps=smoothagg.eps, background=background, znear=znear, zfar=zfar,
             fixed_noise=smoothagg.fixed_noise, **_variant_kw(smoothrast, smoothagg))
-    if not torch.is_tensor(background):
-        background = torch.tensor(background, dtype=torch.float32, device=device)
-    else:
-        background = background.to(device)
+    background = _background_tensor(background, device)
     mask = fragments.pix_to_face >= 0
     prob_map = smoothrast.rasterize(fragments.dists) * mask
-    alpha_chan = torch.prod(1.0 - prob_map, dim=-1)
+    alpha_chan = _variants.prod_last(1.0 - prob_map)  # torch.prod(., dim=-1), capture-safe backward
     weights = smoothagg.aggregate(fragments.zbuf, zfar, znear, prob_map, mask)
     rgb = (weights[..., :-1, None] * colors).sum(dim=-2) + weights[..., -1:] * background
     return torch.cat([rgb, (1.0 - alpha_chan)[..., None]], dim=-1)
@@ -120,12 +133,12 @@ class RandomPhongShader(_RandomShaderBase):
         if cameras is None:
             raise ValueError("Cameras must be specified either at initialization or in the forward "
                              "pass of RandomPhongShader")
-        texels = meshes.sample_textures(fragments)
         lights = kwargs.get("lights", self.lights)
         materials = kwargs.get("materials", self.materials)
         blend_params = kwargs.get("blend_params", self.blend_params)
-        colors = phong_shading(meshes=meshes, fragments=fragments, texels=texels, lights=lights,
-                               cameras=cameras, materials=materials)
+        # texels = meshes.sample_textures(fragments); colors = phong_shading(..., texels) -- one
+        # native kernel pair for TexturesUV / TexturesVertex (renderer/shading.py)
+        colors = textured_phong_shading(meshes, fragments, lights, cameras, materials)
         znear, zfar = _planes_from(cameras, kwargs)
         return smooth_rgb_blend(colors, fragments, self.smoothrast, self.smoothagg, blend_params,
                                 znear=znear, zfar=zfar)

@@ -188,8 +188,14 @@ class FoVPerspectiveCameras:
                             lambda: self.get_projection_transform().matrix)
 
     def get_camera_center(self, **kwargs):
-        w2v = self.get_world_to_view_transform(**kwargs).matrix
-        return torch.linalg.inv(w2v)[:, 3, :3]
+        """(N,3) camera centres: the translation row of the inverse world->view matrix.  Cached
+        while R/T are unchanged and need no gradient (no matrix inverse per render, and none inside
+        a captured graph)."""
+        if kwargs or self.R.requires_grad or self.T.requires_grad:
+            w2v = self.get_world_to_view_transform(**kwargs).matrix
+            return torch.linalg.inv(w2v)[:, 3, :3]
+        return self._cached("_center", ("R", "T"),
+                            lambda: torch.linalg.inv(self.world_to_view_matrix())[:, 3, :3])
 
 
 def OpenGLPerspectiveCameras(znear=1.0, zfar=100.0, aspect_ratio=1.0, fov=60.0, degrees=True, R=None, T=None,

@@ -8,7 +8,7 @@ import torch.nn as nn
 
 from .blending import hard_rgb_blend, sigmoid_alpha_blend, softmax_rgb_blend
 from .renderer import BlendParams, Materials, PointLights
-from .shading import phong_shading
+from .shading import textured_phong_shading
 
 
 class _ShaderBase(nn.Module):
@@ -30,10 +30,9 @@ class _ShaderBase(nn.Module):
         if cameras is None:
             raise ValueError(f"Cameras must be specified either at initialization or in the forward pass of "
                              f"{type(self).__name__}")
-        texels = meshes.sample_textures(fragments)
         lights = kwargs.get("lights", self.lights)
         materials = kwargs.get("materials", self.materials)
-        return cameras, phong_shading(meshes, fragments, lights, cameras, materials, texels)
+        return cameras, textured_phong_shading(meshes, fragments, lights, cameras, materials)
 
 
 class HardPhongShader(_ShaderBase):

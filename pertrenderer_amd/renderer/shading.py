@@ -1,10 +1,24 @@
-"""Phong shading of per-slot texels (PyTorch3D phong_shading, used by
-RandomPhongShader at random_rasterizer.py:103-110).  Pixel positions and normals
-are interpolated on the native pr_interp kernels; the lighting is elementwise."""
+"""Phong shading of per-slot texels (PyTorch3D 0.4.0 phong_shading, used by RandomPhongShader at
+random_rasterizer.py:103-110 and HardPhongShader for eval.py's targets).
+
+On ROCm tensors the whole per-slot computation -- position / normal interpolation, the texel
+lookup (TexturesUV bilinear map sampling, TexturesVertex interpolation, or given texels), the
+point / directional light terms and the specular highlight -- runs as one native kernel pair
+(pr_shade_fwd / pr_shade_bwd, csrc/pr_shade.hip) instead of ~60 elementwise torch kernels over
+(N,H,W,K,3) tensors.  Gradients reach the barycentrics (-> rasterizer), the vertex positions and
+normals, vertex colours / UV maps, the light position and the camera centre (eval.py's
+check_differentiability flows).  ``phong_shading_reference`` is the torch composition of the same
+formulas (PyTorch3D's op order); it serves inputs the kernel does not cover (gradients w.r.t. the
+light / material colours) and is the tests' reference.
+"""
 import torch
 import torch.nn.functional as Fn
 
+from .. import _native as nat
 from .interp import interpolate_vertex_attributes
+from .mesh import TexturesVertex
+
+F32 = torch.float32
 
 
 def _bc(t, like):
@@ -15,6 +29,12 @@ def _bc(t, like):
     return t.reshape((t.shape[0],) + (1,) * (like.dim() - 2))
 
 
+def _is_directional(lights):
+    from .renderer import DirectionalLights
+    return isinstance(lights, DirectionalLights)
+
+
+# ------------------------------------------------------------ torch composition
 def _diffuse(normals, color, direction):
     n = Fn.normalize(normals, p=2, dim=-1, eps=1e-6)
     d = Fn.normalize(direction, p=2, dim=-1, eps=1e-6)
@@ -33,18 +53,19 @@ def _specular(points, normals, direction, camera_position, color, shininess):
     return _bc(color, points) * torch.pow(alpha, _bc(shininess, alpha))[..., None]
 
 
-def phong_shading(meshes, fragments, lights, cameras, materials, texels):
+def phong_shading_reference(meshes, fragments, lights, cameras, materials, texels):
+    """PyTorch3D phong_shading as torch ops: (ambient + diffuse) * texels + specular."""
     verts = meshes.verts_packed()
     faces = meshes.faces_packed()
     vnormals = meshes.verts_normals_packed()
     coords = interpolate_vertex_attributes(fragments.pix_to_face, fragments.bary_coords, verts, faces)
     normals = interpolate_vertex_attributes(fragments.pix_to_face, fragments.bary_coords, vnormals, faces)
-    if hasattr(lights, "light_direction"):
-        direction = lights.light_direction(coords)
-    else:
-        direction = _bc(lights.location, coords) - coords
     N = coords.shape[0]
     expand = lambda t: t.expand(N, -1) if t.shape[0] == 1 else t
+    if _is_directional(lights):
+        direction = _bc(expand(lights.location), coords).expand_as(coords)
+    else:
+        direction = _bc(expand(lights.location), coords) - coords
     diffuse = _diffuse(normals, expand(lights.diffuse_color), direction)
     specular = _specular(coords, normals, direction, expand(cameras.get_camera_center()),
                          expand(lights.specular_color), expand(materials.shininess.reshape(-1)))
@@ -52,3 +73,132 @@ def phong_shading(meshes, fragments, lights, cameras, materials, texels):
     diffuse = _bc(expand(materials.diffuse_color), coords) * diffuse
     specular = _bc(expand(materials.specular_color), coords) * specular
     return (ambient + diffuse) * texels + specular
+
+
+# ------------------------------------------------------------------ native path
+class _ShadeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, bary, verts, normals, tex, light, camera, cfg):
+        nat.require_device(bary, verts, normals, tex, light, camera)
+        lib = nat.load()
+        N, H, W, K = cfg["p2f"].shape
+        keep = dict(bary=bary.detach().to(F32).contiguous(), verts=verts.detach().to(F32).contiguous(),
+                    normals=normals.detach().to(F32).contiguous(), tex=tex.detach().to(F32).contiguous(),
+                    light=light.detach().to(F32).contiguous(), camera=camera.detach().to(F32).contiguous())
+        colors = torch.empty((N, H, W, K, 3), dtype=F32, device=bary.device)
+        a = _args(cfg, keep)
+        a.colors = nat.ptr(colors)
+        nat.check(lib.pr_shade_fwd(a, nat.stream_of(colors)), "pr_shade_fwd")
+        ctx.save_for_backward(*keep.values())
+        ctx.cfg = cfg
+        return colors
+
+    @staticmethod
+    def backward(ctx, gcol):
+        bary, verts, normals, tex, light, camera = ctx.saved_tensors
+        keep = dict(bary=bary, verts=verts, normals=normals, tex=tex, light=light, camera=camera)
+        cfg = ctx.cfg
+        lib = nat.load()
+        need = ctx.needs_input_grad
+        g = gcol.detach().to(F32).contiguous()
+        a = _args(cfg, keep)
+        a.grad_colors = nat.ptr(g)
+        out = [torch.empty_like(t) if need[i] else None
+               for i, t in enumerate((bary, verts, normals, tex, light, camera))]
+        gb, gv, gn, gt, gl, gc = out
+        a.grad_bary, a.grad_verts, a.grad_normals = nat.ptr(gb), nat.ptr(gv), nat.ptr(gn)
+        if cfg["mode"] == nat.PR_TEX_GIVEN:
+            a.grad_texels = nat.ptr(gt)
+        elif cfg["mode"] == nat.PR_TEX_VERTEX:
+            a.grad_vert_colors = nat.ptr(gt)
+        else:
+            a.grad_maps = nat.ptr(gt)
+        a.grad_light, a.grad_camera = nat.ptr(gl), nat.ptr(gc)
+        nat.check(lib.pr_shade_bwd(a, nat.stream_of(g)), "pr_shade_bwd")
+        return gb, gv, gn, gt, gl, gc, None
+
+
+def _args(cfg, t):
+    a = nat.PRShadeArgs()
+    N, H, W, K = cfg["p2f"].shape
+    a.N, a.H, a.W, a.K = N, H, W, K
+    a.pix_to_face, a.pix_count, a.faces = nat.ptr(cfg["p2f"]), nat.ptr(cfg["counts"]), nat.ptr(cfg["faces"])
+    a.bary, a.verts, a.normals = nat.ptr(t["bary"]), nat.ptr(t["verts"]), nat.ptr(t["normals"])
+    a.V, a.F = t["verts"].shape[0], cfg["faces"].shape[0]
+    a.texture = cfg["mode"]
+    if cfg["mode"] == nat.PR_TEX_GIVEN:
+        a.texels = nat.ptr(t["tex"])
+    elif cfg["mode"] == nat.PR_TEX_VERTEX:
+        a.vert_colors = nat.ptr(t["tex"])
+    else:
+        a.maps, a.face_uvs = nat.ptr(t["tex"]), nat.ptr(cfg["face_uvs"])
+        a.Hm, a.Wm = t["tex"].shape[1], t["tex"].shape[2]
+    a.directional = int(cfg["directional"])
+    a.light, a.camera = nat.ptr(t["light"]), nat.ptr(t["camera"])
+    for k in ("ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular", "shininess"):
+        setattr(a, k, nat.ptr(cfg[k]))
+    return a
+
+
+def _rows(t, N, device):
+    """(1|N, C) or (1|N,) -> contiguous (N, C) / (N,) float32 rows on `device`."""
+    t = t.to(device=device, dtype=F32)
+    t = t.reshape(t.shape[0], -1) if t.dim() >= 1 else t.reshape(1, 1)
+    if t.shape[0] == 1:
+        t = t.expand(N, t.shape[1])
+    return t
+
+
+def _native_ok(fragments, lights, materials):
+    if not fragments.pix_to_face.is_cuda:
+        return False
+    fixed = [lights.ambient_color, lights.diffuse_color, lights.specular_color, materials.ambient_color,
+             materials.diffuse_color, materials.specular_color, materials.shininess]
+    return not any(torch.is_tensor(x) and x.requires_grad for x in fixed)
+
+
+def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face_uvs=None):
+    from .rasterizer import valid_counts
+    p2f = fragments.pix_to_face
+    N = p2f.shape[0]
+    dev = p2f.device
+    counts = valid_counts(p2f)
+    if counts is not None and (counts.device != dev or tuple(counts.shape) != tuple(p2f.shape[:3])):
+        counts = None
+    verts = meshes.verts_packed()
+    faces = meshes.faces_packed().to(torch.int64).contiguous()
+    rows = lambda x: _rows(x, N, dev).contiguous()
+    cfg = dict(p2f=p2f.detach().to(torch.int64).contiguous(), counts=counts, faces=faces, mode=mode,
+               face_uvs=face_uvs, directional=_is_directional(lights),
+               ambient=rows(materials.ambient_color * lights.ambient_color),
+               diffuse_color=rows(lights.diffuse_color), specular_color=rows(lights.specular_color),
+               mat_diffuse=rows(materials.diffuse_color), mat_specular=rows(materials.specular_color),
+               shininess=rows(materials.shininess.reshape(-1, 1)).reshape(N).contiguous())
+    light = _rows(lights.location, N, dev)
+    camera = _rows(cameras.get_camera_center(), N, dev)
+    return _ShadeFn.apply(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg)
+
+
+def phong_shading(meshes, fragments, lights, cameras, materials, texels):
+    """PyTorch3D phong_shading(meshes, fragments, lights, cameras, materials, texels)."""
+    if _native_ok(fragments, lights, materials):
+        return _shade_native(meshes, fragments, lights, cameras, materials, nat.PR_TEX_GIVEN, texels)
+    return phong_shading_reference(meshes, fragments, lights, cameras, materials, texels)
+
+
+def textured_phong_shading(meshes, fragments, lights, cameras, materials):
+    """phong_shading(..., texels=meshes.sample_textures(fragments)) with the texel lookup fused
+    into the shading kernel for TexturesUV (maps of one size) and 3-channel TexturesVertex."""
+    from .textures import TexturesUV
+    tex = getattr(meshes, "textures", None)
+    if _native_ok(fragments, lights, materials):
+        if isinstance(tex, TexturesUV) and tex.fusable():
+            maps = tex.maps_padded().to(fragments.pix_to_face.device)
+            if maps.shape[0] == fragments.pix_to_face.shape[0] and maps.shape[-1] == 3:
+                fuv = tex.faces_verts_uvs_packed().to(device=maps.device, dtype=F32).detach().contiguous()
+                return _shade_native(meshes, fragments, lights, cameras, materials, nat.PR_TEX_UV, maps, fuv)
+        if isinstance(tex, TexturesVertex):
+            vc = tex.verts_features_packed()
+            if vc.dim() == 2 and vc.shape[-1] == 3:
+                return _shade_native(meshes, fragments, lights, cameras, materials, nat.PR_TEX_VERTEX, vc)
+    return phong_shading(meshes, fragments, lights, cameras, materials, meshes.sample_textures(fragments))

@@ -44,12 +44,19 @@ class TexturesUV:
     def verts_uvs_list(self):
         return self._verts_uvs
 
-    def _faces_verts_uvs_packed(self):
+    def faces_verts_uvs_packed(self):
         return torch.cat([vu[fu] for vu, fu in zip(self._verts_uvs, self._faces_uvs)], 0)   # (F,3,2)
+
+    def fusable(self):
+        """The native shading kernel samples these maps itself: bilinear, align_corners, border
+        padding, one map size, UVs without gradient (the maps may require one)."""
+        return (self.align_corners and self.padding_mode == "border"
+                and len({tuple(m.shape) for m in self._maps}) == 1
+                and not any(t.requires_grad for t in self._verts_uvs))
 
     def sample_textures(self, fragments, faces_packed=None, **kwargs):
         p2f, bary = fragments.pix_to_face, fragments.bary_coords
-        uv = interpolate_face_attributes(p2f, bary, self._faces_verts_uvs_packed().to(bary.device))
+        uv = interpolate_face_attributes(p2f, bary, self.faces_verts_uvs_packed().to(bary.device))
         N, Ho, Wo, K = p2f.shape
         maps = self.maps_padded().to(bary.device)
         C = maps.shape[-1]

@@ -44,6 +44,34 @@ class _ProdC(torch.autograd.Function):
         return dx, dy
 
 
+class _ProdLast(torch.autograd.Function):
+    """torch.prod(x, dim=-1) with torch's own backward values (grad * result / x when the
+    tensor holds no zero, else the exclusive-cumprod form of prod_safe_zeros_backward) chosen
+    on the device: torch's prod backward reads the zero count on the host (.item()), which a
+    captured graph cannot do."""
+
+    @staticmethod
+    def forward(ctx, x):
+        out = torch.prod(x, dim=-1)
+        ctx.save_for_backward(x, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, out = ctx.saved_tensors
+        g, out = g.unsqueeze(-1), out.unsqueeze(-1)
+        plain = g * (out / x)
+        ones = torch.ones_like(x[..., :1])
+        excl_fwd = torch.cat([ones, x[..., :-1]], dim=-1).cumprod(-1)
+        excl_rev = torch.cat([ones, x[..., 1:].flip(-1)], dim=-1).cumprod(-1).flip(-1)
+        safe = g * (excl_fwd * excl_rev)
+        return torch.where((x == 0).sum() == 0, plain, safe)
+
+
+def prod_last(x):
+    return _ProdLast.apply(x)
+
+
 def log_corrected(x):
     return _LogC.apply(x)
 

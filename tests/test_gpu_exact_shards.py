@@ -44,18 +44,20 @@ def _worker(rank, world, port, S, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from pertrenderer_amd import Noise, perturbed_blend
-        from pertrenderer_amd.parallel import exact_sharded_blend
+        from pertrenderer_amd.parallel import exact_sharded_blend, reduce_scalar_grads
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
         p2f, d, z, c, gimg, (s, gm, al), S = _inputs(dev, S)
         img = exact_sharded_blend(c, p2f, d, z, s, gm, al, S, S, SEEDS[0], SEEDS[1], background=(0.1, 0.2, 0.3))
         (img * gimg).sum().backward()
+        reduce_scalar_grads([s, gm, al])
         out = dict(image=img.detach().cpu(), dists=d.grad.cpu(), zbuf=z.grad.cpu(), colors=c.grad.cpu(),
                    scalars=torch.stack([s.grad, gm.grad, al.grad]))
         # a second backward without zeroing (eval.py never zeroes the smoothing leaves): the
         # leaves accumulate exactly twice the one-backward gradient, as in one process
         img = exact_sharded_blend(c, p2f, d, z, s, gm, al, S, S, SEEDS[0], SEEDS[1], background=(0.1, 0.2, 0.3))
         (img * gimg).sum().backward()
+        reduce_scalar_grads([s, gm, al])
         out["scalars2"] = torch.stack([s.grad, gm.grad, al.grad])
         if world == 1:  # the fused kernel pair with the same keys
             p2f, d, z, c, gimg, (s, gm, al), S = _inputs(dev, S)

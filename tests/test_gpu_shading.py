@@ -1,0 +1,168 @@
+"""Native Phong shading (pr_shade_fwd / pr_shade_bwd) against the PyTorch3D phong_shading
+composition (renderer.shading.phong_shading_reference: the same formulas as torch ops, PyTorch3D's
+op order) evaluated in float64, for the three texel sources: given texels, TexturesVertex and
+TexturesUV (bilinear map lookup).  Gradients: vertex positions (through both the shading and the
+rasterizer's barycentrics), vertex colours, UV maps, the light position and the camera centre --
+the parameters eval.py's check_differentiability optimises (eval.py:693-725)."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from conftest import ROOT
+from pertrenderer_amd.renderer import (FoVPerspectiveCameras, Materials, MeshRasterizer, Meshes, PointLights,
+                                       RasterizationSettings, TexturesUV, TexturesVertex, load_obj,
+                                       look_at_view_transform)
+from pertrenderer_amd.renderer import shading as sh
+from pertrenderer_amd.renderer.renderer import DirectionalLights
+
+pytestmark = pytest.mark.gpu
+
+
+def _interp64(p2f, bary, attr, faces):
+    """interpolate_face_attributes in float64 torch (0 on padded slots)."""
+    mask = (p2f >= 0)[..., None]
+    fa = attr[faces[p2f.clamp(min=0)]]  # (...,3,D)
+    out = (bary[..., 0:1] * fa[..., 0, :] + bary[..., 1:2] * fa[..., 1, :]) + bary[..., 2:3] * fa[..., 2, :]
+    return out * mask
+
+
+def _uv_sample64(p2f, bary, tex):
+    uv = _interp64(p2f, bary, torch.cat([tex.verts_uvs_list()[0]]), tex.faces_uvs_list()[0])
+    N, Ho, Wo, K = p2f.shape
+    maps = tex.maps_padded().double()
+    m = torch.flip(maps.permute(0, 3, 1, 2), [2])
+    g = uv.reshape(N, Ho, Wo * K, 2) * 2.0 - 1.0
+    t = Fn.grid_sample(m, g, align_corners=True, padding_mode="border")
+    return t.reshape(N, 3, Ho, Wo, K).permute(0, 2, 3, 4, 1)
+
+
+def _reference64(mesh, frag, lights, cams, mats, texels):
+    d = lambda t: t.double()
+    verts, faces = d(mesh.verts_packed()), mesh.faces_packed()
+    # area-weighted vertex normals in float64 (Meshes.verts_normals_packed)
+    fv = verts[faces]
+    n = torch.zeros_like(verts)
+    n = n.index_add(0, faces[:, 1], torch.cross(fv[:, 2] - fv[:, 1], fv[:, 0] - fv[:, 1], dim=1))
+    n = n.index_add(0, faces[:, 2], torch.cross(fv[:, 0] - fv[:, 2], fv[:, 1] - fv[:, 2], dim=1))
+    n = n.index_add(0, faces[:, 0], torch.cross(fv[:, 1] - fv[:, 0], fv[:, 2] - fv[:, 0], dim=1))
+    vn = Fn.normalize(n, eps=1e-6, dim=1)
+    p2f, bary = frag.pix_to_face, d(frag.bary_coords)
+    coords, normals = _interp64(p2f, bary, verts, faces), _interp64(p2f, bary, vn, faces)
+    N = coords.shape[0]
+    e = lambda t: d(t).expand(N, -1) if t.shape[0] == 1 else d(t)
+    if isinstance(lights, DirectionalLights):
+        direction = sh._bc(e(lights.location), coords).expand_as(coords)
+    else:
+        direction = sh._bc(e(lights.location), coords) - coords
+    diffuse = sh._diffuse(normals, e(lights.diffuse_color), direction)
+    specular = sh._specular(coords, normals, direction, e(cams.get_camera_center()), e(lights.specular_color),
+                            e(mats.shininess.reshape(-1, 1)).reshape(-1))
+    ambient = sh._bc(e(mats.ambient_color * lights.ambient_color), coords)
+    return (ambient + sh._bc(e(mats.diffuse_color), coords) * diffuse) * d(texels) \
+        + sh._bc(e(mats.specular_color), coords) * specular
+
+
+def _scene(device, kind, light_kind="point", size=48, K=12):
+    torch.manual_seed(3)
+    if kind == "uv":
+        from pertrenderer_amd.pose_opt import load_cube
+        mesh = load_cube(device)
+        tex = mesh.textures
+        verts = mesh.verts_packed().clone()
+        faces = mesh.faces_packed()
+        maps = tex.maps_padded().clone().requires_grad_(True)
+        tex = TexturesUV(maps, [tex.faces_uvs_list()[0]], [tex.verts_uvs_list()[0]])
+        extra = maps
+    else:
+        v, f, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
+        verts, faces = v.to(device), f.verts_idx.to(device)
+        extra = torch.rand((verts.shape[0], 3), device=device).requires_grad_(True)
+        tex = TexturesVertex([extra])
+    verts = (verts - verts.mean(0)).requires_grad_(True)
+    mesh = Meshes([verts], [faces], tex)
+    R, T = look_at_view_transform(2.2 if kind != "uv" else 3.0, 25.0, 40.0, device=device)
+    cams = FoVPerspectiveCameras(R=R, T=T, device=device)
+    loc = torch.tensor([[0.5, 2.0, -2.0]] if light_kind == "point" else [[0.3, 1.0, 0.4]], device=device,
+                       requires_grad=True)
+    lights = (PointLights(device=device, location=loc) if light_kind == "point"
+              else DirectionalLights(device=device, direction=loc))
+    lights.location = loc  # keep the leaf (PointLights stores a reshaped view)
+    mats = Materials(device=device, shininess=32)
+    rs = RasterizationSettings(image_size=size, blur_radius=math.log(1e4 - 1) * 1e-3, faces_per_pixel=K)
+    frag = MeshRasterizer(cameras=cams, raster_settings=rs)(mesh)
+    return mesh, frag, lights, cams, mats, verts, loc, extra
+
+
+def _grads(out, G, leaves):
+    gs = torch.autograd.grad((out * G).sum(), leaves, allow_unused=True, retain_graph=True)
+    return [torch.zeros_like(l) if g is None else g for g, l in zip(gs, leaves)]
+
+
+def _close(a, b, rtol, name):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    scale = float(b.abs().max())
+    err = float((a - b).abs().max())
+    assert err <= rtol * max(scale, 1e-12), (name, err, scale)
+
+
+@pytest.mark.parametrize("kind,light_kind", [("vertex", "point"), ("uv", "point"), ("given", "point"),
+                                             ("vertex", "directional")])
+def test_native_shading_matches_float64_reference(kind, light_kind, device):
+    mesh, frag, lights, cams, mats, verts, loc, extra = _scene(device, kind, light_kind)
+    valid = (frag.pix_to_face >= 0).sum()
+    assert valid > 500
+    if kind == "given":
+        texels = mesh.sample_textures(frag).detach().requires_grad_(True)
+        out = sh.phong_shading(mesh, frag, lights, cams, mats, texels)
+        leaves = [verts, loc, texels]
+        ref_tex = texels
+    else:
+        out = sh.textured_phong_shading(mesh, frag, lights, cams, mats)
+        leaves = [verts, loc, extra]
+        ref_tex = (_uv_sample64(frag.pix_to_face, frag.bary_coords.double(), mesh.textures) if kind == "uv"
+                   else _interp64(frag.pix_to_face, frag.bary_coords.double(), extra.double(), mesh.faces_packed()))
+    ref = _reference64(mesh, frag, lights, cams, mats, ref_tex)
+    _close(out, ref, 5e-6, "colors")  # fp32 kernel vs the fp64 composition
+    G = torch.randn(out.shape, device=device, generator=torch.Generator(device).manual_seed(5))
+    # only valid slots carry gradient in the renderer (the blend's weights are 0 elsewhere)
+    G = G * (frag.pix_to_face >= 0)[..., None]
+    got = _grads(out, G, leaves)
+    exp = _grads(ref, G.double(), leaves)
+    for name, a, b in zip(("verts", "light", "texture"), got, exp):
+        _close(a, b, 2e-4, name)
+
+
+def test_native_shading_camera_gradient(device):
+    """d colour / d camera centre through the specular term (camera parameters with grad take the
+    transform path of MeshRasterizer: eval.py's camera check)."""
+    mesh, frag, lights, cams, mats, verts, loc, extra = _scene(device, "vertex")
+    T = cams.T.clone().requires_grad_(True)
+    cams.T = T
+    out = sh.textured_phong_shading(mesh, frag, lights, cams, mats)
+    ref = _reference64(mesh, frag, lights, cams, mats,
+                       _interp64(frag.pix_to_face, frag.bary_coords.double(), extra.double(), mesh.faces_packed()))
+    G = torch.randn(out.shape, device=device) * (frag.pix_to_face >= 0)[..., None]
+    (ga,) = torch.autograd.grad((out * G).sum(), [T], retain_graph=True)
+    (gb,) = torch.autograd.grad((ref * G.double()).sum(), [T])
+    _close(ga, gb, 2e-4, "camera T")
+    assert float(ga.abs().sum()) > 0
+
+
+def test_renderer_uses_native_shading(device):
+    """RandomPhongShader / HardPhongShader route TexturesUV and TexturesVertex through pr_shade."""
+    import pertrenderer_amd.renderer.shading as shm
+    calls = []
+    orig = shm._ShadeFn.apply
+    try:
+        shm._ShadeFn.apply = lambda *a: calls.append(a[-1]["mode"]) or orig(*a)
+        mesh, frag, lights, cams, mats, *_ = _scene(device, "uv")
+        from pertrenderer_amd.renderer import HardPhongShader
+        HardPhongShader(device=device, cameras=cams, lights=lights)(frag, mesh)
+    finally:
+        shm._ShadeFn.apply = orig
+    from pertrenderer_amd import _native as nat
+    assert calls == [nat.PR_TEX_UV]

@@ -48,7 +48,7 @@ STRUCTS = {
     "PRBlendParams": nat.PRBlendParams, "PRBlendFwdArgs": nat.PRBlendFwdArgs,
     "PRBlendBwdArgs": nat.PRBlendBwdArgs, "PRHeavisideArgs": nat.PRHeavisideArgs,
     "PRRastArgs": nat.PRRastArgs, "PRInterpArgs": nat.PRInterpArgs, "PRProjectArgs": nat.PRProjectArgs,
-    "PRSO3Args": nat.PRSO3Args, "PRRotateArgs": nat.PRRotateArgs,
+    "PRSO3Args": nat.PRSO3Args, "PRRotateArgs": nat.PRRotateArgs, "PRShadeArgs": nat.PRShadeArgs,
 }
 
 

@@ -83,12 +83,16 @@ def _worker(rank, world, port, q):
         P_ref = 0.5 * (xr ** 2 + xr ** 3)
         g_ref = torch.cos(P_ref) * c * 0.5 * (2 * xr + 3 * xr ** 2)
         ok4 = torch.allclose(P.detach(), P_ref, atol=1e-6) and torch.allclose(x.grad, g_ref, atol=1e-6)
-        # 5) a CPU 0-d leaf (the reference's sigma) through _SumBackward: one complete sum per
-        #    backward, accumulated like a local gradient (no re-reduction of earlier steps)
+        # 5) reduce_scalar_grads on a never-zeroed CPU 0-d leaf (the reference's sigma): each call
+        #    completes only this backward's partial, so the leaf accumulates like one process
+        from pertrenderer_amd.parallel import reduce_scalar_grads
         sg = torch.tensor(2.0, requires_grad=True)
-        for _ in range(2):
-            (_SumBackward.apply(sg, None) * float(rank + 1)).backward()
-        ok5 = sg.grad.device.type == "cpu" and abs(float(sg.grad) - 2 * 3.0) < 1e-6
+        vals = []
+        for _ in range(3):
+            (sg * float(rank + 1)).backward()
+            reduce_scalar_grads([sg])
+            vals.append(float(sg.grad))
+        ok5 = sg.grad.device.type == "cpu" and np.allclose(vals, [3.0, 6.0, 9.0])
         ok4 = ok4 and ok5
         q.put((rank, bool(ok1), bool(ok2 and ok3 and ok4)))
     finally:
