@@ -1,26 +1,30 @@
 """Benchmark of the perturbed-renderer hot path (BASELINE.json configs[1]).
 
-One step = one pose-optimisation iteration of experiments/eval.py:343-376: rotate
-the mesh (so3 exp map), MeshRasterizer (native K-nearest rasterizer, 256x256,
-faces_per_pixel=50, blur = ln(1/1e-4 - 1)*sigma), RandomSimpleShader with
-GaussianRast(nb_samples=8) + GaussianAgg(nb_samples=8) (fused native blend with
-TexturesVertex sampling), L2 loss to a fixed synthetic target, backward through
-blend -> rasterizer -> vertices -> pose, Adam step on the pose (lr 5e-2, eval.py:337).
-With N ranks the Monte-Carlo sample
-dimension is sharded (BASELINE north star): every rank renders the SAME frame and
-pose with its own disjoint range of global sample indices (Philox offset rank*S),
-and one RCCL all-reduce averages the gradient estimates, i.e. each step is one
-pose update from an (N*8)-sample estimator.  Per-GPU work is fixed (one 8-sample
-render per rank per step): weak scaling; `value` counts renders over all ranks.
+One step = one pose-optimisation iteration of experiments/eval.py:343-376: rotate the mesh
+(so3 exp map), MeshRasterizer (native K-nearest rasterizer, 256x256, faces_per_pixel=50,
+blur = ln(1/1e-4 - 1)*sigma), RandomSimpleShader with GaussianRast(nb_samples=8) +
+GaussianAgg(nb_samples=8) (fused native blend with TexturesVertex sampling), L2 loss to a fixed
+synthetic target, backward through blend -> rasterizer -> vertices -> pose, Adam step on the
+pose (lr 5e-2, eval.py:337).  The whole step is one captured HIP graph.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|eval]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
-Prints ONE JSON line on rank 0.  `value` = frames/s over all ranks (forward +
-backward per frame); `roofline` is the dominant native kernel's algorithmic HBM
-bytes / its mean HIP-event duration inside the timed region; `cpu_baseline` times
-the CPU oracle (test-infrastructure restatement of the reference + PyTorch3D
-rasterizer) on a bounded sample of the same workload, on rank 0 at N=1.
+Multi-GPU (--shard):
+  frames  (default at N > 1, weak scaling): every rank renders its OWN view of the shared pose
+          (camera azimuth 120 + 360 r / N: a multi-view pose optimisation step) and one RCCL
+          all-reduce averages the pose / smoothing gradients.  value = distinct frames / s.
+  samples (strong scaling): every rank renders the same frame with its shard of the config's
+          Monte-Carlo samples (parallel.sample_shard: global sample offsets, shared Philox keys)
+          and the all-reduce forms the full-S gradient estimate (weights n_r / S).  value =
+          distinct frames / s (each frame counted once).
+
+Prints ONE JSON line on rank 0: `value` = frames/s (forward + backward per frame) over all
+ranks; `ms_forward` / `ms_backward` = HIP events around separately captured forward and
+backward(+Adam) graphs replayed right after the timed region; `roofline` is the dominant native
+call's algorithmic HBM bytes / its HIP-event duration; `cpu_baseline` times the CPU oracle
+(test-infrastructure restatement of the reference + PyTorch3D rasterizer) on a bounded sample of
+the same workload, on rank 0 at N=1, with every CPU this process may use.
 """
 import argparse
 import json
@@ -40,7 +44,7 @@ import pertrenderer_amd as pa  # noqa: E402
 from pertrenderer_amd.renderer import (FoVPerspectiveCameras, MeshRasterizer, MeshRenderer, Meshes,  # noqa: E402
                                        RasterizationSettings, TexturesVertex, load_obj, look_at_view_transform)
 from pertrenderer_amd.renderer.transforms import Rotate, so3_exponential_map  # noqa: E402
-from pertrenderer_amd.parallel import average_gradients  # noqa: E402
+from pertrenderer_amd.parallel import average_gradients, sample_shard  # noqa: E402
 from pertrenderer_amd.timing import KernelTimer  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
@@ -61,43 +65,57 @@ def load_sphere(device):
 
 
 # BASELINE.json configs: cfg2 is the headline (metric's) workload; cfg3/cfg4 are the batch
-# configurations (16 meshes alternating sphere_642 / cube2, each with its own pose)
+# configurations (16 meshes alternating sphere_642 / cube2, each with its own pose); "eval" is
+# eval.py's own renderer (textured cube, RandomPhongShader, GaussianRast's default Sr=16, Sa=8)
 CONFIGS = {
     "cfg2": dict(batch=1, image_size=256, K=50, samples=8),
     "cfg3": dict(batch=16, image_size=256, K=100, samples=16),
     "cfg4": dict(batch=16, image_size=512, K=150, samples=64),
+    "eval": dict(batch=1, image_size=256, K=50, samples=8, rast_samples=16),
 }
 
 
 class Workload:
     def __init__(self, device, image_size=256, K=50, samples=8, sigma=1e-3, gamma=1e-2, dist_cam=2.7, seed=0,
-                 batch=1):
+                 batch=1, azim=120.0, rast_samples=None, eval_scene=False):
         self.device = device
         g = torch.Generator().manual_seed(seed)
-        vl, fl, cl = [], [], []
-        for i in range(batch):
-            verts, faces = load_mesh(device, "sphere_642.obj" if i % 2 == 0 else "cube2.obj")
-            vl.append(verts)
-            fl.append(faces)
-            cl.append(torch.rand((verts.shape[0], 3), generator=g).to(device))
-        self.base = Meshes(vl, fl, TexturesVertex(cl))
-        faces = torch.cat(fl)
-        R, T = look_at_view_transform(dist_cam, 30.0, 120.0, device=device)
-        self.cameras = FoVPerspectiveCameras(R=R, T=T, device=device, fov=60.0)
+        Sr = samples if rast_samples is None else rast_samples
+        blend = pa.random_rasterizer.BlendParams(sigma, gamma, (0.0, 0.0, 0.0))
+        self.rast = pa.GaussianRast(nb_samples=Sr, sigma=sigma)
+        self.agg = pa.GaussianAgg(nb_samples=samples, gamma=gamma, alpha=1.0)
         self.settings = RasterizationSettings(image_size=image_size,
                                               blur_radius=math.log(1.0 / 1e-4 - 1.0) * sigma,
                                               faces_per_pixel=K, max_faces_per_bin=50000,
                                               perspective_correct=False)
-        self.rast = pa.GaussianRast(nb_samples=samples, sigma=sigma)
-        self.agg = pa.GaussianAgg(nb_samples=samples, gamma=gamma, alpha=1.0)
-        self.renderer = MeshRenderer(
-            rasterizer=MeshRasterizer(cameras=self.cameras, raster_settings=self.settings),
-            shader=pa.RandomSimpleShader(device=device, cameras=self.cameras, smoothrast=self.rast,
-                                         smoothagg=self.agg,
-                                         blend_params=pa.random_rasterizer.BlendParams(sigma, gamma, (0.0, 0.0, 0.0))))
+        if eval_scene:  # eval.py:124-180, 727-757: textured cube, Phong, camera at 6.7
+            from pertrenderer_amd import pose_opt
+            scene = pose_opt.Scene(device, image_size)
+            self.base, self.lights = scene.meshes, scene.lights
+            R, T = look_at_view_transform(6.7, 30.0, azim, device=device)
+            self.cameras = FoVPerspectiveCameras(R=R, T=T, device=device, fov=60.0)
+            shader = pa.RandomPhongShader(device=device, cameras=self.cameras, lights=self.lights,
+                                          smoothrast=self.rast, smoothagg=self.agg, blend_params=blend)
+            faces = self.base.faces_packed()
+        else:
+            vl, fl, cl = [], [], []
+            for i in range(batch):
+                verts, faces = load_mesh(device, "sphere_642.obj" if i % 2 == 0 else "cube2.obj")
+                vl.append(verts)
+                fl.append(faces)
+                cl.append(torch.rand((verts.shape[0], 3), generator=g).to(device))
+            self.base = Meshes(vl, fl, TexturesVertex(cl))
+            faces = torch.cat(fl)
+            R, T = look_at_view_transform(dist_cam, 30.0, azim, device=device)
+            self.cameras = FoVPerspectiveCameras(R=R, T=T, device=device, fov=60.0)
+            self.lights = None
+            shader = pa.RandomSimpleShader(device=device, cameras=self.cameras, smoothrast=self.rast,
+                                           smoothagg=self.agg, blend_params=blend)
+        self.renderer = MeshRenderer(rasterizer=MeshRasterizer(cameras=self.cameras, raster_settings=self.settings),
+                                     shader=shader)
         self.log_rot = (0.3 * torch.randn((batch, 3), generator=g)).to(device).requires_grad_(True)
         self.target = torch.rand((batch, image_size, image_size, 3), generator=g).to(device)
-        self.K, self.S, self.H, self.batch = K, samples, image_size, batch
+        self.K, self.S, self.Sr, self.H, self.batch = K, samples, Sr, image_size, batch
         self.F = faces.shape[0]
 
     def params(self):
@@ -111,18 +129,13 @@ class Workload:
     def forward(self):
         R = so3_exponential_map(self.log_rot)
         mesh = self.base.update_padded(Rotate(R).transform_points(self.base.verts_padded()))
-        images = self.renderer(mesh, cameras=self.cameras)
+        kw = {"lights": self.lights} if self.lights is not None else {}
+        images = self.renderer(mesh, cameras=self.cameras, **kw)
         return ((images[..., :3] - self.target) ** 2).mean()
 
     def zero_grad(self):
         for p in self.params():
             p.grad = None
-
-
-def allreduce_grads(params, world):
-    """The single gradient reduction of the data-parallel step: one flattened RCCL
-    all-reduce of every gradient, averaged over ranks (pertrenderer_amd.parallel)."""
-    average_gradients(params)
 
 
 def kernel_bytes(name, P, K, S, F):
@@ -163,13 +176,36 @@ def dense_roofline(device, P_side=256, K=50, S=8, iters=20):
     return out
 
 
+# ------------------------------------------------------------------ CPU baseline
+def host_cpus():
+    """(threads this process may use, logical CPUs of the machine, CPU model): the affinity
+    set, capped by the cgroup CPU quota when one is set."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            avail = max(1, min(avail, int(math.ceil(int(quota) / int(period)))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return avail, os.cpu_count() or avail, model
+
+
 def cpu_baseline(frames, threads):
     """CPU oracle of one step of the same workload (rasterizer in C/OpenMP, blend in torch-CPU)."""
+    os.environ["OMP_NUM_THREADS"] = str(threads)  # the C oracle's OpenMP runtime reads it when loaded
     from oracle import blend_oracle as bo
     from oracle import rast_ref
     torch.set_num_threads(threads)
-    dev = torch.device("cpu")
     wl = WorkloadCPU()
+    wl.step(bo, rast_ref, 0)  # warm-up (library load, allocations): not timed
     t0 = time.perf_counter()
     for i in range(frames):
         wl.step(bo, rast_ref, i)
@@ -218,7 +254,8 @@ class WorkloadCPU:
         rast_ref.rast_bwd(fv, p2f, g["zbuf"].numpy(), gbary.astype(np.float32), g["dists"].numpy(), False, True)
 
 
-def build_step(wl, world, mode, device):
+# ------------------------------------------------------------------ the step
+def build_step(wl, world, mode, device, grad_weight):
     """Returns step() for eager or HIP-graph mode.  A step is one full pose-optimisation
     iteration of eval.py:343-376: forward, loss, backward, (N>1: the gradient all-reduce),
     Adam step on the pose (lr 5e-2, eval.py:320,337).  In graph mode forward+backward
@@ -230,7 +267,7 @@ def build_step(wl, world, mode, device):
         def step():
             wl.forward().backward()
             if world > 1:
-                allreduce_grads(wl.params(), world)
+                average_gradients(wl.params(), weight=grad_weight)
             wl.opt.step()
             wl.zero_grad()
         return step
@@ -267,9 +304,37 @@ def build_step(wl, world, mode, device):
 
     def step():
         graph.replay()
-        allreduce_grads(wl.params(), world)
+        average_gradients(wl.params(), weight=grad_weight)
         opt_graph.replay()
     return step
+
+
+def split_fwd_bwd(wl, steps, world):
+    """Forward and backward(+Adam) as two separately captured graphs sharing one pool, replayed
+    in order with events recorded between the replays: (ms_forward, ms_backward)."""
+    pool = torch.cuda.graph_pool_handle()
+    gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gf, pool=pool, capture_error_mode="thread_local"):
+        wl.seed.advance()
+        loss = wl.forward()
+    with torch.cuda.graph(gb, pool=pool, capture_error_mode="thread_local"):
+        loss.backward(retain_graph=True)
+        if world == 1:
+            wl.opt.step()
+    for _ in range(3):
+        gf.replay()
+        gb.replay()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    torch.cuda.synchronize()
+    for e in ev:
+        e[0].record()
+        gf.replay()
+        e[1].record()
+        gb.replay()
+        e[2].record()
+    torch.cuda.synchronize()
+    return (float(np.mean([a.elapsed_time(b) for a, b, _ in ev])),
+            float(np.mean([b.elapsed_time(c) for _, b, c in ev])))
 
 
 # device-side spin before each timed launch's start event (~80 us at the 2.4 GHz shader
@@ -279,43 +344,38 @@ LEAD_CYCLES = 200_000
 
 
 def instrumented_pass(wl, steps):
-    """Eager replica of the timed step.  (1) HIP events around every native launch (on its
-    stream, each behind a device-side lead spin): per-call kernel durations.  (2) Without
-    the spins, events around forward / backward: the fwd/bwd split.  (ROCm cannot record
-    events inside a captured graph.)"""
+    """Eager replica of the timed step with HIP events around every native launch (on its
+    stream, each behind a device-side lead spin): per-call kernel durations.  (ROCm cannot
+    record events inside a captured graph.)"""
     seed = getattr(wl, "seed", None)
     grads = [p.grad for p in wl.params()]
-
-    def one():
-        if seed is not None:
-            seed.advance()
-        loss = wl.forward()
-        loss.backward()
-        for p in wl.params():
-            p.grad = None
-
     torch.cuda.synchronize()
     with KernelTimer(lead_cycles=LEAD_CYCLES) as kt:
         for _ in range(steps):
-            one()
+            if seed is not None:
+                seed.advance()
+            wl.forward().backward()
+            for p in wl.params():
+                p.grad = None
         torch.cuda.synchronize()
+    for p, g in zip(wl.params(), grads):
+        p.grad = g
+    return kt.summary("median")
+
+
+def eager_split(wl, steps):
+    """ms forward / ms backward of the eager step (events around forward and loss.backward())."""
     fb = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     for i in range(steps):
-        if seed is not None:
-            seed.advance()
         fb[i][0].record()
         loss = wl.forward()
         fb[i][1].record()
         loss.backward()
         fb[i][2].record()
-        for p in wl.params():
-            p.grad = None
+        wl.zero_grad()
     torch.cuda.synchronize()
-    for p, g in zip(wl.params(), grads):
-        p.grad = g
-    ms_fwd = float(np.mean([a.elapsed_time(b) for a, b, _ in fb]))
-    ms_bwd = float(np.mean([b.elapsed_time(c) for _, b, c in fb]))
-    return kt.summary("median"), ms_fwd, ms_bwd
+    return (float(np.mean([a.elapsed_time(b) for a, b, _ in fb])),
+            float(np.mean([b.elapsed_time(c) for _, b, c in fb])))
 
 
 def main():
@@ -326,11 +386,13 @@ def main():
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
                     help="BASELINE.json configuration (cfg2 = the metric's headline workload)")
+    ap.add_argument("--shard", choices=["frames", "samples"], default="frames",
+                    help="N > 1: distinct views per rank (weak) or the Monte-Carlo samples (strong)")
     ap.add_argument("--image-size", type=int, default=None)
     ap.add_argument("--faces-per-pixel", type=int, default=None)
-    ap.add_argument("--samples", type=int, default=None, help="Monte-Carlo samples per rank")
+    ap.add_argument("--samples", type=int, default=None, help="Monte-Carlo samples (global in --shard samples)")
     ap.add_argument("--batch", type=int, default=None, help="meshes per rank")
-    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--cpu-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
     args = ap.parse_args()
@@ -339,7 +401,7 @@ def main():
                      ("batch", args.batch)):
         if val is not None:
             cfg[key] = val
-    headline = cfg == CONFIGS["cfg2"]
+    headline = args.config == "cfg2" and cfg == CONFIGS["cfg2"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -357,23 +419,36 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    torch.manual_seed(1234)  # same Philox keys on every rank ...
-    pa.noise.set_sample_shard(rank)  # ... disjoint global sample ranges
+    torch.manual_seed(1234)  # same Philox keys on every rank
     pa.native_library()
 
-    mk_wl = lambda: Workload(device, cfg["image_size"], cfg["K"], cfg["samples"], seed=0,  # same frame on all ranks
-                             batch=cfg["batch"])
+    S, Sr = cfg["samples"], cfg.get("rast_samples", cfg["samples"])
+    shard = args.shard if world > 1 else "frames"
+    grad_weight = None
+    azim = 120.0
+    if shard == "samples":
+        off_a, n_a = sample_shard(S, rank, world)
+        off_r, n_r = sample_shard(Sr, rank, world)
+        pa.noise.set_sample_offset(off_r, off_a)
+        grad_weight = n_a / S
+        S_local, Sr_local = n_a, n_r
+    else:
+        azim = 120.0 + 360.0 * rank / world
+        S_local, Sr_local = S, Sr
+
+    mk_wl = lambda: Workload(device, cfg["image_size"], cfg["K"], S_local, seed=0, batch=cfg["batch"], azim=azim,
+                             rast_samples=Sr_local, eval_scene=args.config == "eval")
     wl = mk_wl()
     P = cfg["batch"] * cfg["image_size"] * cfg["image_size"]
     mode, note = args.mode, None
     try:
-        step = build_step(wl, world, mode, device)
+        step = build_step(wl, world, mode, device, grad_weight)
     except Exception as e:  # graph capture unavailable: measure eagerly and say so
         note = f"graph capture failed ({type(e).__name__}: {e}); eager fallback"
         pa.noise.use_device_seed(None)
         wl = mk_wl()
         mode = "eager"
-        step = build_step(wl, world, mode, device)
+        step = build_step(wl, world, mode, device, grad_weight)
 
     for _ in range(args.warmup):
         step()
@@ -391,10 +466,19 @@ def main():
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ksum, ms_fwd, ms_bwd = instrumented_pass(wl, min(args.steps, 20))
+
+    n_split = min(args.steps, 20)
+    if mode == "graph":
+        ms_fwd, ms_bwd = split_fwd_bwd(wl, n_split, world)
+        split_from = ("HIP events around separately captured forward and backward(+Adam) graphs, replayed "
+                      "after the timed region")
+    else:
+        ms_fwd, ms_bwd = eager_split(wl, n_split)
+        split_from = "HIP events around the eager forward / loss.backward()"
+    ksum = instrumented_pass(wl, n_split)
     kern = {}
     for name, (n, ms) in ksum.items():
-        bts = kernel_bytes(name, P, wl.K, wl.S, wl.F)
+        bts = kernel_bytes(name, P, wl.K, S_local, wl.F)
         kern[name] = {"launches": n, "ms": round(ms, 4), "bytes": bts,
                       "GBps": round(bts / (ms * 1e-3) / 1e9, 1)}
     dom = max(kern, key=lambda k: kern[k]["ms"] * kern[k]["launches"])
@@ -414,39 +498,52 @@ def main():
                 roof["valu_issue_us"] = tr["valu_issue_us"]
                 roof["valu_frac"] = round(tr["valu_issue_us"] / (1e3 * d["ms"]), 4)
 
-    B, Hs, K, S = cfg["batch"], cfg["image_size"], cfg["K"], cfg["samples"]
-    frames = args.steps * world * B
-    value = frames / elapsed
-    meshes = ("sphere_642 (1280 faces)" if B == 1 else
-              f"{B} meshes alternating sphere_642 / cube2 ({wl.F} faces), one pose each")
+    B, Hs, K = cfg["batch"], cfg["image_size"], cfg["K"]
+    distinct = B * (world if shard == "frames" else 1)  # distinct frames per step
+    value = args.steps * distinct / elapsed
+    if args.config == "eval":
+        meshes = "textured cube (TexturesUV) + RandomPhongShader, eval.py's renderer"
+    elif B == 1:
+        meshes = "sphere_642 (1280 faces)"
+    else:
+        meshes = f"{B} meshes alternating sphere_642 / cube2 ({wl.F} faces), one pose each"
+    samples_txt = f"Sr={Sr} Sa={S}" if Sr != S else f"Sr=Sa={S}"
+    if world == 1:
+        par = "single GPU"
+    elif shard == "frames":
+        par = (f"frame-parallel x{world}: each rank renders its own view (azimuth 120 + 360 r / {world}) of the "
+               "shared pose; one RCCL all-reduce averages the gradients")
+    else:
+        par = (f"sample-parallel x{world}: the same frame on every rank, {S} global samples split "
+               f"{[sample_shard(S, r, world)[1] for r in range(world)]}, shared Philox keys + global sample "
+               "offsets; one RCCL all-reduce forms the full-S gradient estimate")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s (fwd+bwd)", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "strong" if shard == "samples" else "weak", "vs_baseline": None,
+        "dtype": "f32",
         "data": "synthetic (meshes from the reference data, random vertex colours, random target)",
         "config": {"workload": f"{args.config} pose-opt step: {meshes}, {Hs}x{Hs}, faces_per_pixel={K}, "
-                               f"Sr=Sa={S} Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, "
+                               f"{samples_txt} Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, "
                                "fwd + L2 loss + bwd + Adam step on the pose (lr 5e-2)",
-                   "image_size": Hs, "faces_per_pixel": K, "nb_samples": S, "batch": B,
-                   "frames_per_rank_per_step": B, "execution": mode,
-                   "parallelism": f"sample-parallel x{world} (same frames, Philox sample shard per rank, "
-                                  f"one RCCL gradient all-reduce per step)"},
-        "ms_forward": round(ms_fwd, 4), "ms_backward": round(ms_bwd, 4),
-        "fwd_bwd_split_from": "eager instrumented replica (HIP events around forward / loss.backward())",
-        "fwd_frames_per_s": round(world * B * 1e3 / ms_fwd, 2), "kernels": kern, "roofline": roof,
+                   "image_size": Hs, "faces_per_pixel": K, "nb_samples": S, "rast_samples": Sr, "batch": B,
+                   "distinct_frames_per_step": distinct, "execution": mode, "parallelism": par},
+        "ms_forward": round(ms_fwd, 4), "ms_backward": round(ms_bwd, 4), "fwd_bwd_split_from": split_from,
+        "fwd_frames_per_s": round(distinct * 1e3 / ms_fwd, 2), "kernels": kern, "roofline": roof,
     }
     if note:
         out["note"] = note
     if rank == 0 and not args.no_dense and headline:
         out["roofline_dense"] = dense_roofline(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
-        os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+        threads, total, model = host_cpus()
         v, dt = cpu_baseline(args.cpu_frames, threads)
         out["cpu_baseline"] = {"value": round(v, 4), "unit": "frames/s (fwd+bwd)", "cores": threads,
-                               "kind": "port",
-                               "sample": f"{args.cpu_frames} frames of the same workload ({dt:.1f} s): C/OpenMP "
-                                         "rasterizer oracle + torch-CPU blend oracle fwd+bwd + rasterizer bwd"}
+                               "kind": "port", "cpu_model": model, "machine_logical_cpus": total,
+                               "sample": f"{args.cpu_frames} frames of the same workload ({dt:.1f} s) on all "
+                                         f"{threads} CPUs this process may use (affinity / cgroup quota): "
+                                         "C/OpenMP rasterizer oracle + torch-CPU blend oracle fwd+bwd + "
+                                         "rasterizer bwd"}
         out["speedup_vs_cpu"] = round(value / v, 1)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -64,6 +64,10 @@ extern "C" {
 #define PR_BLEND_AGG_CAUCHY 16  /* CauchyAgg: Cauchy agg noise (smoothagg.py:230-250)                    */
 #define PR_BLEND_RAST_WOVR 32   /* GaussianRast_wovr: score without the vr baseline (smoothrast.py:61-108) */
 #define PR_BLEND_AGG_WOVR 64    /* GaussianAgg_wovr: a_s = <g, w_s> (smoothagg.py:75-141; Cauchy keeps vr) */
+/* deterministic SoftRast + SoftAgg (smoothrast.py:126-134, smoothagg.py:165-182; eval.py's
+ * "softras" renderer): P = sigmoid(-d / sigma), W = softmax(z / gamma); with RAST | COLOR and
+ * texel colours; Sr / Sa / noise fields are ignored, winners / rast_cache are not written */
+#define PR_BLEND_SOFT 128
 
 typedef struct PRBlendParams {
   int32_t N, H, W, K;        /* fragment shape */

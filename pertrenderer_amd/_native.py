@@ -22,6 +22,7 @@ PR_BLEND_RAST_CAUCHY = 8
 PR_BLEND_AGG_CAUCHY = 16
 PR_BLEND_RAST_WOVR = 32
 PR_BLEND_AGG_WOVR = 64
+PR_BLEND_SOFT = 128
 PR_GRAD_PREZEROED = 1
 
 _vp = C.c_void_p

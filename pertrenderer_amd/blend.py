@@ -167,7 +167,9 @@ class _FusedBlendFn(torch.autograd.Function):
         image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
         # per-slot (prob, rast score) kept for the backward instead of regenerating rast noise
-        cache = torch.empty((N, H, W, K, 2), dtype=F32, device=dev) if RAST_CACHE and any(ctx.needs_input_grad[:6]) else None
+        soft = bool(cfg["vflags"] & nat.PR_BLEND_SOFT)
+        cache = (torch.empty((N, H, W, K, 2), dtype=F32, device=dev)
+                 if RAST_CACHE and not soft and any(ctx.needs_input_grad[:6]) else None)
         a = nat.PRBlendFwdArgs()
         a.p = p
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
@@ -323,6 +325,23 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
+    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, pix_to_face, znear, zfar, cfg)
+
+
+def soft_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, eps=1e-10, background=(1.0, 1.0, 1.0),
+               znear=1.0, zfar=100.0):
+    """smooth_rgb_blend(colors, fragments, SoftRast(sigma), SoftAgg(gamma, alpha, eps), ...) as one
+    native kernel pair (PR_BLEND_SOFT): P = sigmoid(-dists / sigma) (smoothrast.py:126-134),
+    W = softmax(((gamma/alpha) log P + z_inv - zmax) / gamma) with the background logit
+    (smoothagg.py:165-182), colour mix and alpha (random_rasterizer.py:34-56).  Deterministic;
+    differentiable w.r.t. dists, zbuf, colors, sigma, gamma, alpha."""
+    shape = tuple(pix_to_face.shape)
+    if tuple(colors.shape[:4]) != shape or colors.shape[-1] != 3:
+        raise ValueError(f"colors must be (N,H,W,K,3) = {shape + (3,)}, got {tuple(colors.shape)}")
+    if tuple(dists.shape) != shape or tuple(zbuf.shape) != shape:
+        raise ValueError("dists / zbuf must match pix_to_face's shape")
+    cfg = dict(Sr=1, Sa=1, eps=float(eps), bg=_background(background), noise=Noise.philox(),
+               vflags=nat.PR_BLEND_SOFT, counts=_counts_for(pix_to_face))
     return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, pix_to_face, znear, zfar, cfg)
 
 

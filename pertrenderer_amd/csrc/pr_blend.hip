@@ -1195,6 +1195,7 @@ extern "C" int pr_blend_prof_dump(void* dst, size_t bytes) {
 extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "blend_fwd: null args");
   const PRBlendFwdArgs& a = *args;
+  if (a.p.flags & PR_BLEND_SOFT) return soft_blend_fwd(a, reinterpret_cast<hipStream_t>(stream));
   const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
   if (int e = check_params(a.p, rast)) return e;
   if (!a.pix_to_face && !a.mask) return set_error(PR_ERR_ARG, "blend_fwd: need pix_to_face or mask");
@@ -1220,12 +1221,14 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
 
 extern "C" size_t pr_blend_bwd_workspace_size(const PRBlendBwdArgs* args) {
   if (!args) return 0;
+  if (args->p.flags & PR_BLEND_SOFT) return soft_blend_workspace(args->p);
   return (size_t)bwd_blocks(args->p) * 4 * sizeof(float);
 }
 
 extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "blend_bwd: null args");
   const PRBlendBwdArgs& a = *args;
+  if (a.p.flags & PR_BLEND_SOFT) return soft_blend_bwd(a, reinterpret_cast<hipStream_t>(stream));
   const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
   if (int e = check_params(a.p, rast)) return e;
   if (!a.pix_to_face && !a.mask) return set_error(PR_ERR_ARG, "blend_bwd: need pix_to_face or mask");

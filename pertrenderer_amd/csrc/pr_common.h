@@ -100,4 +100,9 @@ PR_DEV T ld(const T* p) { return *p; }
 namespace pr {
 int set_error(int code, const std::string& msg);
 int check_launch(const char* what);
+
+// PR_BLEND_SOFT: the deterministic SoftRast + SoftAgg blend (pr_softblend.hip)
+size_t soft_blend_workspace(const PRBlendParams& p);
+int soft_blend_fwd(const PRBlendFwdArgs& a, hipStream_t st);
+int soft_blend_bwd(const PRBlendBwdArgs& a, hipStream_t st);
 }  // namespace pr

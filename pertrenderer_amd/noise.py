@@ -101,6 +101,7 @@ class DeviceSeed:
 
 _DEVICE_SEED = None
 _SHARD = 0  # this process's Monte-Carlo sample shard index (set_sample_shard)
+_OFFSET = None  # explicit global (rast, agg) sample offsets (set_sample_offset), override the shard index
 
 
 def set_sample_shard(index):
@@ -115,6 +116,18 @@ def set_sample_shard(index):
 
 def sample_shard():
     return _SHARD
+
+
+def set_sample_offset(offset_r, offset_a=None):
+    """Draw the rast (agg) operators' samples from global index offset_r (offset_a) on; None
+    restores the shard index's offsets.  Uneven sample shards (parallel.sample_shard) of one
+    estimator use this."""
+    global _OFFSET
+    _OFFSET = None if offset_r is None else (int(offset_r), int(offset_r if offset_a is None else offset_a))
+
+
+def _offset(S, which):
+    return _OFFSET[which] if _OFFSET is not None else _SHARD * S
 
 
 def use_device_seed(ds):
@@ -138,8 +151,8 @@ def draw_rast(shape, Sr, device, kind="gaussian"):
     if _SOURCE == "torch":
         return Noise.injected(noise_r=_torch_draw(kind, (Sr,) + tuple(shape)).to(device))
     if _DEVICE_SEED is not None:
-        return Noise.philox(seed_r=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor, offset_r=_SHARD * Sr)
-    return Noise.philox(seed_r=draw_key(), offset_r=_SHARD * Sr)
+        return Noise.philox(seed_r=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor, offset_r=_offset(Sr, 0))
+    return Noise.philox(seed_r=draw_key(), offset_r=_offset(Sr, 0))
 
 
 def draw_agg(shape, Sa, device, fixed_noise=False, kind="gaussian"):
@@ -151,5 +164,5 @@ def draw_agg(shape, Sa, device, fixed_noise=False, kind="gaussian"):
     if _SOURCE == "torch":
         return Noise.injected(noise_a=_torch_draw(kind, (Sa,) + tuple(shape)).to(device))
     if _DEVICE_SEED is not None and not fixed_noise:
-        return Noise.philox(seed_a=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor, offset_a=_SHARD * Sa)
-    return Noise.philox(seed_a=draw_key(), offset_a=_SHARD * Sa)
+        return Noise.philox(seed_a=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor, offset_a=_offset(Sa, 1))
+    return Noise.philox(seed_a=draw_key(), offset_a=_offset(Sa, 1))

@@ -62,6 +62,11 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
             smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
             eps=smoothagg.eps, background=background, znear=znear, zfar=zfar,
             fixed_noise=smoothagg.fixed_noise, **_variant_kw(smoothrast, smoothagg))
+    if type(smoothrast) is SoftRast and type(smoothagg) is SoftAgg and fragments.pix_to_face.is_cuda:
+        # eval.py's "softras" pair as one native kernel pair (PR_BLEND_SOFT)
+        return _blend.soft_blend(colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
+                                 smoothagg.gamma, smoothagg.alpha, eps=smoothagg.eps, background=background,
+                                 znear=znear, zfar=zfar)
     background = _background_tensor(background, device)
     mask = fragments.pix_to_face >= 0
     prob_map = smoothrast.rasterize(fragments.dists) * mask
