@@ -69,8 +69,8 @@ struct Geo {
   int K, KP1, PB, HW;
   int qK, rK, qK1, rK1, qS, rS;  // 256 / {K, K+1, Sa} and remainders
   int lpp, lsh;                  // lanes per pixel in the pixel phases (256 / PB, 8..64) and log2
-  int ck;                        // contiguous per-lane chunk of the pixel phases: ceil((K+1)/lpp)
   int bpi;                       // blocks per image for the centre-out block order (0: linear)
+  int tail;                      // backward: joint masked-tail draw allowed (PR_BLEND_TAIL=0: off)
 };
 
 // pixel block of this workgroup: centre-out within each image when blocks tile images
@@ -139,6 +139,41 @@ PR_DEV void batch_next(Batch& b, int& pl, int& k, int i0, int L, int Q, int R, i
     k += R;
     if (k >= L) { k -= L; ++pl; }
   }
+}
+
+// Compacted walk over per-pixel item ranges (valid-prefix counts): item i of the block
+// belongs to pixel pl with O(pl) = V[pl] + bonus * pl <= i < O(pl + 1), item k = i - O(pl).
+// V is the exclusive prefix of the pixels' counts; bonus 1 appends one extra item (the
+// background entry) per pixel.  Items grow with i, so pl only moves forward.
+PR_DEV void scan_batch(Batch& b, int& pl, int i0, int n, const int* V, int bonus) {
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int i = i0 + u * kThreads;
+    b.ok[u] = i < n;
+    if (b.ok[u])
+      while (V[pl + 1] + bonus * (pl + 1) <= i) ++pl;
+    b.pl[u] = pl;
+    b.k[u] = i - (V[pl] + bonus * pl);
+  }
+}
+
+// Wave 0: per-pixel valid-prefix counts (clamped to [0, K]; K without pix_count) into CP and
+// their exclusive prefix into V[0..npix] (PB <= 32 lanes).  Returns the total in lane 0..63.
+PR_DEV int scan_counts(const int32_t* pcnt, int64_t pix0, int npix, int K, int* CP, int* V) {
+  const int tid = threadIdx.x;
+  const int cp = tid < npix ? (pcnt ? min(max((int)pcnt[pix0 + tid], 0), K) : K) : 0;
+  int x = cp;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (tid >= o) x += y;
+  }
+  if (tid < npix) {
+    CP[tid] = cp;
+    V[tid] = x - cp;
+  }
+  const int tot = __shfl(x, 63);
+  if (tid == 0) V[npix] = tot;
+  return tot;
 }
 
 // Wave-wide append of the lanes with `want` to an LDS queue: one LDS atomic per wave,
@@ -265,6 +300,46 @@ PR_DEV void agg_noise4(const PRBlendParams& p, const Sc& sc, uint32_t gp, int j,
   }
 }
 
+// Masked-tail noise of one agg sample (Philox Gaussian mode, backward only).  The m slots
+// past a pixel's valid prefix have logit -inf: they never win, and their noise reaches the
+// gradient only through S1 = sum_j eps_j (d z_max, B7) and S2 = sum_j eps_j^2 (d gamma).
+// For m iid N(0,1) draws S1 = sqrt(m) Z and S2 = Z^2 + X with X ~ chi2(m-1) independent of
+// Z (Cochran: sample mean and sum of squared deviations are independent), so the pair is
+// drawn directly -- in distribution identical to m per-slot draws, at one Philox block per
+// sample instead of m/4.  X = Z'^2 for m = 2, else 2 Gamma((m-1)/2) by Marsaglia-Tsang
+// (ACM TOMS 26(3), 2000) squeeze + log test (acceptance >= 95 % for shape >= 1); a proposal
+// rejected 8 times in a row (probability < 1e-10) keeps its last proposal.
+PR_DEV void tail_pair(uint64_t key, uint32_t gp, uint32_t sg, int m, float& s1, float& s2) {
+  U4 u = philox_block(key, gp, 0u, sg, kTagTail);
+  float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(u.x)));
+  const float z = rad * __builtin_amdgcn_cosf(u01(u.y));
+  float x = rad * __builtin_amdgcn_sinf(u01(u.y));
+  s1 = __builtin_amdgcn_sqrtf((float)m) * z;
+  float c = 0.f;
+  if (m == 2) {
+    c = x * x;
+  } else if (m >= 3) {
+    const float d = 0.5f * (float)(m - 1) - (1.f / 3.f), cc = __builtin_amdgcn_rsqf(9.f * d);
+    float uu = u01(u.z), v3 = 1.f;
+    for (uint32_t t = 1;; ++t) {
+      const float v = __builtin_fmaf(cc, x, 1.f);
+      if (v > 0.f) {
+        v3 = v * v * v;
+        const float x2 = x * x;
+        if (uu < 1.f - 0.0331f * (x2 * x2)) break;
+        if (logf(uu) < __builtin_fmaf(0.5f, x2, d * ((1.f - v3) + logf(v3)))) break;
+      }
+      if (t == 8) break;
+      u = philox_block(key, gp, t, sg, kTagTail);
+      rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(u.x)));
+      x = rad * __builtin_amdgcn_cosf(u01(u.y));
+      uu = u01(u.z);
+    }
+    c = 2.f * d * v3;
+  }
+  s2 = __builtin_fmaf(z, z, c);
+}
+
 PR_DEV int agg_first_group(const PRBlendParams& p) { return p.sample_offset_a >> 2; }
 PR_DEV int agg_num_groups(const PRBlendParams& p) {
   return ((p.sample_offset_a + p.Sa - 1) >> 2) - (p.sample_offset_a >> 2) + 1;
@@ -301,7 +376,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   float* B = A + PB * KP1;         // [PB][KP1] z_inv, then logits z
   float* PX = B + PB * KP1;        // [PB][4] z_max, alpha, max logit, candidate count
   int* CP = reinterpret_cast<int*>(PX + PB * 4);            // [PB] valid-prefix count (K without pix_count)
-  int* QN = CP + PB;                                        // rast queue length
+  int* V = CP + PB;                                         // [PB+1] exclusive prefix of CP
+  int* QN = V + PB + 1;                                     // rast queue length
   uint16_t* Q = reinterpret_cast<uint16_t*>(QN + 4);        // [PB*K] rast queue (pl << 8 | k)
   uint8_t* LC = reinterpret_cast<uint8_t*>(Q);              // [PB][KP1] argmax candidates (after 1b)
   int* CNT = reinterpret_cast<int*>(A);
@@ -313,20 +389,24 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   if (tid == 0) *QN = 0;
   const int32_t* pcnt = a.pix_count;
-  if (tid < npix) CP[tid] = pcnt ? pcnt[pix0 + tid] : K;
+  if (tid < 64) scan_counts(pcnt, pix0, npix, K, CP, V);
   __syncthreads();
 
   // ---- 1a: slots, kU per thread in flight: mask, z_inv, and the probability wherever
-  //          it needs no noise (masked, or saturated Gaussian); the rest is queued
+  //          it needs no noise (masked, or saturated Gaussian); the rest is queued.  With
+  //          valid-prefix counts only the valid slots are walked: no later phase reads a
+  //          masked slot's LDS entry (its prob is 0, its z_inv 0, its logit -inf)
   {
     // saturation shortcut of rast_count / rast_count_score (Philox Gaussian; the score
     // form also needs variance reduction)
     const bool sat_ok = NOISE == PR_NOISE_PHILOX && !(p.flags & PR_BLEND_RAST_CAUCHY) &&
                         !(a.rast_cache && (p.flags & PR_BLEND_RAST_WOVR));
-    int cpl = tid / K, ck = tid - (tid / K) * K;
-    for (int i0 = tid; i0 < npix * K; i0 += kU * kThreads) {
+    int cpl = tid / K, ck = tid - (tid / K) * K, spl = 0;
+    const int nit = pcnt ? V[npix] : npix * K;
+    for (int i0 = tid; i0 < nit; i0 += kU * kThreads) {
       Batch bt;
-      batch_next(bt, cpl, ck, i0, K, g.qK, g.rK, npix * K);
+      if (pcnt) scan_batch(bt, spl, i0, nit, V, 0);
+      else batch_next(bt, cpl, ck, i0, K, g.qK, g.rK, nit);
       bool mk[kU];
       float dd[kU], zb[kU];
 #pragma unroll
@@ -399,12 +479,14 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   }
   PR_BSTAMP(0);
 
-  // ---- 2: per pixel (8 lanes): alpha, z_max, logits, largest logit, and the list of
-  //         argmax candidates (ascending j)
+  // ---- 2: per pixel (lpp lanes): alpha, z_max, logits, largest logit, and the list of
+  //         argmax candidates (ascending j).  A pixel's entries are its cp walked slots,
+  //         then the background (entry cp -> j = K); lanes take contiguous chunks
   {
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
-    const int j0 = l * g.ck, j1 = min(KP1, j0 + g.ck), k1 = min(K, j1);
+    const int cp = act ? CP[pl] : 0, ckp = (cp + g.lpp) >> g.lsh;  // ceil((cp + 1) / lpp)
+    const int j0 = l * ckp, j1 = min(cp + 1, j0 + ckp), k1 = min(cp, j1);
     float al = 1.f, zm = kNegInf;
     if (act)
       for (int k = j0; k < k1; ++k) {
@@ -415,11 +497,13 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
       al *= __shfl_xor(al, m);
       zm = fmaxf(zm, __shfl_xor(zm, m));
     }
+    if (cp < K) zm = fmaxf(zm, 0.f);  // masked slots' z_inv (0) are in the reference's max
     const float zmax = zm < p.eps ? p.eps : zm;
     const float gal = sc.gamma / sc.alpha;
     float zl = kNegInf;
     if (act)
-      for (int j = j0; j < j1; ++j) {
+      for (int e = j0; e < j1; ++e) {
+        const int j = e < cp ? e : K;
         const float z = j < K ? gal * logf(A[pl * KP1 + j]) + B[pl * KP1 + j] - zmax : p.eps - zmax;
         B[pl * KP1 + j] = z;
         CNT[pl * KP1 + j] = 0;
@@ -434,8 +518,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     const float zfloor = zl - skipm;
     int nc = 0;
     if (act)
-      for (int j = j0; j < j1; ++j) {
-        const float z = B[pl * KP1 + j];
+      for (int e = j0; e < j1; ++e) {
+        const float z = B[pl * KP1 + (e < cp ? e : K)];
         nc += (z > kNegInf && z >= zfloor) ? 1 : 0;
       }
     int off = 0, tot = 0;
@@ -446,7 +530,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
       tot += t;
     }
     if (act)
-      for (int j = j0; j < j1; ++j) {
+      for (int e = j0; e < j1; ++e) {
+        const int j = e < cp ? e : K;
         const float z = B[pl * KP1 + j];
         if (z > kNegInf && z >= zfloor) LC[pl * KP1 + off++] = (uint8_t)j;
       }
@@ -519,7 +604,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
     if (pl < npix) {
-      for (int k = l; k < K; k += g.lpp) {
+      for (int k = l; k < CP[pl]; k += g.lpp) {  // masked slots never win (their CNT is not set)
         const int cw = CNT[pl * KP1 + k];
         if (cw == 0) continue;
         const float w = (float)cw / fSa;
@@ -546,7 +631,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     }
   } else {
     PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
-      a.weights[(pix0 + pl) * KP1 + k] = (float)CNT[pl * KP1 + k] / fSa;
+      const int cw = (k < CP[pl] || k == K) ? CNT[pl * KP1 + k] : 0;
+      a.weights[(pix0 + pl) * KP1 + k] = (float)cw / fSa;
     }
   }
 #ifdef PR_BLEND_PROFILE
@@ -573,24 +659,64 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   float* AS = reinterpret_cast<float*>(CN + PB * KP1);  // [PB][Sa] a_s
   float* PX = AS + PB * Sa;            // [PB][8] per-pixel scalars
   int* CP = reinterpret_cast<int*>(PX + PB * 8);        // [PB] valid-prefix count (K without pix_count)
+  int* V = CP + PB;                    // [PB+1] exclusive prefix of CP
+  int* OFF = V + PB + 1;               // [PB+1] first B6 row of each pixel, then [PB+1] = lanes per row
+  float* TD = reinterpret_cast<float*>(OFF + PB + 2);   // [PB][4] masked-tail d z sums (B6 -> B7)
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
   const int64_t blk = pixel_block(g), pix0 = blk * PB;
   const int npix = (int)min((int64_t)PB, g.P - pix0);
   const int32_t* pcnt = a.pix_count;
-  if (tid < npix) CP[tid] = pcnt ? pcnt[pix0 + tid] : K;
+  const int ng = agg_num_groups(p), g0 = agg_first_group(p);
+  const bool agg_cauchy = p.flags & PR_BLEND_AGG_CAUCHY;
+  // B6 draws the masked tail jointly (tail_pair) in Philox Gaussian mode when the valid
+  // prefix is known; injected noise (parity) and Cauchy noise keep one row per slot
+  const bool tail = NOISE == PR_NOISE_PHILOX && !agg_cauchy && pcnt != nullptr && g.tail;
+  if (tid < 64) {
+    // B6 rows per pixel: its valid slots + background (all K+1 slots without the tail
+    // draw), then 4 tail rows (one per sample of a Philox group) if any slot is masked;
+    // each row is split over nch lanes (power of 2) when the block has few rows.  Wave 0
+    // scans the counts and the row counts (PB <= 32 lanes).
+    scan_counts(pcnt, pix0, npix, K, CP, V);
+    const int cp = tid < npix ? CP[tid] : 0;
+    const int v = tid < npix ? (tail ? cp + 1 + (cp < K ? 4 : 0) : KP1) : 0;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (tid >= o) x += y;
+    }
+    if (tid < npix) OFF[tid] = x - v;
+    const int o = __shfl(x, 63);
+    if (tid == 0) {
+      int nch = 1;
+      while (nch < 64 && 2 * nch <= ng && 2 * nch * o <= kThreads) nch <<= 1;
+      OFF[npix] = o;
+      OFF[PB + 1] = nch;
+    }
+  }
   __syncthreads();
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   const float gal = sc.gamma / sc.alpha;
   float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
 
   // ---- B1: slots + background entry: prob, z_inv, rast score, dL/dW (kU items per
-  //          thread with their global loads in flight together)
+  //          thread with their global loads in flight together).  With valid-prefix
+  //          counts a pixel's entries are its valid slots and the background: no later
+  //          phase reads a masked slot's LDS entry except B6/B7 without the tail draw,
+  //          which write and read only their own ZZ rows
   {
-    int cpl = tid / KP1, ck = tid - (tid / KP1) * KP1;
-    for (int i0 = tid; i0 < npix * KP1; i0 += kU * kThreads) {
+    int cpl = tid / KP1, ck = tid - (tid / KP1) * KP1, spl = 0;
+    const int nit = pcnt ? V[npix] + npix : npix * KP1;
+    for (int i0 = tid; i0 < nit; i0 += kU * kThreads) {
       Batch bt;
-      batch_next(bt, cpl, ck, i0, KP1, g.qK1, g.rK1, npix * KP1);
+      if (pcnt) {
+        scan_batch(bt, spl, i0, nit, V, 1);
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (bt.ok[u] && bt.k[u] == CP[bt.pl[u]]) bt.k[u] = K;  // the background entry
+      } else {
+        batch_next(bt, cpl, ck, i0, KP1, g.qK1, g.rK1, nit);
+      }
       bool mk[kU];
       float2 pg[kU];  // (prob, gm) from the cache / input prob, or (dist, -) to recount
       float zb[kU], dw[kU];
@@ -665,12 +791,14 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   __syncthreads();
   PR_BSTAMP(0);
 
-  // ---- B2: per pixel (8 lanes, contiguous chunks): z_max + first argmax, exclusive
+  // ---- B2: per pixel (lpp lanes, contiguous chunks of its entries: the cp walked slots,
+  //          then the background as entry cp -> j = K): z_max + first argmax, exclusive
   //          products for the alpha gradient, logits, unperturbed argmax j0
   {
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
-    const int j0c = l * g.ck, j1c = min(KP1, j0c + g.ck), k1c = min(K, j1c);
+    const int cp = act ? CP[pl] : 0, ckp = (cp + g.lpp) >> g.lsh;  // ceil((cp + 1) / lpp)
+    const int j0c = l * ckp, j1c = min(cp + 1, j0c + ckp), k1c = min(cp, j1c);
     float zm = kNegInf, tp = 1.f;
     int km = 1 << 30;
     if (act)
@@ -684,10 +812,13 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
       const int ok = __shfl_xor(km, m);
       if (oz > zm || (oz == zm && ok < km)) { zm = oz; km = ok; }
     }
+    // masked slots hold z_inv = 0 in the reference's max; they follow every walked slot, so a
+    // walked slot wins a tie
+    if (cp < K && 0.f > zm) { zm = 0.f; km = cp; }
     if (km == (1 << 30)) km = 0;
     const float zmax = zm < p.eps ? p.eps : zm;
     if constexpr (CM != 0) {
-      // exclusive products across the 8 lane chunks, then within the chunk
+      // exclusive products across the lane chunks, then within the chunk
       float pre = 1.f, suf = 1.f;
       const int lane8 = (tid & 63) & ~(g.lpp - 1);  // the pixel's first lane
       for (int o = 0; o < g.lpp; ++o) {
@@ -695,6 +826,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         if (o < l) pre *= t;
         if (o > l) suf *= t;
       }
+      if (act && l == 0) PX[pl * 8 + 5] = tp * suf;  // prod (1 - prob): a masked slot's exclusive product
       if (act) {
         for (int k = k1c - 1; k >= j0c; --k) {
           EX[pl * KP1 + k] = suf;
@@ -709,7 +841,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     float zb = kNegInf;
     int jb = 1 << 30;
     if (act)
-      for (int j = j0c; j < j1c; ++j) {
+      for (int e = j0c; e < j1c; ++e) {
+        const int j = e < cp ? e : K;
         const float z = j < K ? gal * logf(PR[pl * KP1 + j]) + ZZ[pl * KP1 + j] - zmax : p.eps - zmax;
         if (z > zb || jb == (1 << 30)) { zb = z; jb = j; }
       }
@@ -763,40 +896,65 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
 
   // ---- B6: dz_j = mean_s(a_s * score(eps_sj) / gamma) and sum_s a_s * eps_sj * score(eps_sj)
   //          (d gamma; score = eps for Gaussian noise, 2 eps / (1 + eps^2) for Cauchy)
+  //          Rows (OFF) are split over nch adjacent lanes (groups gi = c, c + nch, ...) and
+  //          merged with xor-shuffles; a tail row t carries sample 4g + t of every group.
   {
-    const int ng = agg_num_groups(p), g0 = agg_first_group(p);
-    const bool cauchy = p.flags & PR_BLEND_AGG_CAUCHY;
     // the reference divides each sample's a_s * score by gamma (smoothagg.py:52); one
     // reciprocal here instead of an IEEE division per (slot, sample): within 1 ulp
     const float inv_gamma = 1.f / sc.gamma;
-    PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
-      const int j = k;
-      const int64_t gp = pix0 + pl;
+    const int nrow = OFF[npix], nch = OFF[PB + 1], lch = 31 - __builtin_clz(nch);
+    int pl = 0;
+    for (int i0 = 0; i0 < nrow * nch; i0 += kThreads) {  // uniform trip count (shuffles below)
+      const int i = i0 + tid, row = i >> lch, c = i & (nch - 1);
+      const bool live = row < nrow;
       float dz = 0.f, q = 0.f;
-      for (int gi = 0; gi < ng; ++gi) {
-        const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
-        const int sbase = (int)(4 * gg) - (NOISE == PR_NOISE_INJECTED ? 0 : p.sample_offset_a);
-        float av[4];
-        bool any = false;
+      int r = 0, ns = 0;
+      if (live) {
+        while (OFF[pl + 1] <= row) ++pl;
+        r = row - OFF[pl];
+        ns = tail ? CP[pl] + 1 : KP1;
+        const int64_t gp = pix0 + pl;
+        const int j = (tail && r == ns - 1) ? K : r;  // slot row (the last one is the background)
+        const int m = K - CP[pl];                     // masked slots (tail rows)
+        for (int gi = c; gi < ng; gi += nch) {
+          const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
+          const int sbase = (int)(4 * gg) - (NOISE == PR_NOISE_INJECTED ? 0 : p.sample_offset_a);
+          if (r >= ns) {  // tail row: one sample of this group
+            const int t = r - ns, s = sbase + t;
+            const float as = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
+            if (as == 0.f) continue;
+            float s1, s2;
+            tail_pair(sc.ka, (uint32_t)gp, 4u * gg + (uint32_t)t, m, s1, s2);
+            dz += (as * s1) * inv_gamma;
+            q += as * s2;
+            continue;
+          }
+          float av[4];
+          bool any = false;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int s = sbase + r;
-          av[r] = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
-          any |= av[r] != 0.f;
-        }
-        if (!any) continue;
-        float e[4];
-        agg_noise4<NOISE>(p, sc, (uint32_t)gp, j, gg, g.P, KP1, e);
+          for (int u = 0; u < 4; ++u) {
+            const int s = sbase + u;
+            av[u] = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
+            any |= av[u] != 0.f;
+          }
+          if (!any) continue;
+          float e[4];
+          agg_noise4<NOISE>(p, sc, (uint32_t)gp, j, gg, g.P, KP1, e);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (av[r] != 0.f) {
-            const float scr = noise_score(e[r], cauchy);
-            dz += (av[r] * scr) * inv_gamma;
-            q += av[r] * (e[r] * scr);
+          for (int u = 0; u < 4; ++u) {
+            if (av[u] != 0.f) {
+              const float scr = noise_score(e[u], agg_cauchy);
+              dz += (av[u] * scr) * inv_gamma;
+              q += av[u] * (e[u] * scr);
+            }
           }
         }
       }
-      ZZ[pl * KP1 + j] = dz / (float)Sa;  // ZZ now holds dL/dz
+      for (int mm = 1; mm < nch; mm <<= 1) dz += __shfl_xor(dz, mm);
+      if (live && c == 0) {
+        if (r < ns) ZZ[pl * KP1 + ((tail && r == ns - 1) ? K : r)] = dz / (float)Sa;  // ZZ now holds dL/dz
+        else TD[pl * 4 + (r - ns)] = dz / (float)Sa;
+      }
       part_q += q;
     }
   }
@@ -807,12 +965,15 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   {
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
-    const int j0c = l * g.ck, k1c = min(K, j0c + g.ck);
+    // with the tail draw B6 wrote the valid slots' rows only (the tail's sum is in TD)
+    const int ns = act ? (tail ? CP[pl] : K) : 0, cks = (ns + g.lpp - 1) >> g.lsh;
+    const int j0c = l * cks, k1c = min(ns, j0c + cks);
     float s = 0.f;
     if (act)
       for (int k = j0c; k < k1c; ++k) s += ZZ[pl * KP1 + k];
     for (int m = 1; m < g.lpp; m <<= 1) s += __shfl_xor(s, m);
     if (act && l == 0) {
+      if (tail && CP[pl] < K) s += (TD[pl * 4] + TD[pl * 4 + 1]) + (TD[pl * 4 + 2] + TD[pl * 4 + 3]);
       float dzm = -s - ZZ[pl * KP1 + K];
       dzm = dzm * (PX[pl * 8 + 0] >= p.eps ? 1.f : 0.f);
       PX[pl * 8 + 4] = dzm;
@@ -821,11 +982,14 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   __syncthreads();
   PR_BSTAMP(4);
 
-  // ---- B8: per-slot gradients (kU slots per thread, mask and upstream gradient loads batched)
-  int cpl = tid / K, ck = tid - (tid / K) * K;
-  for (int i0 = tid; i0 < npix * K; i0 += kU * kThreads) {
+  // ---- B8: per-slot gradients (kU slots per thread, mask and upstream gradient loads batched);
+  //          with valid-prefix counts the valid slots here, the masked ones in B8m
+  int cpl = tid / K, ck = tid - (tid / K) * K, spl = 0;
+  const int nit8 = pcnt ? V[npix] : npix * K;
+  for (int i0 = tid; i0 < nit8; i0 += kU * kThreads) {
     Batch bt;
-    batch_next(bt, cpl, ck, i0, K, g.qK, g.rK, npix * K);
+    if (pcnt) scan_batch(bt, spl, i0, nit8, V, 0);
+    else batch_next(bt, cpl, ck, i0, K, g.qK, g.rK, nit8);
     int64_t fk[kU];
     bool mk[kU];
     float4 gik[kU];
@@ -907,6 +1071,35 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
       a.grad_bary[gs * 3 + 1] = gb[1];
       a.grad_bary[gs * 3 + 2] = gb[2];
     }
+    }
+  }
+
+  // ---- B8m: masked slots (valid-prefix counts): constant gradients, no LDS entry read.
+  //           d zbuf, d dists and d colour are 0 (mask factor 0, no wins); without dists
+  //           d prob keeps the alpha term g_alpha * prod_j (1 - prob_j) (its dL term is 0:
+  //           prob = 0 there).  Masked item i of the block: pixel pl with
+  //           pl*K - V[pl] <= i < (pl+1)*K - V[pl+1], slot CP[pl] + i - (pl*K - V[pl]).
+  if (pcnt) {
+    const int nm = npix * K - V[npix];
+    int mpl = 0;
+    for (int i = tid; i < nm; i += kThreads) {
+      while ((mpl + 1) * K - V[mpl + 1] <= i) ++mpl;
+      const int k = CP[mpl] + (i - (mpl * K - V[mpl]));
+      const int64_t gp = pix0 + mpl, gs = gp * K + k;
+      a.grad_zbuf[gs] = 0.f;
+      if constexpr (RAST) {
+        a.grad_dists[gs] = 0.f;
+      } else {
+        float dprob = 0.f;
+        if constexpr (CM != 0) dprob = a.grad_image[gp * 4 + 3] * PX[mpl * 8 + 5];
+        a.grad_prob[gs] = dprob;
+      }
+      if constexpr (CM == 1) {
+        float* dc = a.grad_colors + gs * 3;
+        dc[0] = dc[1] = dc[2] = 0.f;
+      } else if constexpr (CM == 2) {
+        a.grad_bary[gs * 3] = a.grad_bary[gs * 3 + 1] = a.grad_bary[gs * 3 + 2] = 0.f;
+      }
     }
   }
 
@@ -1075,10 +1268,10 @@ __global__ void __launch_bounds__(kThreads) philox_kernel(const uint4* ctr, cons
 // A, B, PX, CP, queue length (+pad), then the uint16 rast queue [PB*K] (which also holds the
 // uint8 candidate lists [PB][KP1]: 2K >= K+1)
 size_t fwd_lds(int PB, int KP1) {
-  return (size_t)(2 * PB * KP1 + 5 * PB + 4) * sizeof(float) + (size_t)PB * (KP1 - 1) * sizeof(uint16_t);
+  return (size_t)(2 * PB * KP1 + 6 * PB + 5) * sizeof(float) + (size_t)PB * (KP1 - 1) * sizeof(uint16_t);
 }
 size_t bwd_lds(int PB, int KP1, int Sa) {
-  const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + 9 * PB) * sizeof(float);
+  const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + 15 * PB + 3) * sizeof(float);
   return b < 16 * sizeof(float) ? 16 * sizeof(float) : b;
 }
 constexpr size_t kLdsBudget = 48 * 1024;  // forward: >= 3 workgroups (12 waves) per CU
@@ -1162,15 +1355,20 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   // blocks made its pixel phase slower -- longer shuffle prefixes outweigh shorter chunks)
   // PR_BLEND_LPP=16|32|64 (sweeps; capped at 256 / PB so every pixel keeps its lanes):
   // 8 / 16 / 32 measured within 1 % at cfg2 and cfg3
-  static const int lpp_env = getenv("PR_BLEND_LPP") ? atoi(getenv("PR_BLEND_LPP")) : 8;
-  int lpp = (lpp_env == 16 || lpp_env == 32 || lpp_env == 64) ? lpp_env : 8;
+  // Default: 8, doubled while a lane would walk more than 8 slots and the block has idle
+  // lanes (cfg4's 8-pixel backward blocks at K = 150: 32 lanes, chunks of 5 instead of 19).
+  static const int lpp_env = getenv("PR_BLEND_LPP") ? atoi(getenv("PR_BLEND_LPP")) : 0;
+  int lpp = 8;
+  if (lpp_env == 8 || lpp_env == 16 || lpp_env == 32 || lpp_env == 64) lpp = lpp_env;
+  else while (lpp < 64 && 2 * lpp * PB <= kThreads && g.KP1 > 8 * lpp) lpp <<= 1;
   while (lpp > 8 && lpp * PB > kThreads) lpp >>= 1;
   g.lpp = lpp;
   g.lsh = 31 - __builtin_clz(g.lpp);
-  g.ck = (g.KP1 + g.lpp - 1) / g.lpp;
   // centre-out block order (PR_BLEND_ORDER bit 0: forward, bit 1: backward; 0 = linear)
   static const int order = getenv("PR_BLEND_ORDER") ? atoi(getenv("PR_BLEND_ORDER")) : 1;
   g.bpi = (order >> (bwd ? 1 : 0) & 1) && g.HW % PB == 0 ? g.HW / PB : 0;
+  static const int tail = getenv("PR_BLEND_TAIL") ? atoi(getenv("PR_BLEND_TAIL")) : 1;
+  g.tail = tail;
   return g;
 }
 

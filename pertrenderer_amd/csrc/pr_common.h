@@ -24,6 +24,7 @@ constexpr int kThreads = 256;  // 4 waves per workgroup
 // stream tags (4th counter word) so the two draws never share a counter
 constexpr uint32_t kTagRast = 0x52415354u;  // "RAST"
 constexpr uint32_t kTagAgg = 0x41474752u;   // "AGGR"
+constexpr uint32_t kTagTail = 0x5441494Cu;  // "TAIL": joint draw of a pixel's masked agg slots
 
 struct U4 {
   uint32_t x, y, z, w;

@@ -12,6 +12,7 @@ from conftest import assert_close, load_golden
 from oracle import blend_oracle as bo
 from oracle import philox_ref
 from pertrenderer_amd import Noise, perturbed_aggregate, perturbed_blend, perturbed_heaviside
+from pertrenderer_amd.renderer.rasterizer import attach_valid_counts
 
 pytestmark = pytest.mark.gpu
 BLEND_CASES = ["blend_small", "blend_eval", "blend_edge", "blend_fixed", "blend_k100"]
@@ -22,11 +23,13 @@ def _leaf(v):
     return torch.tensor(float(v), requires_grad=True)
 
 
-def _run_fused(f, dev, noise=None):
+def _run_fused(f, dev, noise=None, counts=False):
     d = torch.tensor(f["dists"], device=dev, requires_grad=True)
     z = torch.tensor(f["zbuf"], device=dev, requires_grad=True)
     c = torch.tensor(f["colors"], device=dev, requires_grad=True)
     p2f = torch.tensor(f["pix_to_face"], device=dev)
+    if counts:  # the rasterizer's valid-prefix counts (packed fragments only)
+        attach_valid_counts(p2f, (p2f >= 0).sum(-1).to(torch.int32))
     s, g, a = _leaf(f["sigma"]), _leaf(f["gamma"]), _leaf(f["alpha"])
     N = p2f.shape[0]
     zn = torch.full((N, 1, 1, 1), float(f["znear"]), device=dev)
@@ -110,12 +113,17 @@ def _oracle(f):
     return img, bo.blend_backward(T(f["grad_image"]), s), s
 
 
+@pytest.mark.parametrize("counts", [False, True])
 @pytest.mark.parametrize("shape", [(2, 16, 20, 50, 8, 8), (1, 8, 8, 150, 16, 4), (1, 12, 9, 7, 3, 5),
                                    (1, 4, 4, 255, 4, 4)])
-def test_fused_blend_matches_oracle_random(shape, device):
+def test_fused_blend_matches_oracle_random(shape, counts, device):
+    """counts=True: the rasterizer's valid-prefix counts are attached, so the kernels walk
+    valid slots only and fill masked slots' gradients without reading them."""
     N, H, W, K, Sr, Sa = shape
+    if counts and K == 7:
+        pytest.skip("scattered valid slots: no valid prefix")
     f = _synthetic(N, H, W, K, Sr, Sa, seed=sum(shape), packed=K != 7)
-    img, g = _run_fused(f, device)
+    img, g = _run_fused(f, device, counts=counts)
     oimg, og, saved = _oracle(f)
     # the Monte-Carlo weights are counts / Sa: exact, so the image matches to fp32 summation order
     assert_close(img, oimg, name="image")
@@ -225,6 +233,43 @@ def test_philox_is_deterministic_per_seed(device):
     assert torch.equal(i1, i2)
     for k in ("dists", "zbuf", "colors"):
         assert torch.equal(g1[k], g2[k])
+
+
+def test_philox_masked_tail_draw_matches_per_slot_draws(device):
+    """With valid-prefix counts the backward draws a pixel's masked agg slots jointly
+    (pr_blend.hip tail_pair: Sum eps = sqrt(m) Z, Sum eps^2 = Z^2 + chi2(m-1)) instead of
+    one normal per (slot, sample).  Every gradient that sees per-slot noise is bit-identical
+    to the per-slot path; d zbuf at each pixel's nearest slot (it carries d z_max) and
+    d gamma (Sum eps^2) are equal in distribution: means and variances agree across
+    pixels and seeds."""
+    f = _synthetic(1, 64, 64, 60, 8, 64, seed=21, p_valid=0.1)
+    valid = f["pix_to_face"] >= 0
+    km = np.where(valid, -f["zbuf"], -np.inf).argmax(-1)[..., None]  # first max of z_inv
+    xs, ys, gx, gy = [], [], [], []
+    for seed in range(12):
+        n = Noise.philox(seed_r=1000 + seed, seed_a=2000 + seed)
+        ix, x = _run_fused(f, device, noise=n, counts=True)
+        iy, y = _run_fused(f, device, noise=n)
+        assert torch.equal(ix, iy)
+        for k in ("dists", "colors"):
+            assert torch.equal(x[k], y[k]), k
+        zx, zy = x["zbuf"].cpu().numpy(), y["zbuf"].cpu().numpy()
+        other = np.ones_like(valid)
+        np.put_along_axis(other, km, False, -1)
+        np.testing.assert_array_equal(zx[other], zy[other])
+        px, py = np.take_along_axis(zx, km, -1), np.take_along_axis(zy, km, -1)
+        sel = valid.any(-1, keepdims=True) & (px != 0)  # pixels whose d z_max is live
+        xs.append(px[sel]), ys.append(py[sel])
+        gx.append(float(x["gamma"])), gy.append(float(y["gamma"]))
+    xs, ys = np.concatenate(xs).astype(np.float64), np.concatenate(ys).astype(np.float64)
+    assert xs.size > 5000, xs.size
+    se = np.sqrt(xs.var() / xs.size + ys.var() / ys.size)
+    assert abs(xs.mean() - ys.mean()) < 5 * se, (xs.mean(), ys.mean(), se)
+    assert 0.85 < xs.var() / ys.var() < 1.15, (xs.var(), ys.var())
+    gx, gy = np.array(gx), np.array(gy)
+    se = np.sqrt(gx.var(ddof=1) / gx.size + gy.var(ddof=1) / gy.size)
+    assert abs(gx.mean() - gy.mean()) < 5 * se, (gx, gy)
+    assert 0.15 < gx.var() / gy.var() < 7.0, (gx, gy)
 
 
 @pytest.mark.parametrize("mode", ["philox", "injected"])

@@ -15,7 +15,12 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from pertrenderer_amd import _native as nat  # noqa: E402
 
-wl = bench.Workload(torch.device("cuda:0"))
+import argparse  # noqa: E402
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", choices=sorted(bench.CONFIGS), default="cfg2")
+cfg = bench.CONFIGS[ap.parse_args().config]
+# blocks past the first 65536 are not recorded (a cfg4 frame has 524288: images 0-1 only)
+wl = bench.Workload(torch.device("cuda:0"), cfg["image_size"], cfg["K"], cfg["samples"], batch=cfg["batch"])
 for _ in range(3):
     wl.forward().backward()
     torch.cuda.synchronize()

@@ -20,13 +20,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--dense", action="store_true", help="dense synthetic fragments (blend only)")
+    ap.add_argument("--config", choices=sorted(bench.CONFIGS), default="cfg2")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     pa.native_library()
     if args.dense:
         bench.dense_roofline(dev, iters=args.iters)
     else:
-        wl = bench.Workload(dev)
+        c = bench.CONFIGS[args.config]
+        wl = bench.Workload(dev, c["image_size"], c["K"], c["samples"], batch=c["batch"])
         for _ in range(args.iters):
             wl.forward().backward()
             wl.zero_grad()
