@@ -327,7 +327,11 @@ PR_DEV void tail_pair(uint64_t key, uint32_t gp, uint32_t sg, int m, float& s1, 
         v3 = v * v * v;
         const float x2 = x * x;
         if (uu < 1.f - 0.0331f * (x2 * x2)) break;
-        if (logf(uu) < __builtin_fmaf(0.5f, x2, d * ((1.f - v3) + logf(v3)))) break;
+        // natural logs on the hardware log2 (acceptance test only: 1 ulp moves the
+        // boundary by < 1e-6 of the density)
+        const float lu = __builtin_amdgcn_logf(uu) * 0.693147180559945f;
+        const float lv = __builtin_amdgcn_logf(v3) * 0.693147180559945f;
+        if (lu < __builtin_fmaf(0.5f, x2, d * ((1.f - v3) + lv))) break;
       }
       if (t == 8) break;
       u = philox_block(key, gp, t, sg, kTagTail);
@@ -661,7 +665,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   int* CP = reinterpret_cast<int*>(PX + PB * 8);        // [PB] valid-prefix count (K without pix_count)
   int* V = CP + PB;                    // [PB+1] exclusive prefix of CP
   int* OFF = V + PB + 1;               // [PB+1] first B6 row of each pixel, then [PB+1] = lanes per row
-  float* TD = reinterpret_cast<float*>(OFF + PB + 2);   // [PB][4] masked-tail d z sums (B6 -> B7)
+  // [PB][Sa] masked-tail d z terms (B6 -> B7): in DW's space (dead after B5) when it fits
+  float* TD = Sa <= KP1 ? DW : reinterpret_cast<float*>(OFF + PB + 2);
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
   const int64_t blk = pixel_block(g), pix0 = blk * PB;
@@ -674,12 +679,11 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   const bool tail = NOISE == PR_NOISE_PHILOX && !agg_cauchy && pcnt != nullptr && g.tail;
   if (tid < 64) {
     // B6 rows per pixel: its valid slots + background (all K+1 slots without the tail
-    // draw), then 4 tail rows (one per sample of a Philox group) if any slot is masked;
-    // each row is split over nch lanes (power of 2) when the block has few rows.  Wave 0
+    // draw), each split over nch lanes (power of 2) when the block has few rows.  Wave 0
     // scans the counts and the row counts (PB <= 32 lanes).
     scan_counts(pcnt, pix0, npix, K, CP, V);
     const int cp = tid < npix ? CP[tid] : 0;
-    const int v = tid < npix ? (tail ? cp + 1 + (cp < K ? 4 : 0) : KP1) : 0;
+    const int v = tid < npix ? (tail ? cp + 1 : KP1) : 0;
     int x = v;
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(x, o);
@@ -896,8 +900,10 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
 
   // ---- B6: dz_j = mean_s(a_s * score(eps_sj) / gamma) and sum_s a_s * eps_sj * score(eps_sj)
   //          (d gamma; score = eps for Gaussian noise, 2 eps / (1 + eps^2) for Cauchy)
-  //          Rows (OFF) are split over nch adjacent lanes (groups gi = c, c + nch, ...) and
-  //          merged with xor-shuffles; a tail row t carries sample 4g + t of every group.
+  //   6a: slot rows (OFF), each split over nch adjacent lanes (groups gi = c, c + nch, ...)
+  //       and merged with xor-shuffles;
+  //   6b: with the tail draw, one item per (pixel, sample): the masked slots' joint draw,
+  //       a_s * S1 / gamma into TD (summed in B7), a_s * S2 into d gamma.
   {
     // the reference divides each sample's a_s * score by gamma (smoothagg.py:52); one
     // reciprocal here instead of an IEEE division per (slot, sample): within 1 ulp
@@ -908,27 +914,15 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
       const int i = i0 + tid, row = i >> lch, c = i & (nch - 1);
       const bool live = row < nrow;
       float dz = 0.f, q = 0.f;
-      int r = 0, ns = 0;
+      int j = 0;
       if (live) {
         while (OFF[pl + 1] <= row) ++pl;
-        r = row - OFF[pl];
-        ns = tail ? CP[pl] + 1 : KP1;
+        const int r = row - OFF[pl];
+        j = (tail && r == CP[pl]) ? K : r;  // with the tail draw the last row is the background
         const int64_t gp = pix0 + pl;
-        const int j = (tail && r == ns - 1) ? K : r;  // slot row (the last one is the background)
-        const int m = K - CP[pl];                     // masked slots (tail rows)
         for (int gi = c; gi < ng; gi += nch) {
           const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
           const int sbase = (int)(4 * gg) - (NOISE == PR_NOISE_INJECTED ? 0 : p.sample_offset_a);
-          if (r >= ns) {  // tail row: one sample of this group
-            const int t = r - ns, s = sbase + t;
-            const float as = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
-            if (as == 0.f) continue;
-            float s1, s2;
-            tail_pair(sc.ka, (uint32_t)gp, 4u * gg + (uint32_t)t, m, s1, s2);
-            dz += (as * s1) * inv_gamma;
-            q += as * s2;
-            continue;
-          }
           float av[4];
           bool any = false;
 #pragma unroll
@@ -951,11 +945,22 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         }
       }
       for (int mm = 1; mm < nch; mm <<= 1) dz += __shfl_xor(dz, mm);
-      if (live && c == 0) {
-        if (r < ns) ZZ[pl * KP1 + ((tail && r == ns - 1) ? K : r)] = dz / (float)Sa;  // ZZ now holds dL/dz
-        else TD[pl * 4 + (r - ns)] = dz / (float)Sa;
-      }
+      if (live && c == 0) ZZ[pl * KP1 + j] = dz / (float)Sa;  // ZZ now holds dL/dz
       part_q += q;
+    }
+    if (tail) {
+      PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
+        const int s = k, m = K - CP[pl];
+        const float as = AS[pl * Sa + s];
+        float t = 0.f;
+        if (m > 0 && as != 0.f) {
+          float s1, s2;
+          tail_pair(sc.ka, (uint32_t)(pix0 + pl), (uint32_t)(p.sample_offset_a + s), m, s1, s2);
+          t = (as * s1) * inv_gamma;
+          part_q += as * s2;
+        }
+        TD[pl * Sa + s] = t;
+      }
     }
   }
   __syncthreads();
@@ -965,15 +970,23 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   {
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
-    // with the tail draw B6 wrote the valid slots' rows only (the tail's sum is in TD)
+    // with the tail draw B6 wrote the valid slots' rows only; the masked slots' sum is
+    // sum_s TD[s] / Sa
     const int ns = act ? (tail ? CP[pl] : K) : 0, cks = (ns + g.lpp - 1) >> g.lsh;
     const int j0c = l * cks, k1c = min(ns, j0c + cks);
-    float s = 0.f;
-    if (act)
+    const int nt = act && tail ? Sa : 0, ckt = (nt + g.lpp - 1) >> g.lsh;
+    const int t0 = l * ckt, t1 = min(nt, t0 + ckt);
+    float s = 0.f, st = 0.f;
+    if (act) {
       for (int k = j0c; k < k1c; ++k) s += ZZ[pl * KP1 + k];
-    for (int m = 1; m < g.lpp; m <<= 1) s += __shfl_xor(s, m);
+      for (int t = t0; t < t1; ++t) st += TD[pl * Sa + t];
+    }
+    for (int m = 1; m < g.lpp; m <<= 1) {
+      s += __shfl_xor(s, m);
+      st += __shfl_xor(st, m);
+    }
     if (act && l == 0) {
-      if (tail && CP[pl] < K) s += (TD[pl * 4] + TD[pl * 4 + 1]) + (TD[pl * 4 + 2] + TD[pl * 4 + 3]);
+      if (tail) s += st / (float)Sa;
       float dzm = -s - ZZ[pl * KP1 + K];
       dzm = dzm * (PX[pl * 8 + 0] >= p.eps ? 1.f : 0.f);
       PX[pl * 8 + 4] = dzm;
@@ -1271,7 +1284,7 @@ size_t fwd_lds(int PB, int KP1) {
   return (size_t)(2 * PB * KP1 + 6 * PB + 5) * sizeof(float) + (size_t)PB * (KP1 - 1) * sizeof(uint16_t);
 }
 size_t bwd_lds(int PB, int KP1, int Sa) {
-  const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + 15 * PB + 3) * sizeof(float);
+  const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + (Sa > KP1 ? PB * Sa : 0) + 11 * PB + 3) * sizeof(float);
   return b < 16 * sizeof(float) ? 16 * sizeof(float) : b;
 }
 constexpr size_t kLdsBudget = 48 * 1024;  // forward: >= 3 workgroups (12 waves) per CU

@@ -238,8 +238,8 @@ def test_philox_is_deterministic_per_seed(device):
 def test_philox_masked_tail_draw_matches_per_slot_draws(device):
     """With valid-prefix counts the backward draws a pixel's masked agg slots jointly
     (pr_blend.hip tail_pair: Sum eps = sqrt(m) Z, Sum eps^2 = Z^2 + chi2(m-1)) instead of
-    one normal per (slot, sample).  Every gradient that sees per-slot noise is bit-identical
-    to the per-slot path; d zbuf at each pixel's nearest slot (it carries d z_max) and
+    one normal per (slot, sample).  Every gradient that sees per-slot noise matches the
+    per-slot path (to fp32 summation order); d zbuf at each pixel's nearest slot (it carries d z_max) and
     d gamma (Sum eps^2) are equal in distribution: means and variances agree across
     pixels and seeds."""
     f = _synthetic(1, 64, 64, 60, 8, 64, seed=21, p_valid=0.1)
@@ -251,12 +251,14 @@ def test_philox_masked_tail_draw_matches_per_slot_draws(device):
         ix, x = _run_fused(f, device, noise=n, counts=True)
         iy, y = _run_fused(f, device, noise=n)
         assert torch.equal(ix, iy)
-        for k in ("dists", "colors"):
-            assert torch.equal(x[k], y[k]), k
+        assert torch.equal(x["colors"], y["colors"])
+        # per-slot d z sums may be split over a different number of lanes (fewer B6 rows):
+        # fp32 summation order
+        assert_close(x["dists"], y["dists"], rtol=1e-5, name="dists")
         zx, zy = x["zbuf"].cpu().numpy(), y["zbuf"].cpu().numpy()
         other = np.ones_like(valid)
         np.put_along_axis(other, km, False, -1)
-        np.testing.assert_array_equal(zx[other], zy[other])
+        np.testing.assert_allclose(zx[other], zy[other], rtol=1e-5, atol=1e-6 * np.abs(zy).max())
         px, py = np.take_along_axis(zx, km, -1), np.take_along_axis(zy, km, -1)
         sel = valid.any(-1, keepdims=True) & (px != 0)  # pixels whose d z_max is live
         xs.append(px[sel]), ys.append(py[sel])
