@@ -49,7 +49,7 @@ __device__ long long g_blend_prof[2 * kBProfBlocks * 10];
     for (int i_ = 0; i_ < 6; ++i_) r_[2 + i_] = bst_[i_];                                       \
     r_[8] = hw_; r_[9] = 1;                                                                    \
   }
-#define PR_BSTAMP(i) (bst_[i] = __builtin_amdgcn_s_memtime() - bt_, bt_ = __builtin_amdgcn_s_memtime())
+#define PR_BSTAMP(i) (bst_[i] += __builtin_amdgcn_s_memtime() - bt_, bt_ = __builtin_amdgcn_s_memtime())
 #else
 #define PR_BPROF_DECL (void)0
 #define PR_BSTAMP(i) (void)0
@@ -71,9 +71,13 @@ struct Geo {
   int lpp, lsh;                  // lanes per pixel in the pixel phases (256 / PB, 8..64) and log2
   int bpi;                       // blocks per image for the centre-out block order (0: linear)
   int tail;                      // backward: joint masked-tail draw allowed (PR_BLEND_TAIL=0: off)
+  int cap;                       // LDS entry records per workgroup (>= K + 1)
 };
 
 // pixel block of this workgroup: centre-out within each image when blocks tile images
+// a value every lane holds alike (read from LDS: a vector register) into a scalar register
+PR_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
 PR_DEV int64_t pixel_block(const Geo& g) {
   if (g.bpi == 0) return blockIdx.x;
   const int64_t n = blockIdx.x / g.bpi;
@@ -121,59 +125,83 @@ PR_DEV int image_of(int n0, int rem0, int pl, int HW) {
   for (int i_ = tid, pl = tid / (L), k = tid - (tid / (L)) * (L); i_ < (NTOT);          \
        i_ += kThreads, pl += (Q), k += (R), (k >= (L) ? (k -= (L), ++pl) : 0))
 
-// Batched slot walk: the same (pl, k) sequence as PR_FOR_SLOTS, kU items per thread per
-// batch, so a batch's global loads are all in flight before the first is consumed
-// (the slot phases are latency-bound: one HBM round trip per dependent iteration).
+// Batched walks: kU items per thread per batch, so a batch's global loads are all in
+// flight before the first is consumed (the slot phases are latency-bound: one HBM round
+// trip per dependent iteration).
 constexpr int kU = 4;
 struct Batch {
   int pl[kU], k[kU];
   bool ok[kU];
 };
-PR_DEV void batch_next(Batch& b, int& pl, int& k, int i0, int L, int Q, int R, int NTOT) {
-#pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    b.pl[u] = pl;
-    b.k[u] = k;
-    b.ok[u] = i0 + u * kThreads < NTOT;
-    pl += Q;
-    k += R;
-    if (k >= L) { k -= L; ++pl; }
-  }
-}
 
-// Compacted walk over per-pixel item ranges (valid-prefix counts): item i of the block
-// belongs to pixel pl with O(pl) = V[pl] + bonus * pl <= i < O(pl + 1), item k = i - O(pl).
-// V is the exclusive prefix of the pixels' counts; bonus 1 appends one extra item (the
-// background entry) per pixel.  Items grow with i, so pl only moves forward.
-PR_DEV void scan_batch(Batch& b, int& pl, int i0, int n, const int* V, int bonus) {
+// Entry walks of a pass: entry i belongs to pixel OWN[i] (the owner map, filled per pass
+// by fill_owner) and is that pixel's entry i - (ea[pl] - eb): no search per item.
+PR_DEV void entry_batch(Batch& b, int i0, int n, const uint8_t* OWN, const int* ea, int eb) {
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int i = i0 + u * kThreads;
     b.ok[u] = i < n;
-    if (b.ok[u])
-      while (V[pl + 1] + bonus * (pl + 1) <= i) ++pl;
+    const int pl = b.ok[u] ? OWN[i] : 0;
     b.pl[u] = pl;
-    b.k[u] = i - (V[pl] + bonus * pl);
+    b.k[u] = i - (ea[pl] - eb);
   }
 }
 
-// Wave 0: per-pixel valid-prefix counts (clamped to [0, K]; K without pix_count) into CP and
-// their exclusive prefix into V[0..npix] (PB <= 32 lanes).  Returns the total in lane 0..63.
-PR_DEV int scan_counts(const int32_t* pcnt, int64_t pix0, int npix, int K, int* CP, int* V) {
+// The pixel lanes (lpp per pixel) write their pixel's id over its entries (and zero the
+// entries' win counts when CN is given).
+PR_DEV void fill_owner(uint8_t* OWN, const int* ea, int eb, const int* cl, int npix, int lsh, int lpp,
+                       int* CN = nullptr) {
+  const int pl = threadIdx.x >> lsh, l = threadIdx.x & (lpp - 1);
+  if (pl < npix) {
+    const int e0 = ea[pl] - eb, c = cl[pl];
+    for (int e = l; e <= c; e += lpp) {
+      OWN[e0 + e] = (uint8_t)pl;
+      if (CN) CN[e0 + e] = 0;
+    }
+  }
+}
+
+// Wave 0 (PB <= 32 pixels): per-pixel valid-prefix counts CP (clamped to [0, K]; K without
+// pix_count), slot entries CL (CP when compact, else K), the exclusive prefix EA[0..npix] of
+// the entries (CL + 1: the background entry), and the passes: maximal runs of consecutive
+// pixels whose entries fit CAP records (CAP >= K + 1, so a pixel always fits), as starts
+// PS[0..np) + end PS[np] = npix, with the pass count in PS[PB + 1].
+PR_DEV void block_entries(const int32_t* pcnt, int64_t pix0, int npix, int K, bool compact, int CAP, int PB,
+                          int* CL, int* CP, int* EA, int* PS) {
   const int tid = threadIdx.x;
   const int cp = tid < npix ? (pcnt ? min(max((int)pcnt[pix0 + tid], 0), K) : K) : 0;
-  int x = cp;
+  const int c = compact ? cp : K;
+  const int v = tid < npix ? c + 1 : 0;
+  int x = v;
   for (int o = 1; o < 64; o <<= 1) {
     const int y = __shfl_up(x, o);
     if (tid >= o) x += y;
   }
+  const int ex = x - v, tot = __shfl(x, 63);
   if (tid < npix) {
     CP[tid] = cp;
-    V[tid] = x - cp;
+    CL[tid] = c;
+    EA[tid] = ex;
   }
-  const int tot = __shfl(x, 63);
-  if (tid == 0) V[npix] = tot;
-  return tot;
+  if (tid == 0) {
+    EA[npix] = tot;
+    PS[0] = 0;
+  }
+  // greedy passes, uniform over the wave (every value broadcast by shuffles); one pass
+  // when everything fits
+  int np = 0, est = 0;
+  for (int pl = tot > CAP ? 1 : npix; pl < npix; ++pl) {
+    const int end = pl + 1 < npix ? __shfl(ex, pl + 1) : tot;  // EA[pl + 1]
+    if (end - est > CAP) {
+      ++np;
+      est = __shfl(ex, pl);
+      if (tid == 0) PS[np] = pl;
+    }
+  }
+  if (tid == 0) {
+    PS[np + 1] = npix;
+    PS[PB + 1] = np + 1;
+  }
 }
 
 // Wave-wide append of the lanes with `want` to an LDS queue: one LDS atomic per wave,
@@ -370,47 +398,68 @@ PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
 
 // ================================================================== forward
 // CM: colour mode, 0 = weights out (no colour), 1 = texel colours, 2 = vertex colours
-template <int NOISE, bool RAST, int CM>
+//
+// LDS holds one record per ENTRY: a pixel's slot entries (its valid prefix with
+// pix_count, else all K slots) followed by its background entry.  A workgroup owns PB
+// pixels and walks them in passes of consecutive pixels whose entries fit the CAP
+// records (one pass unless the block is unusually deep), so a block is sized by the
+// fragments it really has, not by K.
+// MULTI: the block may need several passes (CAP < PB * (K + 1)); without it the pass loop
+// is a single straight-line pass (no loop-carried registers: 46 instead of 70 VGPRs).
+template <int NOISE, bool RAST, int CM, bool MULTI>
 __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(PRBlendFwdArgs a, Geo g, int NC) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
   const Sc sc = resolve(p);
-  const int K = g.K, KP1 = g.KP1, PB = g.PB;
-  float* A = smem;                 // [PB][KP1] prob, then int win counts
-  float* B = A + PB * KP1;         // [PB][KP1] z_inv, then logits z
-  float* PX = B + PB * KP1;        // [PB][4] z_max, alpha, max logit, candidate count
-  int* CP = reinterpret_cast<int*>(PX + PB * 4);            // [PB] valid-prefix count (K without pix_count)
-  int* V = CP + PB;                                         // [PB+1] exclusive prefix of CP
-  int* QN = V + PB + 1;                                     // rast queue length
-  uint16_t* Q = reinterpret_cast<uint16_t*>(QN + 4);        // [PB*K] rast queue (pl << 8 | k)
-  uint8_t* LC = reinterpret_cast<uint8_t*>(Q);              // [PB][KP1] argmax candidates (after 1b)
+  const int K = g.K, KP1 = g.KP1, PB = g.PB, CAP = g.cap;
+  float* A = smem;                 // [CAP] prob (the distance while queued), then int win counts
+  float* B = A + CAP;              // [CAP] z_inv, then logits z
+  float* PX = B + CAP;             // [PB][4] z_max, alpha, max logit, candidate count
+  int* CL = reinterpret_cast<int*>(PX + PB * 4);            // [PB] slot entries (valid prefix or K)
+  int* CP = CL + PB;                                        // [PB] valid-prefix count (K without pix_count)
+  int* EA = CP + PB;                                        // [PB+1] exclusive prefix of entries (CL + 1)
+  int* PS = EA + PB + 1;                                    // [PB+2] pass starts; [PB+1] = pass count
+  int* QN = PS + PB + 2;                                    // rast queue length
+  uint16_t* Q = reinterpret_cast<uint16_t*>(QN + 4);        // [CAP] rast queue (pl << 8 | k)
+  uint8_t* LC = reinterpret_cast<uint8_t*>(Q);              // [CAP] argmax candidates (after 1b)
+  uint8_t* OWN = reinterpret_cast<uint8_t*>(Q + CAP);       // [CAP] pixel of each entry
   int* CNT = reinterpret_cast<int*>(A);
   int* PXI = reinterpret_cast<int*>(PX);
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
-  const int64_t blk = pixel_block(g), pix0 = blk * PB;
-  const int npix = (int)min((int64_t)PB, g.P - pix0);
+  const int64_t blk = pixel_block(g), bpix0 = blk * PB;
+  const int bnpix = (int)min((int64_t)PB, g.P - bpix0);
+  const int32_t* pcnt = a.pix_count;
+  if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, pcnt != nullptr, CAP, PB, CL, CP, EA, PS);
+  __syncthreads();
+  const float gal = sc.gamma / sc.alpha;
+
+  const int npass = MULTI ? uni(PS[PB + 1]) : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+  const int ps = uni(PS[pass]), npix = uni(PS[pass + 1]) - ps;
+  const int64_t pix0 = bpix0 + ps;
+  const int* cl = CL + ps;
+  const int* cpv = CP + ps;
+  const int* ea = EA + ps;
+  const int eb = uni(ea[0]);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   if (tid == 0) *QN = 0;
-  const int32_t* pcnt = a.pix_count;
-  if (tid < 64) scan_counts(pcnt, pix0, npix, K, CP, V);
+  fill_owner(OWN, ea, eb, cl, npix, g.lsh, g.lpp);
   __syncthreads();
 
-  // ---- 1a: slots, kU per thread in flight: mask, z_inv, and the probability wherever
-  //          it needs no noise (masked, or saturated Gaussian); the rest is queued.  With
-  //          valid-prefix counts only the valid slots are walked: no later phase reads a
-  //          masked slot's LDS entry (its prob is 0, its z_inv 0, its logit -inf)
+  // ---- 1a: slot entries, kU per thread in flight: mask, z_inv, and the probability
+  //          wherever it needs no noise (masked, or saturated Gaussian); the rest is queued
   {
     // saturation shortcut of rast_count / rast_count_score (Philox Gaussian; the score
     // form also needs variance reduction)
     const bool sat_ok = NOISE == PR_NOISE_PHILOX && !(p.flags & PR_BLEND_RAST_CAUCHY) &&
                         !(a.rast_cache && (p.flags & PR_BLEND_RAST_WOVR));
-    int cpl = tid / K, ck = tid - (tid / K) * K, spl = 0;
-    const int nit = pcnt ? V[npix] : npix * K;
+    const int nit = uni(ea[npix]) - eb;  // entries of the pass (background entries skipped)
     for (int i0 = tid; i0 < nit; i0 += kU * kThreads) {
       Batch bt;
-      if (pcnt) scan_batch(bt, spl, i0, nit, V, 0);
-      else batch_next(bt, cpl, ck, i0, K, g.qK, g.rK, nit);
+      entry_batch(bt, i0, nit, OWN, ea, eb);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) bt.ok[u] = bt.ok[u] && bt.k[u] < cl[bt.pl[u]];
       bool mk[kU];
       float dd[kU], zb[kU];
 #pragma unroll
@@ -420,7 +469,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         if (bt.ok[u]) {
           const int64_t gs = (pix0 + bt.pl[u]) * K + bt.k[u];
           // with valid-prefix counts nothing is read at a masked slot
-          mk[u] = pcnt ? bt.k[u] < CP[bt.pl[u]] : slot_mask(a.pix_to_face, a.mask, gs);
+          mk[u] = pcnt ? bt.k[u] < cpv[bt.pl[u]] : slot_mask(a.pix_to_face, a.mask, gs);
           if (mk[u] || !pcnt) {
             dd[u] = RAST ? a.dists[gs] : a.prob[gs];
             zb[u] = a.zbuf[gs];
@@ -429,7 +478,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int pl = bt.pl[u], k = bt.k[u], li = pl * KP1 + k;
+        const int pl = bt.pl[u], k = bt.k[u], li = i0 + u * kThreads;  // entry index
         bool want = false;
         if (bt.ok[u]) {
           const int64_t gs = (pix0 + pl) * K + k;
@@ -465,7 +514,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   if constexpr (RAST) {
     const int nq = *QN;
     for (int i = tid; i < nq; i += kThreads) {
-      const int e = Q[i], pl = e >> 8, k = e & 255, li = pl * KP1 + k;
+      const int e = Q[i], pl = e >> 8, k = e & 255, li = ea[pl] - eb + k;
       const int64_t gp = pix0 + pl, gs = gp * K + k;
       const float dist = A[li];
       float prob;
@@ -484,33 +533,31 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   PR_BSTAMP(0);
 
   // ---- 2: per pixel (lpp lanes): alpha, z_max, logits, largest logit, and the list of
-  //         argmax candidates (ascending j).  A pixel's entries are its cp walked slots,
-  //         then the background (entry cp -> j = K); lanes take contiguous chunks
+  //         argmax candidates (ascending j).  A pixel's entries are its cl slot entries,
+  //         then the background (entry cl -> j = K); lanes take contiguous chunks
   {
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
-    const int cp = act ? CP[pl] : 0, ckp = (cp + g.lpp) >> g.lsh;  // ceil((cp + 1) / lpp)
-    const int j0 = l * ckp, j1 = min(cp + 1, j0 + ckp), k1 = min(cp, j1);
+    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, ckp = (c + g.lpp) >> g.lsh;  // ceil((c+1)/lpp)
+    const int j0 = l * ckp, j1 = min(c + 1, j0 + ckp), k1 = min(c, j1);
     float al = 1.f, zm = kNegInf;
     if (act)
       for (int k = j0; k < k1; ++k) {
-        al *= (1.f - A[pl * KP1 + k]);
-        zm = fmaxf(zm, B[pl * KP1 + k]);
+        al *= (1.f - A[e0 + k]);
+        zm = fmaxf(zm, B[e0 + k]);
       }
     for (int m = 1; m < g.lpp; m <<= 1) {
       al *= __shfl_xor(al, m);
       zm = fmaxf(zm, __shfl_xor(zm, m));
     }
-    if (cp < K) zm = fmaxf(zm, 0.f);  // masked slots' z_inv (0) are in the reference's max
+    if (c < K) zm = fmaxf(zm, 0.f);  // slots past the walked ones: z_inv 0, in the reference's max
     const float zmax = zm < p.eps ? p.eps : zm;
-    const float gal = sc.gamma / sc.alpha;
     float zl = kNegInf;
     if (act)
       for (int e = j0; e < j1; ++e) {
-        const int j = e < cp ? e : K;
-        const float z = j < K ? gal * logf(A[pl * KP1 + j]) + B[pl * KP1 + j] - zmax : p.eps - zmax;
-        B[pl * KP1 + j] = z;
-        CNT[pl * KP1 + j] = 0;
+        const float z = e < c ? gal * logf(A[e0 + e]) + B[e0 + e] - zmax : p.eps - zmax;
+        B[e0 + e] = z;
+        CNT[e0 + e] = 0;
         zl = fmaxf(zl, z);
       }
     for (int m = 1; m < g.lpp; m <<= 1) zl = fmaxf(zl, __shfl_xor(zl, m));
@@ -523,21 +570,20 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     int nc = 0;
     if (act)
       for (int e = j0; e < j1; ++e) {
-        const float z = B[pl * KP1 + (e < cp ? e : K)];
+        const float z = B[e0 + e];
         nc += (z > kNegInf && z >= zfloor) ? 1 : 0;
       }
-    int off = 0, tot = 0;
-    const int lane8 = (tid & 63) & ~(g.lpp - 1);  // the pixel's first lane
-    for (int o = 0; o < g.lpp; ++o) {
-      const int t = __shfl(nc, lane8 + o);
-      off += o < l ? t : 0;
-      tot += t;
+    int inc = nc;  // inclusive scan of the lane counts within the pixel's lanes
+    for (int o = 1; o < g.lpp; o <<= 1) {
+      const int y = __shfl_up(inc, o, g.lpp);
+      if (l >= o) inc += y;
     }
+    int off = inc - nc;
+    const int tot = __shfl(inc, g.lpp - 1, g.lpp);
     if (act)
       for (int e = j0; e < j1; ++e) {
-        const int j = e < cp ? e : K;
-        const float z = B[pl * KP1 + j];
-        if (z > kNegInf && z >= zfloor) LC[pl * KP1 + off++] = (uint8_t)j;
+        const float z = B[e0 + e];
+        if (z > kNegInf && z >= zfloor) LC[e0 + off++] = (uint8_t)(e < c ? e : K);
       }
     if (act && l == 0) {
       PX[pl * 4 + 0] = zmax;
@@ -560,13 +606,14 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
       const int pl = act ? pg / ng : 0, gi = act ? pg - pl * ng : 0;
       const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
       const int64_t gp = pix0 + pl;
+      const int e0 = ea[pl] - eb, cpl = cl[pl];
       float best[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
       int bidx[4] = {-1, -1, -1, -1};
       if (act) {
         const int len = PXI[pl * 4 + 3];
         for (int i = c; i < len; i += NC) {  // ascending j within the thread
-          const int j = LC[pl * KP1 + i];
-          const float z = B[pl * KP1 + j];
+          const int j = LC[e0 + i];
+          const float z = B[e0 + (j == K ? cpl : j)];
           float e[4];
           agg_noise4<NOISE>(p, sc, (uint32_t)gp, j, gg, g.P, KP1, e);
 #pragma unroll
@@ -593,7 +640,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
           if (s < 0 || s >= p.Sa) continue;
           const int w = bidx[q] < 0 ? K : bidx[q];
           a.winners[gp * p.Sa + s] = (uint8_t)w;
-          atomicAdd(&CNT[pl * KP1 + w], 1);
+          atomicAdd(&CNT[e0 + (w == K ? cpl : w)], 1);
         }
       }
     }
@@ -604,12 +651,13 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   // ---- 4: outputs
   const float fSa = (float)p.Sa;
   if constexpr (CM != 0) {
-    // the pixel's lanes sweep its slots; only slots that won a sample are read
+    // the pixel's lanes sweep its slot entries; only slots that won a sample are read
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
     if (pl < npix) {
-      for (int k = l; k < CP[pl]; k += g.lpp) {  // masked slots never win (their CNT is not set)
-        const int cw = CNT[pl * KP1 + k];
+      const int e0 = ea[pl] - eb;
+      for (int k = l; k < cl[pl]; k += g.lpp) {
+        const int cw = CNT[e0 + k];
         if (cw == 0) continue;
         const float w = (float)cw / fSa;
         float c[3];
@@ -625,7 +673,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
       acc2 += __shfl_xor(acc2, m);
     }
     if (pl < npix && l == 0) {
-      const float wb = (float)CNT[pl * KP1 + K] / fSa;
+      const float wb = (float)CNT[ea[pl] - eb + cl[pl]] / fSa;
       float4 o;
       o.x = acc0 + wb * p.background[0];
       o.y = acc1 + wb * p.background[1];
@@ -634,93 +682,80 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
       reinterpret_cast<float4*>(a.image)[pix0 + pl] = o;
     }
   } else {
-    PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {
-      const int cw = (k < CP[pl] || k == K) ? CNT[pl * KP1 + k] : 0;
+    PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {  // dense K+1 weights: 0 past the slot entries
+      const int c = cl[pl];
+      const int cw = (k < c || k == K) ? CNT[ea[pl] - eb + (k == K ? c : k)] : 0;
       a.weights[(pix0 + pl) * KP1 + k] = (float)cw / fSa;
     }
   }
+  __syncthreads();  // the next pass reuses every LDS record
+  }  // passes
 #ifdef PR_BLEND_PROFILE
-  __syncthreads();
   PR_BSTAMP(3);
   PR_BPROF_DUMP(0);
 #endif
 }
 
 // ================================================================= backward
-template <int NOISE, bool RAST, int CM>
+// Same entry layout and passes as the forward.  Entries are compacted (a pixel's valid
+// slots + background) when the masked tail is drawn jointly (B6); otherwise every slot
+// keeps its entry, since injected / Cauchy noise needs each masked slot's own d z.
+template <int NOISE, bool RAST, int CM, bool MULTI>
 __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
   const Sc sc = resolve(p);
-  const int K = g.K, KP1 = g.KP1, PB = g.PB;
+  const int K = g.K, KP1 = g.KP1, PB = g.PB, CAP = g.cap;
   const int Sa = p.Sa;
-  float* PR = smem;                    // [PB][KP1] prob
-  float* ZZ = PR + PB * KP1;           // [PB][KP1] z_inv -> z -> dL/dz
-  float* GM = ZZ + PB * KP1;           // [PB][KP1] rast score mean (gmaps)
-  float* EX = GM + PB * KP1;           // [PB][KP1] exclusive products of (1 - prob)
-  float* DW = EX + PB * KP1;           // [PB][KP1] dL/dW
-  int* CN = reinterpret_cast<int*>(DW + PB * KP1);      // [PB][KP1] win counts
-  float* AS = reinterpret_cast<float*>(CN + PB * KP1);  // [PB][Sa] a_s
-  float* PX = AS + PB * Sa;            // [PB][8] per-pixel scalars
-  int* CP = reinterpret_cast<int*>(PX + PB * 8);        // [PB] valid-prefix count (K without pix_count)
-  int* V = CP + PB;                    // [PB+1] exclusive prefix of CP
-  int* OFF = V + PB + 1;               // [PB+1] first B6 row of each pixel, then [PB+1] = lanes per row
-  // [PB][Sa] masked-tail d z terms (B6 -> B7): in DW's space (dead after B5) when it fits
-  float* TD = Sa <= KP1 ? DW : reinterpret_cast<float*>(OFF + PB + 2);
+  float* PR = smem;                    // [CAP] prob
+  float* ZZ = PR + CAP;                // [CAP] z_inv -> dL/dz
+  float* GM = ZZ + CAP;                // [CAP] rast score mean (gmaps)
+  float* EX = GM + CAP;                // [CAP] exclusive products of (1 - prob)
+  float* DW = EX + CAP;                // [CAP] dL/dW
+  int* CN = reinterpret_cast<int*>(DW + CAP);           // [CAP] win counts
+  float* AS = reinterpret_cast<float*>(CN + CAP);       // [PB][Sa] a_s, then the tail terms (B6b)
+  float* PX = AS + PB * Sa;            // [PB][12] per-pixel scalars; [8..12) the upstream image gradient
+  int* CL = reinterpret_cast<int*>(PX + PB * 12);       // [PB] slot entries (valid prefix or K)
+  int* CP = CL + PB;                   // [PB] valid-prefix count (K without pix_count)
+  int* EA = CP + PB;                   // [PB+1] exclusive prefix of entries (CL + 1)
+  int* PS = EA + PB + 1;               // [PB+2] pass starts; [PB+1] = pass count
+  uint8_t* OWN = reinterpret_cast<uint8_t*>(PS + PB + 2);  // [CAP] pixel of each entry
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
-  const int64_t blk = pixel_block(g), pix0 = blk * PB;
-  const int npix = (int)min((int64_t)PB, g.P - pix0);
+  const int64_t blk = pixel_block(g), bpix0 = blk * PB;
+  const int bnpix = (int)min((int64_t)PB, g.P - bpix0);
   const int32_t* pcnt = a.pix_count;
   const int ng = agg_num_groups(p), g0 = agg_first_group(p);
   const bool agg_cauchy = p.flags & PR_BLEND_AGG_CAUCHY;
   // B6 draws the masked tail jointly (tail_pair) in Philox Gaussian mode when the valid
   // prefix is known; injected noise (parity) and Cauchy noise keep one row per slot
   const bool tail = NOISE == PR_NOISE_PHILOX && !agg_cauchy && pcnt != nullptr && g.tail;
-  if (tid < 64) {
-    // B6 rows per pixel: its valid slots + background (all K+1 slots without the tail
-    // draw), each split over nch lanes (power of 2) when the block has few rows.  Wave 0
-    // scans the counts and the row counts (PB <= 32 lanes).
-    scan_counts(pcnt, pix0, npix, K, CP, V);
-    const int cp = tid < npix ? CP[tid] : 0;
-    const int v = tid < npix ? (tail ? cp + 1 : KP1) : 0;
-    int x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(x, o);
-      if (tid >= o) x += y;
-    }
-    if (tid < npix) OFF[tid] = x - v;
-    const int o = __shfl(x, 63);
-    if (tid == 0) {
-      int nch = 1;
-      while (nch < 64 && 2 * nch <= ng && 2 * nch * o <= kThreads) nch <<= 1;
-      OFF[npix] = o;
-      OFF[PB + 1] = nch;
-    }
-  }
+  if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, tail, CAP, PB, CL, CP, EA, PS);
   __syncthreads();
-  const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   const float gal = sc.gamma / sc.alpha;
   float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
 
-  // ---- B1: slots + background entry: prob, z_inv, rast score, dL/dW (kU items per
-  //          thread with their global loads in flight together).  With valid-prefix
-  //          counts a pixel's entries are its valid slots and the background: no later
-  //          phase reads a masked slot's LDS entry except B6/B7 without the tail draw,
-  //          which write and read only their own ZZ rows
+  const int npass = MULTI ? uni(PS[PB + 1]) : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+  const int ps = uni(PS[pass]), npix = uni(PS[pass + 1]) - ps;
+  const int64_t pix0 = bpix0 + ps;
+  const int* cl = CL + ps;
+  const int* cpv = CP + ps;
+  const int* ea = EA + ps;
+  const int eb = uni(ea[0]), nent = uni(ea[npix]) - eb;
+  const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
+  fill_owner(OWN, ea, eb, cl, npix, g.lsh, g.lpp, CN);
+  __syncthreads();
+
+  // ---- B1: entries (slots + background): prob, z_inv, rast score, dL/dW (kU items per
+  //          thread with their global loads in flight together)
   {
-    int cpl = tid / KP1, ck = tid - (tid / KP1) * KP1, spl = 0;
-    const int nit = pcnt ? V[npix] + npix : npix * KP1;
-    for (int i0 = tid; i0 < nit; i0 += kU * kThreads) {
+    for (int i0 = tid; i0 < nent; i0 += kU * kThreads) {
       Batch bt;
-      if (pcnt) {
-        scan_batch(bt, spl, i0, nit, V, 1);
+      entry_batch(bt, i0, nent, OWN, ea, eb);
 #pragma unroll
-        for (int u = 0; u < kU; ++u)
-          if (bt.ok[u] && bt.k[u] == CP[bt.pl[u]]) bt.k[u] = K;  // the background entry
-      } else {
-        batch_next(bt, cpl, ck, i0, KP1, g.qK1, g.rK1, nit);
-      }
+      for (int u = 0; u < kU; ++u)
+        if (bt.ok[u] && bt.k[u] == cl[bt.pl[u]]) bt.k[u] = K;  // the background entry
       bool mk[kU];
       float2 pg[kU];  // (prob, gm) from the cache / input prob, or (dist, -) to recount
       float zb[kU], dw[kU];
@@ -735,7 +770,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         if (k < K) {
           const int64_t gs = gp * K + k;
           // with valid-prefix counts nothing is read at a masked slot (prob, score, z_inv are 0)
-          mk[u] = pcnt ? k < CP[pl] : slot_mask(a.pix_to_face, a.mask, gs);
+          mk[u] = pcnt ? k < cpv[pl] : slot_mask(a.pix_to_face, a.mask, gs);
           if (!mk[u] && pcnt) continue;
           if constexpr (RAST) {
             if (a.rast_cache) pg[u] = reinterpret_cast<const float2*>(a.rast_cache)[gs];
@@ -744,18 +779,18 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
             pg[u].x = a.prob[gs];
           }
           zb[u] = a.zbuf[gs];
-          // CM 2: dW computed on demand in B5 (only winners and j0 need it)
           if constexpr (CM == 1) {
             const float4 gi = reinterpret_cast<const float4*>(a.grad_image)[gp];
             const float* c = a.colors + gs * 3;
             dw[u] = (gi.x * c[0] + gi.y * c[1]) + gi.z * c[2];
-          } else if constexpr (CM == 0) {
+          } else if constexpr (CM == 0) {  // (CM 2: dW of the slots that won a sample, B5b)
             dw[u] = a.grad_weights[gp * KP1 + k];
           }
         } else {
-          if constexpr (CM != 0) {
+          if constexpr (CM != 0) {  // the background entry also keeps the pixel's g_image for B8
             const float4 gi = reinterpret_cast<const float4*>(a.grad_image)[gp];
             dw[u] = (gi.x * p.background[0] + gi.y * p.background[1]) + gi.z * p.background[2];
+            *reinterpret_cast<float4*>(PX + pl * 12 + 8) = gi;
           } else {
             dw[u] = a.grad_weights[gp * KP1 + K];
           }
@@ -764,8 +799,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         if (!bt.ok[u]) continue;
-        const int pl = bt.pl[u], k = bt.k[u], li = pl * KP1 + k;
-        CN[li] = 0;
+        const int pl = bt.pl[u], k = bt.k[u], li = i0 + u * kThreads;  // entry index
         DW[li] = dw[u];
         if (k == K) continue;
         const int64_t gp = pix0 + pl, gs = gp * K + k;
@@ -773,15 +807,9 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         const float mf = m ? 1.f : 0.f;
         float prob = pg[u].x, gm = pg[u].y;
         if constexpr (RAST) {
-          if (!a.rast_cache) {
-            gm = 0.f;
-            prob = 0.f;
-            if (m) {
-              float gacc;
-              const int cnt = rast_count_score<NOISE>(p, sc, pg[u].x, (uint32_t)gp, k, gs, g.PK, gacc);
-              prob = ((float)cnt / (float)p.Sr) * mf;
-              gm = gacc / (float)p.Sr;
-            }
+          if (!a.rast_cache) {  // recount below (B1r): keep the distance and the mask
+            prob = pg[u].x;
+            gm = mf;
           }
         }
         const int n = image_of(n0, rem0, pl, g.HW);
@@ -791,54 +819,81 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         GM[li] = gm;
       }
     }
+    // B1r: without the forward's cache, the Monte-Carlo rasterization again (same arithmetic
+    // as the forward's 1b); each thread revisits its own B1 entries, one at a time
+    if constexpr (RAST) {
+      if (!a.rast_cache) {
+        for (int li = tid; li < nent; li += kThreads) {
+          const int pl = OWN[li], k = li - (ea[pl] - eb);
+          if (k >= cl[pl]) continue;
+          float prob = 0.f, gm = 0.f;
+          if (GM[li] != 0.f) {
+            const int64_t gp = pix0 + pl, gs = gp * K + k;
+            float gacc;
+            const int cnt = rast_count_score<NOISE>(p, sc, PR[li], (uint32_t)gp, k, gs, g.PK, gacc);
+            prob = ((float)cnt / (float)p.Sr) * 1.f;
+            gm = gacc / (float)p.Sr;
+          }
+          PR[li] = prob;
+          GM[li] = gm;
+        }
+      }
+    }
+    // win counts of the forward's winners (CN zeroed with the owner map)
+    PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
+      const int jw = a.winners[(pix0 + pl) * Sa + k];
+      atomicAdd(&CN[ea[pl] - eb + (jw == K ? cl[pl] : jw)], 1);
+    }
   }
   __syncthreads();
   PR_BSTAMP(0);
 
-  // ---- B2: per pixel (lpp lanes, contiguous chunks of its entries: the cp walked slots,
-  //          then the background as entry cp -> j = K): z_max + first argmax, exclusive
+  // ---- B2: per pixel (lpp lanes, contiguous chunks of its entries: the cl slot entries,
+  //          then the background as entry cl -> j = K): z_max + first argmax, exclusive
   //          products for the alpha gradient, logits, unperturbed argmax j0
   {
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
-    const int cp = act ? CP[pl] : 0, ckp = (cp + g.lpp) >> g.lsh;  // ceil((cp + 1) / lpp)
-    const int j0c = l * ckp, j1c = min(cp + 1, j0c + ckp), k1c = min(cp, j1c);
+    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, ckp = (c + g.lpp) >> g.lsh;  // ceil((c+1)/lpp)
+    const int j0c = l * ckp, j1c = min(c + 1, j0c + ckp), k1c = min(c, j1c);
     float zm = kNegInf, tp = 1.f;
     int km = 1 << 30;
     if (act)
       for (int k = j0c; k < k1c; ++k) {
-        const float zi = ZZ[pl * KP1 + k];
+        const float zi = ZZ[e0 + k];
         if (zi > zm) { zm = zi; km = k; }
-        tp *= (1.f - PR[pl * KP1 + k]);
+        tp *= (1.f - PR[e0 + k]);
       }
     for (int m = 1; m < g.lpp; m <<= 1) {
       const float oz = __shfl_xor(zm, m);
       const int ok = __shfl_xor(km, m);
       if (oz > zm || (oz == zm && ok < km)) { zm = oz; km = ok; }
     }
-    // masked slots hold z_inv = 0 in the reference's max; they follow every walked slot, so a
-    // walked slot wins a tie
-    if (cp < K && 0.f > zm) { zm = 0.f; km = cp; }
+    // slots past the slot entries hold z_inv = 0 in the reference's max; they follow every
+    // walked slot, so a walked slot wins a tie
+    if (c < K && 0.f > zm) { zm = 0.f; km = c; }
     if (km == (1 << 30)) km = 0;
     const float zmax = zm < p.eps ? p.eps : zm;
     if constexpr (CM != 0) {
-      // exclusive products across the lane chunks, then within the chunk
-      float pre = 1.f, suf = 1.f;
-      const int lane8 = (tid & 63) & ~(g.lpp - 1);  // the pixel's first lane
-      for (int o = 0; o < g.lpp; ++o) {
-        const float t = __shfl(tp, lane8 + o);
-        if (o < l) pre *= t;
-        if (o > l) suf *= t;
+      // exclusive products across the lane chunks (log-step scans up and down the
+      // pixel's lanes), then within the chunk
+      float inc = tp, sinc = tp;
+      for (int o = 1; o < g.lpp; o <<= 1) {
+        const float y = __shfl_up(inc, o, g.lpp), z = __shfl_down(sinc, o, g.lpp);
+        if (l >= o) inc *= y;
+        if (l + o < g.lpp) sinc *= z;
       }
-      if (act && l == 0) PX[pl * 8 + 5] = tp * suf;  // prod (1 - prob): a masked slot's exclusive product
+      const float iu = __shfl_up(inc, 1, g.lpp), sd = __shfl_down(sinc, 1, g.lpp);
+      float pre = l > 0 ? iu : 1.f, suf = l + 1 < g.lpp ? sd : 1.f;
+      if (act && l == 0) PX[pl * 12 + 5] = tp * suf;  // prod (1 - prob): a masked slot's exclusive product
       if (act) {
         for (int k = k1c - 1; k >= j0c; --k) {
-          EX[pl * KP1 + k] = suf;
-          suf *= (1.f - PR[pl * KP1 + k]);
+          EX[e0 + k] = suf;
+          suf *= (1.f - PR[e0 + k]);
         }
         for (int k = j0c; k < k1c; ++k) {
-          EX[pl * KP1 + k] = pre * EX[pl * KP1 + k];
-          pre *= (1.f - PR[pl * KP1 + k]);
+          EX[e0 + k] = pre * EX[e0 + k];
+          pre *= (1.f - PR[e0 + k]);
         }
       }
     }
@@ -846,8 +901,8 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     int jb = 1 << 30;
     if (act)
       for (int e = j0c; e < j1c; ++e) {
-        const int j = e < cp ? e : K;
-        const float z = j < K ? gal * logf(PR[pl * KP1 + j]) + ZZ[pl * KP1 + j] - zmax : p.eps - zmax;
+        const int j = e < c ? e : K;
+        const float z = j < K ? gal * logf(PR[e0 + e]) + ZZ[e0 + e] - zmax : p.eps - zmax;
         if (z > zb || jb == (1 << 30)) { zb = z; jb = j; }
       }
     for (int m = 1; m < g.lpp; m <<= 1) {
@@ -856,69 +911,65 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
       if (oj != (1 << 30) && (jb == (1 << 30) || oz > zb || (oz == zb && oj < jb))) { zb = oz; jb = oj; }
     }
     if (act && l == 0) {
-      PX[pl * 8 + 0] = zm;          // raw max z_inv (clamp test)
-      PX[pl * 8 + 2] = (float)km;   // its first index
-      PX[pl * 8 + 3] = (float)jb;   // unperturbed argmax of the K+1 logits
+      PX[pl * 12 + 0] = zm;          // raw max z_inv (clamp test)
+      PX[pl * 12 + 2] = (float)km;   // its first index
+      PX[pl * 12 + 3] = (float)jb;   // unperturbed argmax of the K+1 logits
+    }
+    if constexpr (CM == 2) {
+      // dW = g_rgb . colour of the slot entries B5 reads (a win, or j0): the colour is
+      // interpolated from the vertex colours here, once per such entry
+      if (act) {
+        const float* gi = PX + pl * 12 + 8;
+        for (int e = l; e < c; e += g.lpp) {
+          if (CN[e0 + e] == 0 && e != jb) continue;
+          float cc[3];
+          slot_color<CM>(a, (pix0 + pl) * K + e, cc);
+          DW[e0 + e] = (gi[0] * cc[0] + gi[1] * cc[1]) + gi[2] * cc[2];
+        }
+      }
     }
   }
   __syncthreads();
   PR_BSTAMP(1);
 
-  // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0], win counts
+  // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0] (win counts: B1, CM 2's dW: B2)
   PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
     const int s = k;
     const int64_t gp = pix0 + pl;
+    const int e0 = ea[pl] - eb, c = cl[pl];
     const int jw = a.winners[gp * Sa + s];
-    const int j0 = (int)PX[pl * 8 + 3];
+    const int j0 = (int)PX[pl * 12 + 3];
+    const int ew = e0 + (jw == K ? c : jw), e0j = e0 + (j0 == K ? c : j0);
     // GaussianAgg_wovr: a_s = <g, w_s> (smoothagg.py:118); else <g, w_s - vr'>
     const bool nobase = (p.flags & PR_BLEND_AGG_WOVR) && !(p.flags & PR_BLEND_AGG_CAUCHY);
-    float as;
-    if constexpr (CM == 2) {  // dW_j = g_rgb . colour_j for the two slots involved
-      const float* gi = a.grad_image + gp * 4;
-      float dw2[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int j = e == 0 ? jw : j0;
-        if (j == K) {
-          dw2[e] = DW[pl * KP1 + K];
-        } else {
-          float c[3];
-          slot_color<CM>(a, gp * K + j, c);
-          dw2[e] = (gi[0] * c[0] + gi[1] * c[1]) + gi[2] * c[2];
-        }
-      }
-      as = nobase ? dw2[0] : dw2[0] - dw2[1];
-    } else {
-      as = nobase ? DW[pl * KP1 + jw] : DW[pl * KP1 + jw] - DW[pl * KP1 + j0];
-    }
+    const float as = nobase ? DW[ew] : DW[ew] - DW[e0j];
     AS[pl * Sa + s] = as;
     part_a += as;
-    atomicAdd(&CN[pl * KP1 + jw], 1);
   }
   __syncthreads();
   PR_BSTAMP(2);
 
   // ---- B6: dz_j = mean_s(a_s * score(eps_sj) / gamma) and sum_s a_s * eps_sj * score(eps_sj)
   //          (d gamma; score = eps for Gaussian noise, 2 eps / (1 + eps^2) for Cauchy)
-  //   6a: slot rows (OFF), each split over nch adjacent lanes (groups gi = c, c + nch, ...)
+  //   6a: one row per entry, split over nch adjacent lanes (groups gi = c, c + nch, ...)
   //       and merged with xor-shuffles;
   //   6b: with the tail draw, one item per (pixel, sample): the masked slots' joint draw,
-  //       a_s * S1 / gamma into TD (summed in B7), a_s * S2 into d gamma.
+  //       a_s * S2 into d gamma and a_s * S1 / gamma over a_s in AS (summed in B7).
   {
     // the reference divides each sample's a_s * score by gamma (smoothagg.py:52); one
     // reciprocal here instead of an IEEE division per (slot, sample): within 1 ulp
     const float inv_gamma = 1.f / sc.gamma;
-    const int nrow = OFF[npix], nch = OFF[PB + 1], lch = 31 - __builtin_clz(nch);
-    int pl = 0;
-    for (int i0 = 0; i0 < nrow * nch; i0 += kThreads) {  // uniform trip count (shuffles below)
+    int nch = 1;
+    while (nch < 64 && 2 * nch <= ng && 2 * nch * nent <= kThreads) nch <<= 1;
+    const int lch = 31 - __builtin_clz(nch);
+    for (int i0 = 0; i0 < nent * nch; i0 += kThreads) {  // uniform trip count (shuffles below)
       const int i = i0 + tid, row = i >> lch, c = i & (nch - 1);
-      const bool live = row < nrow;
+      const bool live = row < nent;
       float dz = 0.f, q = 0.f;
-      int j = 0;
       if (live) {
-        while (OFF[pl + 1] <= row) ++pl;
-        const int r = row - OFF[pl];
-        j = (tail && r == CP[pl]) ? K : r;  // with the tail draw the last row is the background
+        const int pl = OWN[row];
+        const int r = row - (ea[pl] - eb);
+        const int j = r == cl[pl] ? K : r;
         const int64_t gp = pix0 + pl;
         for (int gi = c; gi < ng; gi += nch) {
           const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
@@ -945,12 +996,13 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         }
       }
       for (int mm = 1; mm < nch; mm <<= 1) dz += __shfl_xor(dz, mm);
-      if (live && c == 0) ZZ[pl * KP1 + j] = dz / (float)Sa;  // ZZ now holds dL/dz
+      if (live && c == 0) ZZ[i >> lch] = dz / (float)Sa;  // ZZ now holds dL/dz (entry = row)
       part_q += q;
     }
     if (tail) {
+      __syncthreads();  // 6a has read every a_s: 6b overwrites them in place
       PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
-        const int s = k, m = K - CP[pl];
+        const int s = k, m = K - cpv[pl];
         const float as = AS[pl * Sa + s];
         float t = 0.f;
         if (m > 0 && as != 0.f) {
@@ -959,27 +1011,26 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
           t = (as * s1) * inv_gamma;
           part_q += as * s2;
         }
-        TD[pl * Sa + s] = t;
+        AS[pl * Sa + s] = t;
       }
     }
   }
   __syncthreads();
   PR_BSTAMP(3);
 
-  // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps
+  // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps; with the tail
+  //          draw the masked slots' sum is sum_s AS[s] / Sa
   {
     const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
     const bool act = pl < npix;
-    // with the tail draw B6 wrote the valid slots' rows only; the masked slots' sum is
-    // sum_s TD[s] / Sa
-    const int ns = act ? (tail ? CP[pl] : K) : 0, cks = (ns + g.lpp - 1) >> g.lsh;
-    const int j0c = l * cks, k1c = min(ns, j0c + cks);
+    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, cks = (c + g.lpp - 1) >> g.lsh;
+    const int j0c = l * cks, k1c = min(c, j0c + cks);
     const int nt = act && tail ? Sa : 0, ckt = (nt + g.lpp - 1) >> g.lsh;
     const int t0 = l * ckt, t1 = min(nt, t0 + ckt);
     float s = 0.f, st = 0.f;
     if (act) {
-      for (int k = j0c; k < k1c; ++k) s += ZZ[pl * KP1 + k];
-      for (int t = t0; t < t1; ++t) st += TD[pl * Sa + t];
+      for (int k = j0c; k < k1c; ++k) s += ZZ[e0 + k];
+      for (int t = t0; t < t1; ++t) st += AS[pl * Sa + t];
     }
     for (int m = 1; m < g.lpp; m <<= 1) {
       s += __shfl_xor(s, m);
@@ -987,55 +1038,37 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     }
     if (act && l == 0) {
       if (tail) s += st / (float)Sa;
-      float dzm = -s - ZZ[pl * KP1 + K];
-      dzm = dzm * (PX[pl * 8 + 0] >= p.eps ? 1.f : 0.f);
-      PX[pl * 8 + 4] = dzm;
+      float dzm = -s - ZZ[e0 + c];
+      dzm = dzm * (PX[pl * 12 + 0] >= p.eps ? 1.f : 0.f);
+      PX[pl * 12 + 4] = dzm;
     }
   }
   __syncthreads();
   PR_BSTAMP(4);
 
-  // ---- B8: per-slot gradients (kU slots per thread, mask and upstream gradient loads batched);
-  //          with valid-prefix counts the valid slots here, the masked ones in B8m
-  int cpl = tid / K, ck = tid - (tid / K) * K, spl = 0;
-  const int nit8 = pcnt ? V[npix] : npix * K;
-  for (int i0 = tid; i0 < nit8; i0 += kU * kThreads) {
-    Batch bt;
-    if (pcnt) scan_batch(bt, spl, i0, nit8, V, 0);
-    else batch_next(bt, cpl, ck, i0, K, g.qK, g.rK, nit8);
-    int64_t fk[kU];
-    bool mk[kU];
-    float4 gik[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      fk[u] = -1;
-      mk[u] = false;
-      gik[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!bt.ok[u]) continue;
-      const int64_t gp = pix0 + bt.pl[u], gs = gp * K + bt.k[u];
-      if (pcnt) {  // the face id is read below, for the (few) slots that won a sample
-        mk[u] = bt.k[u] < CP[bt.pl[u]];
-      } else if (a.pix_to_face) {
-        fk[u] = a.pix_to_face[gs];
-        mk[u] = fk[u] >= 0;
-      } else {
-        mk[u] = a.mask[gs] != 0;
-      }
-      if constexpr (CM != 0) gik[u] = reinterpret_cast<const float4*>(a.grad_image)[gp];
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-    if (!bt.ok[u]) continue;
-    const int pl = bt.pl[u], k = bt.k[u];
+  // ---- B8: per-slot gradients of the slot entries (LDS records and the pixel's g_image in
+  //          LDS: one entry per iteration); with compacted entries the masked slots in B8m
+  for (int li = tid; li < nent; li += kThreads) {
+    const int pl = OWN[li], k = li - (ea[pl] - eb);
+    if (k >= cl[pl]) continue;  // the background entry
     const int64_t gp = pix0 + pl, gs = gp * K + k;
-    const bool m = mk[u];
+    int64_t fk = -1;
+    bool m;
+    if (pcnt) {  // the face id is read below, for the (few) slots that won a sample
+      m = k < cpv[pl];
+    } else if (a.pix_to_face) {
+      fk = a.pix_to_face[gs];
+      m = fk >= 0;
+    } else {
+      m = a.mask[gs] != 0;
+    }
     const float mf = m ? 1.f : 0.f;
-    const float dzk = ZZ[pl * KP1 + k];
-    const float dzinv = dzk + (k == (int)PX[pl * 8 + 2] ? PX[pl * 8 + 4] : 0.f);
+    const float dzk = ZZ[li];
+    const float dzinv = dzk + (k == (int)PX[pl * 12 + 2] ? PX[pl * 12 + 4] : 0.f);
     const int n = image_of(n0, rem0, pl, g.HW);
     // gradient only: hardware reciprocal of (zfar - znear) instead of an IEEE division
     a.grad_zbuf[gs] = -((dzinv * mf) * __builtin_amdgcn_rcpf(p.zfar[n] - p.znear[n]));
-    const float prob = PR[pl * KP1 + k];
+    const float prob = PR[li];
     // L and 1/prob feed only gradients (tolerance, not winners): hardware log2 / rcp
     // (prob = count / Sr: never denormal; log2(1) = 0 and rcp(0) = inf exactly)
     const float L = __builtin_amdgcn_logf(prob) * 0.693147180559945f;
@@ -1046,26 +1079,27 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     float r = __builtin_amdgcn_rcpf(prob);
     if (__builtin_isinf(r)) r = 0.f;
     float dprob = r * dL;
-    const float4 gi = gik[u];
-    if constexpr (CM != 0) dprob = -((-gi.w) * EX[pl * KP1 + k]) + dprob;
+    float4 gi = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (CM != 0) gi = *reinterpret_cast<const float4*>(PX + pl * 12 + 8);
+    if constexpr (CM != 0) dprob = -((-gi.w) * EX[li]) + dprob;
     if constexpr (RAST) {
-      const float dD = GM[pl * KP1 + k] * (dprob * mf);
+      const float dD = GM[li] * (dprob * mf);
       a.grad_dists[gs] = -dD;
       part_sigma += dD;
     } else {
       a.grad_prob[gs] = dprob;
     }
     if constexpr (CM == 1) {
-      const float w = (float)CN[pl * KP1 + k] / (float)Sa;
+      const float w = (float)CN[li] / (float)Sa;
       float* dc = a.grad_colors + gs * 3;
       dc[0] = w * gi.x;
       dc[1] = w * gi.y;
       dc[2] = w * gi.z;
     } else if constexpr (CM == 2) {
       // d colour = w * g_rgb, pushed through the interpolation (interp_bwd_kernel's order)
-      const int cnt = CN[pl * KP1 + k];
+      const int cnt = CN[li];
       float gb[3] = {0.f, 0.f, 0.f};
-      const int64_t f = (cnt != 0 && m) ? (pcnt ? a.pix_to_face[gs] : fk[u]) : -1;
+      const int64_t f = (cnt != 0 && m) ? (pcnt ? a.pix_to_face[gs] : fk) : -1;
       if (f >= 0) {
         const float w = (float)cnt / (float)Sa;
         const float dc[3] = {w * gi.x, w * gi.y, w * gi.z};
@@ -1084,37 +1118,34 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
       a.grad_bary[gs * 3 + 1] = gb[1];
       a.grad_bary[gs * 3 + 2] = gb[2];
     }
-    }
   }
 
-  // ---- B8m: masked slots (valid-prefix counts): constant gradients, no LDS entry read.
+  // ---- B8m: slots past the compacted entries: constant gradients, no LDS record read.
   //           d zbuf, d dists and d colour are 0 (mask factor 0, no wins); without dists
   //           d prob keeps the alpha term g_alpha * prod_j (1 - prob_j) (its dL term is 0:
-  //           prob = 0 there).  Masked item i of the block: pixel pl with
-  //           pl*K - V[pl] <= i < (pl+1)*K - V[pl+1], slot CP[pl] + i - (pl*K - V[pl]).
-  if (pcnt) {
-    const int nm = npix * K - V[npix];
-    int mpl = 0;
-    for (int i = tid; i < nm; i += kThreads) {
-      while ((mpl + 1) * K - V[mpl + 1] <= i) ++mpl;
-      const int k = CP[mpl] + (i - (mpl * K - V[mpl]));
-      const int64_t gp = pix0 + mpl, gs = gp * K + k;
-      a.grad_zbuf[gs] = 0.f;
-      if constexpr (RAST) {
-        a.grad_dists[gs] = 0.f;
-      } else {
-        float dprob = 0.f;
-        if constexpr (CM != 0) dprob = a.grad_image[gp * 4 + 3] * PX[mpl * 8 + 5];
-        a.grad_prob[gs] = dprob;
-      }
-      if constexpr (CM == 1) {
-        float* dc = a.grad_colors + gs * 3;
-        dc[0] = dc[1] = dc[2] = 0.f;
-      } else if constexpr (CM == 2) {
-        a.grad_bary[gs * 3] = a.grad_bary[gs * 3 + 1] = a.grad_bary[gs * 3 + 2] = 0.f;
+  //           prob = 0 there).  One wave per pixel: its lanes store consecutive slots.
+  if (tail) {
+    const int lane = tid & 63;
+    for (int mpl = tid >> 6; mpl < npix; mpl += kThreads / 64) {
+      const int64_t gp = pix0 + mpl;
+      float dprob = 0.f;
+      if constexpr (!RAST && CM != 0) dprob = PX[mpl * 12 + 11] * PX[mpl * 12 + 5];
+      for (int k = cl[mpl] + lane; k < K; k += 64) {
+        const int64_t gs = gp * K + k;
+        a.grad_zbuf[gs] = 0.f;
+        if constexpr (RAST) a.grad_dists[gs] = 0.f;
+        else a.grad_prob[gs] = dprob;
+        if constexpr (CM == 1) {
+          float* dc = a.grad_colors + gs * 3;
+          dc[0] = dc[1] = dc[2] = 0.f;
+        } else if constexpr (CM == 2) {
+          a.grad_bary[gs * 3] = a.grad_bary[gs * 3 + 1] = a.grad_bary[gs * 3 + 2] = 0.f;
+        }
       }
     }
   }
+  __syncthreads();  // the next pass reuses every LDS record
+  }  // passes
 
   // ---- block reduction of the scalar partials (fixed order -> deterministic)
 #pragma unroll
@@ -1124,8 +1155,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     part_a += __shfl_xor(part_a, m);
     part_gal += __shfl_xor(part_gal, m);
   }
-  __syncthreads();
-  float* RED = smem;  // all per-slot arrays are dead now
+  float* RED = smem;  // all per-entry arrays are dead now
   if ((tid & 63) == 0) {
     RED[(tid >> 6) * 4 + 0] = part_sigma;
     RED[(tid >> 6) * 4 + 1] = part_q;
@@ -1280,30 +1310,38 @@ __global__ void __launch_bounds__(kThreads) philox_kernel(const uint4* ctr, cons
 // ================================================================== host side
 // A, B, PX, CP, queue length (+pad), then the uint16 rast queue [PB*K] (which also holds the
 // uint8 candidate lists [PB][KP1]: 2K >= K+1)
-size_t fwd_lds(int PB, int KP1) {
-  return (size_t)(2 * PB * KP1 + 6 * PB + 5) * sizeof(float) + (size_t)PB * (KP1 - 1) * sizeof(uint16_t);
+// Workgroup shape: PB pixels (<= 32: the entry scan runs in one wave) and CAP entry records
+// in LDS.  CAP is as large as an LDS target allows (kept small enough for ~8 workgroups per
+// CU), clamped to [K + 1, PB * (K + 1)]: a block whose pixels hold more entries takes several
+// passes.  Forward record: prob, z_inv / logit, queue and candidate bytes; backward record:
+// 6 words, plus a_s per (pixel, sample).  The backward uses 16-pixel blocks on small frames
+// (fewer than 4096 blocks of 32: cfg2 measured 0.093 vs 0.109 ms).
+struct Shape {
+  int PB, cap;
+};
+size_t fwd_lds(int PB, int cap) {
+  return (size_t)(2 * cap + 8 * PB + 7) * sizeof(float) + (size_t)cap * (sizeof(uint16_t) + 1);
 }
-size_t bwd_lds(int PB, int KP1, int Sa) {
-  const size_t b = (size_t)(6 * PB * KP1 + PB * Sa + (Sa > KP1 ? PB * Sa : 0) + 11 * PB + 3) * sizeof(float);
-  return b < 16 * sizeof(float) ? 16 * sizeof(float) : b;
+size_t bwd_lds(int PB, int cap, int Sa) {
+  return (size_t)(6 * cap + PB * Sa + 16 * PB + 3) * sizeof(float) + (size_t)cap;
 }
-constexpr size_t kLdsBudget = 48 * 1024;  // forward: >= 3 workgroups (12 waves) per CU
-constexpr size_t kLdsBudgetBwd = 32 * 1024;  // backward: PB=16 at K=50 -> 7 workgroups per CU (measured best)
+constexpr size_t kLdsTargetFwd = 20 * 1024, kLdsTargetBwd = 24 * 1024, kLdsMax = 60 * 1024;
 
-// PR_BLEND_LDS_KB_FWD / _BWD override the per-workgroup LDS budget (tuning sweeps)
-size_t lds_budget(bool bwd) {
+// PR_BLEND_LDS_KB_FWD / _BWD (LDS target) and PR_BLEND_PB_FWD / _BWD (pixels) for sweeps
+Shape pick_shape(int KP1, int Sa, int64_t P, bool bwd) {
   const char* e = getenv(bwd ? "PR_BLEND_LDS_KB_BWD" : "PR_BLEND_LDS_KB_FWD");
-  const long v = e ? atol(e) : 0;
-  return v > 0 ? (size_t)v * 1024 : (bwd ? kLdsBudgetBwd : kLdsBudget);
-}
-
-int pick_pb(int KP1, int Sa, bool bwd) {
-  const size_t budget = lds_budget(bwd);
-  for (int PB = 32; PB >= 1; PB >>= 1) {
-    const size_t b = bwd ? bwd_lds(PB, KP1, Sa) : fwd_lds(PB, KP1);
-    if (b <= budget || PB == 1) return PB;
+  const size_t target = e && atoi(e) > 0 ? (size_t)atoi(e) * 1024 : (bwd ? kLdsTargetBwd : kLdsTargetFwd);
+  const char* b0 = getenv(bwd ? "PR_BLEND_PB_BWD" : "PR_BLEND_PB_FWD");
+  int PB = b0 ? atoi(b0) : (bwd && P < 4096 * 32 ? 16 : 32);
+  if (PB != 1 && PB != 2 && PB != 4 && PB != 8 && PB != 16) PB = 32;
+  for (;; PB >>= 1) {
+    const size_t fixed = bwd ? bwd_lds(PB, 0, Sa) : fwd_lds(PB, 0);
+    const size_t per = bwd ? 6 * sizeof(float) + 1 : 2 * sizeof(float) + 3;
+    const int fit = target > fixed ? (int)((target - fixed) / per) : 0;
+    const int cap = max(KP1, min(PB * KP1, fit));
+    const size_t lds = bwd ? bwd_lds(PB, cap, Sa) : fwd_lds(PB, cap);
+    if (lds <= kLdsMax || PB == 1) return Shape{PB, cap};
   }
-  return 1;
 }
 
 int check_params(const PRBlendParams& p, bool need_rast) {
@@ -1329,28 +1367,28 @@ int color_mode(int flags) {
   return !(flags & PR_BLEND_COLOR) ? 0 : ((flags & PR_BLEND_VERTEX) ? 2 : 1);
 }
 
-template <int NOISE>
+template <int NOISE, bool MULTI>
 void launch_fwd(const PRBlendFwdArgs& a, Geo geo, int NC, hipStream_t st, size_t lds, int nblk) {
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
-  if (rast && cm == 2) blend_fwd_kernel<NOISE, true, 2><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (rast && cm == 1) blend_fwd_kernel<NOISE, true, 1><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (rast) blend_fwd_kernel<NOISE, true, 0><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (cm == 1) blend_fwd_kernel<NOISE, false, 1><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (cm == 2) blend_fwd_kernel<NOISE, false, 2><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else blend_fwd_kernel<NOISE, false, 0><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  if (rast && cm == 2) blend_fwd_kernel<NOISE, true, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (rast && cm == 1) blend_fwd_kernel<NOISE, true, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (rast) blend_fwd_kernel<NOISE, true, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (cm == 1) blend_fwd_kernel<NOISE, false, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else if (cm == 2) blend_fwd_kernel<NOISE, false, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  else blend_fwd_kernel<NOISE, false, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
 }
 
-template <int NOISE>
+template <int NOISE, bool MULTI>
 void launch_bwd(const PRBlendBwdArgs& a, Geo geo, hipStream_t st, size_t lds, int nblk, float* part) {
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
-  if (rast && cm == 2) blend_bwd_kernel<NOISE, true, 2><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (rast && cm == 1) blend_bwd_kernel<NOISE, true, 1><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (rast) blend_bwd_kernel<NOISE, true, 0><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (cm == 1) blend_bwd_kernel<NOISE, false, 1><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (cm == 2) blend_bwd_kernel<NOISE, false, 2><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else blend_bwd_kernel<NOISE, false, 0><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  if (rast && cm == 2) blend_bwd_kernel<NOISE, true, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (rast && cm == 1) blend_bwd_kernel<NOISE, true, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (rast) blend_bwd_kernel<NOISE, true, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (cm == 1) blend_bwd_kernel<NOISE, false, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else if (cm == 2) blend_bwd_kernel<NOISE, false, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  else blend_bwd_kernel<NOISE, false, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
 }
 
 Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
@@ -1386,7 +1424,7 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
 }
 
 int64_t bwd_blocks(const PRBlendParams& p) {
-  const int PB = pick_pb(p.K + 1, p.Sa, true);
+  const int PB = pick_shape(p.K + 1, p.Sa, (int64_t)p.N * p.H * p.W, true).PB;
   const int64_t P = (int64_t)p.N * p.H * p.W;
   return (P + PB - 1) / PB;
 }
@@ -1416,17 +1454,25 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
       (cm == 2 && (!a.image || !a.bary || !a.faces || !a.vert_colors || !a.pix_to_face)))
     return set_error(PR_ERR_ARG, "blend_fwd: missing buffer");
   const int KP1 = a.p.K + 1;
-  const int PB = pick_pb(KP1, a.p.Sa, false);
-  const Geo geo = make_geo(a.p, PB, false);
+  const Shape sh = pick_shape(KP1, a.p.Sa, (int64_t)a.p.N * a.p.H * a.p.W, false);
+  const int PB = sh.PB;
+  Geo geo = make_geo(a.p, PB, false);
+  geo.cap = sh.cap;
   // slot chunks per (pixel, sample group) so that ~256 threads share the MC loop
   const int ng = ((a.p.sample_offset_a + a.p.Sa - 1) >> 2) - (a.p.sample_offset_a >> 2) + 1;
   int NC = 1;
   while (NC < 64 && PB * ng * NC * 2 <= kThreads && (KP1 + NC * 2 - 1) / (NC * 2) >= 4) NC <<= 1;
   const int64_t nblk = (geo.P + PB - 1) / PB;
-  const size_t lds = fwd_lds(PB, KP1);
+  const size_t lds = fwd_lds(PB, sh.cap);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (a.p.noise_mode == PR_NOISE_INJECTED) launch_fwd<PR_NOISE_INJECTED>(a, geo, NC, st, lds, (int)nblk);
-  else launch_fwd<PR_NOISE_PHILOX>(a, geo, NC, st, lds, (int)nblk);
+  const bool multi = sh.cap < PB * KP1;
+  if (a.p.noise_mode == PR_NOISE_INJECTED) {
+    if (multi) launch_fwd<PR_NOISE_INJECTED, true>(a, geo, NC, st, lds, (int)nblk);
+    else launch_fwd<PR_NOISE_INJECTED, false>(a, geo, NC, st, lds, (int)nblk);
+  } else {
+    if (multi) launch_fwd<PR_NOISE_PHILOX, true>(a, geo, NC, st, lds, (int)nblk);
+    else launch_fwd<PR_NOISE_PHILOX, false>(a, geo, NC, st, lds, (int)nblk);
+  }
   return check_launch("blend_fwd");
 }
 
@@ -1453,14 +1499,22 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
   const size_t need = pr_blend_bwd_workspace_size(args);
   if (!a.workspace || a.workspace_bytes < need) return set_error(PR_ERR_WORKSPACE, "blend_bwd: workspace too small");
   const int KP1 = a.p.K + 1;
-  const int PB = pick_pb(KP1, a.p.Sa, true);
-  const Geo geo = make_geo(a.p, PB, true);
+  const Shape sh = pick_shape(KP1, a.p.Sa, (int64_t)a.p.N * a.p.H * a.p.W, true);
+  const int PB = sh.PB;
+  Geo geo = make_geo(a.p, PB, true);
+  geo.cap = sh.cap;
   const int64_t nblk = (geo.P + PB - 1) / PB;
-  const size_t lds = bwd_lds(PB, KP1, a.p.Sa);
+  const size_t lds = bwd_lds(PB, sh.cap, a.p.Sa);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* part = reinterpret_cast<float*>(a.workspace);
-  if (a.p.noise_mode == PR_NOISE_INJECTED) launch_bwd<PR_NOISE_INJECTED>(a, geo, st, lds, (int)nblk, part);
-  else launch_bwd<PR_NOISE_PHILOX>(a, geo, st, lds, (int)nblk, part);
+  const bool multi = sh.cap < PB * KP1;
+  if (a.p.noise_mode == PR_NOISE_INJECTED) {
+    if (multi) launch_bwd<PR_NOISE_INJECTED, true>(a, geo, st, lds, (int)nblk, part);
+    else launch_bwd<PR_NOISE_INJECTED, false>(a, geo, st, lds, (int)nblk, part);
+  } else {
+    if (multi) launch_bwd<PR_NOISE_PHILOX, true>(a, geo, st, lds, (int)nblk, part);
+    else launch_bwd<PR_NOISE_PHILOX, false>(a, geo, st, lds, (int)nblk, part);
+  }
   if (int e = check_launch("blend_bwd")) return e;
   blend_finalize_kernel<<<1, kThreads, 0, st>>>(part, (int)nblk, a.p, rast ? 1 : 0, a.grad_scalars);
   return check_launch("blend_finalize");

@@ -1,9 +1,11 @@
-# bench sweeps over tuning env vars on a batch configuration:
-#   bash tools/gpu_sweep_cfg.sh cfg3 "PR_BLEND_LPP=16" ...
+# bench sweeps over tuning env vars at one config (no profiler):
+#   CONFIG=cfg4 bash tools/gpu_sweep_cfg.sh "PR_BLEND_LDS_KB_FWD=24" "PR_BLEND_LDS_KB_FWD=48" ...
 set -u
-R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out"; mkdir -p "$OUT"; CFG="$1"; shift
+R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out"; mkdir -p "$OUT"
 cd "$R"
-for cfg in "$@"; do
-  env $cfg timeout -k 10 300 python bench.py --config "$CFG" --no-cpu-baseline --no-dense --steps 10 --warmup 3 > "$OUT/swc.json" 2> "$OUT/swc.err" || { echo "FAIL $cfg"; tail -3 "$OUT/swc.err"; exit 1; }
-  python -c "import json;d=json.load(open('$OUT/swc.json'));print('$CFG $cfg', d['ms_per_step'], {k:v['ms'] for k,v in d['kernels'].items()})"
-done
+C="${CONFIG:-cfg2}"
+run() {
+  env "$@" timeout -k 10 200 python bench.py --config $C --no-cpu-baseline --no-dense --steps 20 --warmup 5 > "$OUT/sw.json" 2> "$OUT/sw.err" || { echo "FAIL $*"; tail -3 "$OUT/sw.err"; return 1; }
+  python -c "import json;d=json.load(open('$OUT/sw.json'));print('$C $*', d['value'], d['ms_per_step'], {k:v['ms'] for k,v in d['kernels'].items()})"
+}
+for cfg in "$@"; do run $cfg || exit 1; done
