@@ -34,20 +34,21 @@ constexpr float kNegInf = -__builtin_inff();
 constexpr float kEpsMaxBM = 5.8f;               // > sqrt(-2 ln 2^-24) = 5.7683
 
 #ifdef PR_BLEND_PROFILE
-// diagnostic build: per block [start, end (100 MHz), phases (shader clock) x6, hw id]; fwd
-// blocks at [0, 1<<16), bwd blocks at [1<<16, 2<<16)
+// diagnostic build: per block [start, end (100 MHz), phases (shader clock) x8, hw id, flag];
+// fwd blocks at [0, 1<<16), bwd blocks at [1<<16, 2<<16)
 constexpr unsigned kBProfBlocks = 1 << 16;
-__device__ long long g_blend_prof[2 * kBProfBlocks * 10];
-#define PR_BPROF_DECL long long bst_[6] = {0, 0, 0, 0, 0, 0}, bt_ = __builtin_amdgcn_s_memtime(), \
+constexpr int kBProfRec = 12;
+__device__ long long g_blend_prof[2 * kBProfBlocks * kBProfRec];
+#define PR_BPROF_DECL long long bst_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bt_ = __builtin_amdgcn_s_memtime(), \
                       brt_ = __builtin_amdgcn_s_memrealtime()
 #define PR_BPROF_DUMP(which)                                                                   \
   if (threadIdx.x == 0 && blockIdx.x < kBProfBlocks) {                                         \
     unsigned hw_;                                                                              \
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                          \
-    long long* r_ = g_blend_prof + ((size_t)(which) * kBProfBlocks + blockIdx.x) * 10;         \
+    long long* r_ = g_blend_prof + ((size_t)(which) * kBProfBlocks + blockIdx.x) * kBProfRec;  \
     r_[0] = brt_; r_[1] = (long long)__builtin_amdgcn_s_memrealtime();                          \
-    for (int i_ = 0; i_ < 6; ++i_) r_[2 + i_] = bst_[i_];                                       \
-    r_[8] = hw_; r_[9] = 1;                                                                    \
+    for (int i_ = 0; i_ < 8; ++i_) r_[2 + i_] = bst_[i_];                                       \
+    r_[10] = hw_; r_[11] = 1;                                                                  \
   }
 #define PR_BSTAMP(i) (bst_[i] += __builtin_amdgcn_s_memtime() - bt_, bt_ = __builtin_amdgcn_s_memtime())
 #else
@@ -446,6 +447,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   if (tid == 0) *QN = 0;
   fill_owner(OWN, ea, eb, cl, npix, g.lsh, g.lpp);
   __syncthreads();
+  PR_BSTAMP(0);
 
   // ---- 1a: slot entries, kU per thread in flight: mask, z_inv, and the probability
   //          wherever it needs no noise (masked, or saturated Gaussian); the rest is queued
@@ -509,6 +511,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     }
   }
   __syncthreads();
+  PR_BSTAMP(1);
 
   // ---- 1b: queued slots (valid, unsaturated): Monte-Carlo rasterization, all lanes busy
   if constexpr (RAST) {
@@ -530,7 +533,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     }
     __syncthreads();
   }
-  PR_BSTAMP(0);
+  PR_BSTAMP(2);
 
   // ---- 2: per pixel (lpp lanes): alpha, z_max, logits, largest logit, and the list of
   //         argmax candidates (ascending j).  A pixel's entries are its cl slot entries,
@@ -593,7 +596,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     }
   }
   __syncthreads();
-  PR_BSTAMP(1);
+  PR_BSTAMP(3);
 
   // ---- 3: Monte-Carlo argmax: thread = (pixel, 4-sample group, candidate stripe c::NC)
   {
@@ -646,7 +649,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     }
   }
   __syncthreads();
-  PR_BSTAMP(2);
+  PR_BSTAMP(4);
 
   // ---- 4: outputs
   const float fSa = (float)p.Sa;
@@ -689,9 +692,9 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     }
   }
   __syncthreads();  // the next pass reuses every LDS record
+  PR_BSTAMP(5);
   }  // passes
 #ifdef PR_BLEND_PROFILE
-  PR_BSTAMP(3);
   PR_BPROF_DUMP(0);
 #endif
 }
@@ -700,8 +703,9 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
 // Same entry layout and passes as the forward.  Entries are compacted (a pixel's valid
 // slots + background) when the masked tail is drawn jointly (B6); otherwise every slot
 // keeps its entry, since injected / Cauchy noise needs each masked slot's own d z.
+// (MULTI: at least 6 waves per SIMD, the occupancy its 24 KB of LDS allows anyway)
 template <int NOISE, bool RAST, int CM, bool MULTI>
-__global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
+__global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
   const Sc sc = resolve(p);
@@ -720,6 +724,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   int* EA = CP + PB;                   // [PB+1] exclusive prefix of entries (CL + 1)
   int* PS = EA + PB + 1;               // [PB+2] pass starts; [PB+1] = pass count
   uint8_t* OWN = reinterpret_cast<uint8_t*>(PS + PB + 2);  // [CAP] pixel of each entry
+  uint8_t* WN = OWN + CAP;             // [PB][Sa] the forward's winners of the pass
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
   const int64_t blk = pixel_block(g), bpix0 = blk * PB;
@@ -746,6 +751,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   fill_owner(OWN, ea, eb, cl, npix, g.lsh, g.lpp, CN);
   __syncthreads();
+  PR_BSTAMP(0);
 
   // ---- B1: entries (slots + background): prob, z_inv, rast score, dL/dW (kU items per
   //          thread with their global loads in flight together)
@@ -839,14 +845,26 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
         }
       }
     }
-    // win counts of the forward's winners (CN zeroed with the owner map)
-    PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
-      const int jw = a.winners[(pix0 + pl) * Sa + k];
-      atomicAdd(&CN[ea[pl] - eb + (jw == K ? cl[pl] : jw)], 1);
+    // the pass's winners (one contiguous byte range) into LDS for B5, with their win counts
+    // (CN zeroed with the owner map); kU loads in flight per thread
+    const uint8_t* wsrc = a.winners + pix0 * Sa;
+    const int nw = npix * Sa;
+    for (int i0 = tid; i0 < nw; i0 += kU * kThreads) {
+      int w[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) w[u] = i0 + u * kThreads < nw ? wsrc[i0 + u * kThreads] : 0;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + u * kThreads;
+        if (i >= nw) continue;
+        WN[i] = (uint8_t)w[u];
+        const int pl = i / Sa;  // (Sa: runtime divisor, once per winner)
+        atomicAdd(&CN[ea[pl] - eb + (w[u] == K ? cl[pl] : w[u])], 1);
+      }
     }
   }
   __syncthreads();
-  PR_BSTAMP(0);
+  PR_BSTAMP(1);
 
   // ---- B2: per pixel (lpp lanes, contiguous chunks of its entries: the cl slot entries,
   //          then the background as entry cl -> j = K): z_max + first argmax, exclusive
@@ -930,14 +948,14 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     }
   }
   __syncthreads();
-  PR_BSTAMP(1);
+  PR_BSTAMP(2);
 
   // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0] (win counts: B1, CM 2's dW: B2)
   PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
     const int s = k;
     const int64_t gp = pix0 + pl;
     const int e0 = ea[pl] - eb, c = cl[pl];
-    const int jw = a.winners[gp * Sa + s];
+    const int jw = WN[pl * Sa + s];
     const int j0 = (int)PX[pl * 12 + 3];
     const int ew = e0 + (jw == K ? c : jw), e0j = e0 + (j0 == K ? c : j0);
     // GaussianAgg_wovr: a_s = <g, w_s> (smoothagg.py:118); else <g, w_s - vr'>
@@ -947,7 +965,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     part_a += as;
   }
   __syncthreads();
-  PR_BSTAMP(2);
+  PR_BSTAMP(3);
 
   // ---- B6: dz_j = mean_s(a_s * score(eps_sj) / gamma) and sum_s a_s * eps_sj * score(eps_sj)
   //          (d gamma; score = eps for Gaussian noise, 2 eps / (1 + eps^2) for Cauchy)
@@ -1016,7 +1034,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     }
   }
   __syncthreads();
-  PR_BSTAMP(3);
+  PR_BSTAMP(4);
 
   // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps; with the tail
   //          draw the masked slots' sum is sum_s AS[s] / Sa
@@ -1044,7 +1062,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     }
   }
   __syncthreads();
-  PR_BSTAMP(4);
+  PR_BSTAMP(5);
 
   // ---- B8: per-slot gradients of the slot entries (LDS records and the pixel's g_image in
   //          LDS: one entry per iteration); with compacted entries the masked slots in B8m
@@ -1145,6 +1163,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     }
   }
   __syncthreads();  // the next pass reuses every LDS record
+  PR_BSTAMP(6);
   }  // passes
 
   // ---- block reduction of the scalar partials (fixed order -> deterministic)
@@ -1167,7 +1186,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_BWD_WPE) blend_bwd_kernel(P
     partials[blk * 4 + tid] = (RED[tid] + RED[4 + tid]) + (RED[8 + tid] + RED[12 + tid]);
   }
 #ifdef PR_BLEND_PROFILE
-  PR_BSTAMP(5);
+  PR_BSTAMP(7);
   PR_BPROF_DUMP(1);
 #endif
 }
@@ -1323,7 +1342,7 @@ size_t fwd_lds(int PB, int cap) {
   return (size_t)(2 * cap + 8 * PB + 7) * sizeof(float) + (size_t)cap * (sizeof(uint16_t) + 1);
 }
 size_t bwd_lds(int PB, int cap, int Sa) {
-  return (size_t)(6 * cap + PB * Sa + 16 * PB + 3) * sizeof(float) + (size_t)cap;
+  return (size_t)(6 * cap + PB * Sa + 16 * PB + 3) * sizeof(float) + (size_t)cap + (size_t)PB * Sa;
 }
 constexpr size_t kLdsTargetFwd = 20 * 1024, kLdsTargetBwd = 24 * 1024, kLdsMax = 60 * 1024;
 

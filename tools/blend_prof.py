@@ -2,7 +2,8 @@
 -DPR_BLEND_PROFILE variant:
     python -m pertrenderer_amd.build_native --out pertrenderer_amd/libpertrender_prof.so -D PR_BLEND_PROFILE
     PR_NATIVE_LIB=pertrenderer_amd/libpertrender_prof.so python tools/blend_prof.py
-Forward phases: slots+MC rast / pixel / MC argmax / output.  Backward: B1 / B2 / B5 / B6 / B7 / B8."""
+Forward phases: setup / slots / MC rast / pixel / MC argmax / output.  Backward: setup / B1 / B2 /
+B5 / B6 / B7 / B8 / reduction.  Phases are summed over a block's passes."""
 import ctypes
 import os
 import sys
@@ -26,12 +27,13 @@ for _ in range(3):
     torch.cuda.synchronize()
 lib = nat.load()
 NB = 1 << 16
-buf = np.zeros(2 * NB * 10, dtype=np.int64)
+REC = 12
+buf = np.zeros(2 * NB * REC, dtype=np.int64)
 assert lib.pr_blend_prof_dump(ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(buf.nbytes)) == 0
-rec = buf.reshape(2, NB, 10)
-for w, name, ph in ((0, "blend_fwd", ["slots+rast", "pixel", "argmax", "out"]),
-                    (1, "blend_bwd", ["B1", "B2", "B5", "B6", "B7", "B8"])):
-    r = rec[w][rec[w][:, 9] == 1]
+rec = buf.reshape(2, NB, REC)
+for w, name, ph in ((0, "blend_fwd", ["setup", "slots", "rast", "pixel", "argmax", "out"]),
+                    (1, "blend_bwd", ["setup", "B1", "B2", "B5", "B6", "B7", "B8", "red"])):
+    r = rec[w][rec[w][:, REC - 1] == 1]
     t0 = r[:, 0].min()
     st, en = (r[:, 0] - t0) / 100.0, (r[:, 1] - t0) / 100.0
     print(f"{name}: blocks {len(r)} span {en.max():.1f} us, last start {st.max():.1f}, dur mean {(en - st).mean():.1f} "
