@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 10
+#define PR_ABI_VERSION 11
 
 /* error codes */
 #define PR_OK 0
@@ -68,6 +68,10 @@ extern "C" {
  * "softras" renderer): P = sigmoid(-d / sigma), W = softmax(z / gamma); with RAST | COLOR and
  * texel colours; Sr / Sa / noise fields are ignored, winners / rast_cache are not written */
 #define PR_BLEND_SOFT 128
+/* UniformAgg: U(-1/2, 1/2) agg noise (smoothagg.py:28-30, 252-271); forward only -- the
+ * reference's backward has no uniform branch and fails (smoothagg.py:64-70), so
+ * pr_blend_bwd rejects the flag with PR_ERR_ARG */
+#define PR_BLEND_AGG_UNIFORM 256
 
 typedef struct PRBlendParams {
   int32_t N, H, W, K;        /* fragment shape */

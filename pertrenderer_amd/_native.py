@@ -20,6 +20,7 @@ PR_BLEND_COLOR = 2
 PR_BLEND_VERTEX = 4
 PR_BLEND_RAST_CAUCHY = 8
 PR_BLEND_AGG_CAUCHY = 16
+PR_BLEND_AGG_UNIFORM = 256
 PR_BLEND_RAST_WOVR = 32
 PR_BLEND_AGG_WOVR = 64
 PR_BLEND_SOFT = 128
@@ -143,7 +144,7 @@ EXPORTS = {
     "pr_shade_fwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
     "pr_shade_bwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
 }
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lib = None
 

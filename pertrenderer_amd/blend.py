@@ -60,7 +60,7 @@ def _scalars(vals, device):
     return tuple(float(v.detach().cpu()) if torch.is_tensor(v) else float(v) for v in vals), None
 
 
-KINDS = ("gaussian", "cauchy")
+KINDS = ("gaussian", "cauchy", "uniform")  # uniform: UniformAgg's forward only
 
 
 def variant_flags(rast_kind="gaussian", rast_vr=True, agg_kind="gaussian", agg_vr=True):
@@ -68,10 +68,13 @@ def variant_flags(rast_kind="gaussian", rast_vr=True, agg_kind="gaussian", agg_v
     GaussianAgg_wovr."""
     for k in (rast_kind, agg_kind):
         if k not in KINDS:
-            raise NotImplementedError(f"noise type {k!r} not implemented (gaussian, cauchy)")
+            raise NotImplementedError(f"noise type {k!r} not implemented (gaussian, cauchy, uniform)")
+    if rast_kind == "uniform":
+        raise NotImplementedError("uniform noise exists for the aggregation only (smoothagg.py:28-30)")
     f = 0
     f |= nat.PR_BLEND_RAST_CAUCHY if rast_kind == "cauchy" else 0
     f |= nat.PR_BLEND_AGG_CAUCHY if agg_kind == "cauchy" else 0
+    f |= nat.PR_BLEND_AGG_UNIFORM if agg_kind == "uniform" else 0
     f |= 0 if rast_vr else nat.PR_BLEND_RAST_WOVR
     f |= 0 if agg_vr else nat.PR_BLEND_AGG_WOVR
     return f
@@ -150,6 +153,14 @@ def _timed(name, fn):
 RAST_CACHE = True
 
 
+def _no_uniform_grad(vflags):
+    """The reference's randomArgmax.backward has no uniform branch and fails on it
+    (smoothagg.py:64-70: grad_z stays None): so does every backward here."""
+    if vflags & nat.PR_BLEND_AGG_UNIFORM:
+        raise NotImplementedError("UniformAgg: the reference implements no gradient for uniform noise "
+                                  "(smoothagg.py:64-70)")
+
+
 class _FusedBlendFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, dists, zbuf, colors, sigma, gamma, alpha, p2f, znear, zfar, cfg):
@@ -184,6 +195,7 @@ class _FusedBlendFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gimg):
+        _no_uniform_grad(ctx.cfg.get("vflags", 0))
         p2f_c, d_c, z_c, c_c, zn, zf, winners, cache = ctx.saved_tensors
         sc_dev = ctx.sc_dev
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
@@ -248,6 +260,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gimg):
+        _no_uniform_grad(ctx.cfg.get("vflags", 0))
         p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache = ctx.saved_tensors
         sc_dev = ctx.sc_dev
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
@@ -434,6 +447,7 @@ class _AggregateFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gW):
+        _no_uniform_grad(ctx.cfg["vflags"])
         z_c, p_c, m_c, zn, zf, winners = ctx.saved_tensors
         sc_dev = ctx.sc_dev
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
@@ -459,8 +473,9 @@ class _AggregateFn(torch.autograd.Function):
 
 def perturbed_aggregate(zbuf, zfar, znear, prob_map, mask, gamma, alpha, nb_samples, eps=1e-10,
                         noise=None, fixed_noise=False, kind="gaussian", variance_reduction=True):
-    """GaussianAgg / CauchyAgg (kind="cauchy") / GaussianAgg_wovr (variance_reduction=False)
-    .aggregate(zbuf, zfar, znear, prob_map, mask) -> (N,H,W,K+1) weights (smoothagg.py:196-250)."""
+    """GaussianAgg / CauchyAgg (kind="cauchy") / GaussianAgg_wovr (variance_reduction=False) /
+    UniformAgg (kind="uniform", forward only) .aggregate(zbuf, zfar, znear, prob_map, mask) ->
+    (N,H,W,K+1) weights (smoothagg.py:196-271)."""
     N, H, W, K = zbuf.shape
     vflags = variant_flags(agg_kind=kind, agg_vr=variance_reduction)
     if noise is None:

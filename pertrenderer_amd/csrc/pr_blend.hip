@@ -325,7 +325,13 @@ PR_DEV void agg_noise4(const PRBlendParams& p, const Sc& sc, uint32_t gp, int j,
     }
   } else {
     const U4 u = philox_block(sc.ka, gp, (uint32_t)j, g, kTagAgg);
-    if (p.flags & PR_BLEND_AGG_CAUCHY) cauchy4(u, e); else gauss4(u, e);
+    if (p.flags & PR_BLEND_AGG_CAUCHY) {
+      cauchy4(u, e);
+    } else if (p.flags & PR_BLEND_AGG_UNIFORM) {  // U(-1/2, 1/2): u01 is odd/2^24, never 0 or 1
+      e[0] = u01(u.x) - 0.5f; e[1] = u01(u.y) - 0.5f; e[2] = u01(u.z) - 0.5f; e[3] = u01(u.w) - 0.5f;
+    } else {
+      gauss4(u, e);
+    }
   }
 }
 
@@ -567,8 +573,9 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
     // candidates: finite logits not below zl - skipm (bounded Box-Muller noise only: a
     // logit further below the best can never win); lane chunks are contiguous, so an
     // exclusive scan of the lane counts gives each lane its output offset
-    const float skipm = NOISE == PR_NOISE_PHILOX && !(p.flags & PR_BLEND_AGG_CAUCHY) ? 2.f * kEpsMaxBM * sc.gamma
-                                                                                    : __builtin_inff();
+    // (uniform noise: |eps| < 1/2, so a logit gamma below the best never wins)
+    const float skipm = NOISE != PR_NOISE_PHILOX || (p.flags & PR_BLEND_AGG_CAUCHY) ? __builtin_inff()
+                        : (p.flags & PR_BLEND_AGG_UNIFORM) ? sc.gamma : 2.f * kEpsMaxBM * sc.gamma;
     const float zfloor = zl - skipm;
     int nc = 0;
     if (act)
@@ -1505,6 +1512,8 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "blend_bwd: null args");
   const PRBlendBwdArgs& a = *args;
   if (a.p.flags & PR_BLEND_SOFT) return soft_blend_bwd(a, reinterpret_cast<hipStream_t>(stream));
+  if (a.p.flags & PR_BLEND_AGG_UNIFORM)
+    return set_error(PR_ERR_ARG, "blend_bwd: UniformAgg has no gradient (reference smoothagg.py:64-70)");
   const bool rast = a.p.flags & PR_BLEND_RAST, color = a.p.flags & PR_BLEND_COLOR;
   if (int e = check_params(a.p, rast)) return e;
   if (!a.pix_to_face && !a.mask) return set_error(PR_ERR_ARG, "blend_bwd: need pix_to_face or mask");

@@ -138,10 +138,13 @@ def use_device_seed(ds):
 
 def _torch_draw(kind, shape):
     """The reference's draws on the CPU generator: torch.normal(0, 1) (smoothrast.py:21,
-    smoothagg.py:21) or Cauchy(0, 1) samples clamped to +-1e7 (smoothrast.py:23-24,
-    smoothagg.py:26-27)."""
+    smoothagg.py:21), Cauchy(0, 1) samples clamped to +-1e7 (smoothrast.py:23-24,
+    smoothagg.py:26-27) or Uniform(-1/2, 1/2) samples (smoothagg.py:28-30)."""
     if kind == "gaussian":
         return torch.randn(shape)
+    if kind == "uniform":  # smoothagg.py:28-30
+        m = torch.distributions.uniform.Uniform(torch.tensor([-0.5]), torch.tensor([0.5]))
+        return m.sample(shape).squeeze(-1)
     m = torch.distributions.cauchy.Cauchy(torch.tensor([0.0]), torch.tensor([1.0]))
     return torch.clamp(m.sample(shape).squeeze(-1), min=-1e7, max=1e7)
 

@@ -90,16 +90,16 @@ class CauchyAgg(_PerturbedAgg, SmoothAggBase):
         self.fixed_noise = fixed_noise
 
 
-class UniformAgg(SmoothAggBase):
-    """Uniform-noise argmax: the reference has no backward for it (smoothagg.py:64-65,252-271)."""
+class UniformAgg(_PerturbedAgg, SmoothAggBase):
+    """Uniform-noise perturbed argmax (smoothagg.py:252-271): the native forward with
+    U(-1/2, 1/2) noise; like the reference (smoothagg.py:64-70), the backward raises."""
+
+    noise_kind = "uniform"
+    variance_reduction = True
 
     def __init__(self, nb_samples=16, gamma=4e-2, alpha=1.0, eps=1e-10, fixed_noise=False):
         self.fixed_noise = fixed_noise
         super().__init__(gamma, alpha, eps, nb_samples)
-
-    def aggregate(self, zbuf, zfar, znear, prob_map, mask):
-        raise NotImplementedError("UniformAgg: the reference implements no gradient for uniform noise "
-                                  "(smoothagg.py:64-65)")
 
 
 class HardAgg:

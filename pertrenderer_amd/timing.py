@@ -26,11 +26,15 @@ class KernelTimer:
     """external=True creates events that become record nodes when the launches are
     captured into a HIP graph; after a replay they time that replay's kernels."""
 
-    def __init__(self, external=False, lead_cycles=0):
+    def __init__(self, external=False, lead_cycles=0, warm_bytes=0):
         self._open = {}
         self.events = collections.defaultdict(list)
         self.external = external
         self.lead_cycles = lead_cycles
+        # after the (single-wave) spin the chip is idle and its clocks drop; a short full-chip
+        # elementwise pass right before the start event brings them back before the timed launch
+        self._warm = (torch.empty(warm_bytes // 4, dtype=torch.float32, device="cuda").fill_(1.0)
+                      if warm_bytes else None)
 
     def __enter__(self):
         global _ACTIVE
@@ -45,6 +49,8 @@ class KernelTimer:
     def start(self, name):
         if self.lead_cycles and hasattr(torch.cuda, "_sleep"):
             torch.cuda._sleep(self.lead_cycles)
+        if self._warm is not None:
+            self._warm.mul_(1.0)
         ev = torch.cuda.Event(enable_timing=True, external=self.external)
         ev.record(torch.cuda.current_stream())
         self._open[name] = ev
@@ -58,7 +64,7 @@ class KernelTimer:
         self.events.clear()
 
     def summary(self, stat="mean"):
-        """{name: (launches, ms)} with ms the mean or the median over launches — call after
+        """{name: (launches, ms)} with ms the mean, median or minimum over launches — call after
         torch.cuda.synchronize()."""
         out = {}
         for name, pairs in self.events.items():
@@ -68,6 +74,8 @@ class KernelTimer:
             if stat == "median":
                 m = len(ms) // 2
                 v = ms[m] if len(ms) % 2 else 0.5 * (ms[m - 1] + ms[m])
+            elif stat == "min":
+                v = ms[0]
             else:
                 v = sum(ms) / len(ms)
             out[name] = (len(ms), v)

@@ -17,7 +17,8 @@ For every case it records, into ``tests/golden/<case>.npz``:
 The fixtures are DATA (inputs and expected outputs); no reference source is
 copied into this repository.  Re-run with::
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py            # all cases
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py uniform    # agg_uniform only
 """
 import collections
 import os
@@ -186,6 +187,41 @@ def run_agg_case(name, ref, fr, prob, Sa, gamma, alpha, znear, zfar, seed, eps=1
     print("wrote", name, tuple(Wt.shape))
 
 
+def run_uniform_agg_case(name, ref, fr, prob, Sa, gamma, alpha, znear, zfar, seed, eps=1e-10):
+    """UniformAgg.aggregate forward (smoothagg.py:252-271, noise :28-30); the reference has no
+    backward for it (smoothagg.py:64-70), so only the weights are recorded."""
+    _, _, sa, _ = ref
+    N, H, W, K = fr.zbuf.shape
+    agg = sa.UniformAgg(nb_samples=Sa, gamma=gamma, alpha=alpha, eps=eps)
+    mask = fr.pix_to_face >= 0
+    pr = prob * mask
+    zn = torch.full((N,), znear)[:, None, None, None]
+    zf = torch.full((N,), zfar)[:, None, None, None]
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        Wt = agg.aggregate(fr.zbuf, zf, zn, pr, mask)
+    torch.manual_seed(seed)
+    m = torch.distributions.uniform.Uniform(torch.tensor([-0.5]), torch.tensor([0.5]))
+    ea = m.sample((Sa, N, H, W, K + 1)).squeeze(-1)
+    np.savez_compressed(
+        os.path.join(OUT, name + ".npz"), pix_to_face=fr.pix_to_face.numpy(), zbuf=fr.zbuf.numpy(),
+        prob=pr.numpy(), znear=np.float32(znear), zfar=np.float32(zfar),
+        gamma=np.float32(gamma), alpha=np.float32(alpha), eps=np.float64(eps), Sa=np.int64(Sa),
+        seed=np.int64(seed), noise_a=ea.numpy(), W=Wt.numpy())
+    print("wrote", name, tuple(Wt.shape))
+
+
+def main_uniform():
+    """Only the UniformAgg case (added after the other fixtures: leaves them untouched)."""
+    ref = _import_reference()
+    torch.set_num_threads(1)
+    g = torch.Generator().manual_seed(12)
+    fr = synth_fragments(g, 2, 4, 5, 9, 1e-3, packed=True)
+    prob = torch.rand((2, 4, 5, 9), generator=g)
+    prob[0, 0, 0, :2] = 1.0
+    run_uniform_agg_case("agg_uniform", ref, fr, prob, 6, 2e-2, 1.0, 1.0, 100.0, 91)
+
+
 def redraw(kind, shape):
     """The reference's own noise draw (smoothrast.py:20-24, smoothagg.py:20-27) replayed
     from the same global generator state."""
@@ -319,4 +355,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main_uniform() if sys.argv[1:] == ["uniform"] else main()

@@ -51,6 +51,17 @@ def test_aggregate_oracle_matches_reference_bitwise():
     np.testing.assert_array_equal(da.numpy(), f["grad_alpha"])
 
 
+def test_uniform_aggregate_oracle_matches_reference_bitwise():
+    """UniformAgg forward (smoothagg.py:252-271): the oracle's logits + argmax with the
+    reference's U(-1/2, 1/2) draw reproduce its weights."""
+    f = load_golden("agg_uniform")
+    zn, zf = _planes(f, f["zbuf"].shape[0])
+    z, _ = bo.logits(T(f["zbuf"]), zf, zn, T(f["prob"]), T(f["pix_to_face"]) >= 0, T(f["gamma"]), T(f["alpha"]),
+                     float(f["eps"]))
+    W, _, _ = bo.argmax_fwd(z, T(f["noise_a"]), T(f["gamma"]))
+    np.testing.assert_array_equal(W.numpy(), f["W"])
+
+
 def test_soft_blend_oracle_matches_reference_bitwise():
     f = load_golden("soft_blend")
     zn, zf = _planes(f, 1)

@@ -134,6 +134,41 @@ def test_seeded_standalone_aggregate_matches_reference(device, torch_noise):
     assert_close(agg.alpha.grad, f["grad_alpha"], rtol=SCALAR_RTOL, name="alpha")
 
 
+@pytest.mark.gpu
+def test_seeded_uniform_aggregate_matches_reference(device, torch_noise):
+    """UniformAgg.aggregate (smoothagg.py:252-271) through the public class, seeded like the
+    reference: weights equal; the backward raises as the reference's does (:64-70)."""
+    f = load_golden("agg_uniform")
+    agg = pa.UniformAgg(nb_samples=int(f["Sa"]), gamma=float(f["gamma"]), alpha=float(f["alpha"]),
+                        eps=float(f["eps"]))
+    z = torch.tensor(f["zbuf"], device=device, requires_grad=True)
+    pr = torch.tensor(f["prob"], device=device)
+    mask = torch.tensor(f["pix_to_face"], device=device) >= 0
+    zn, zf = _planes(f, z.shape[0], device)
+    torch.manual_seed(int(f["seed"]))
+    W = agg.aggregate(z, zf, zn, pr, mask)
+    np.testing.assert_array_equal(W.detach().cpu().numpy(), f["W"])
+    with pytest.raises(NotImplementedError):
+        W.sum().backward()
+
+
+@pytest.mark.gpu
+def test_philox_uniform_argmax_frequencies(device):
+    """Native Philox U(-1/2, 1/2) agg noise: weights converge to P(argmax z + gamma u) (numpy MC)."""
+    reps = 4096
+    zbuf = torch.tensor([5.0, 5.004]).reshape(1, 1, 1, 2).repeat(1, reps, 1, 1).to(device)
+    prob = torch.ones_like(zbuf) * 0.5
+    mask = torch.ones_like(zbuf, dtype=torch.bool)
+    agg = pa.UniformAgg(nb_samples=16, gamma=1e-2)
+    W = agg.aggregate(zbuf, 100.0, 1.0, prob, mask)
+    w = W.detach().mean(dim=(0, 1, 2)).cpu().double().numpy()
+    z_inv = (100.0 - np.array([5.0, 5.004])) / 99.0
+    z = np.concatenate([1e-2 * np.log(0.5) + z_inv - z_inv.max(), [1e-10 - z_inv.max()]])
+    u = np.random.default_rng(0).uniform(-0.5, 0.5, (400000, 3))
+    ref = np.bincount(np.argmax(z + 1e-2 * u, axis=1), minlength=3) / 400000.0
+    assert np.all(np.abs(w - ref) < 0.01), (w, ref)
+
+
 def _soft(dev):
     f = load_golden("soft_blend")
     fr, d, z = _fragments(f, dev)

@@ -15,7 +15,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from pertrenderer_amd import _native as nat  # noqa: E402
 
-wl = bench.Workload(torch.device("cuda:0"))
+cfg = bench.CONFIGS[os.environ.get("PR_PROF_CONFIG", "cfg2")]
+wl = bench.Workload(torch.device("cuda:0"), cfg["image_size"], cfg["K"], cfg["samples"], batch=cfg["batch"])
 for _ in range(3):  # warm: the last forward's records are kept
     wl.forward().backward()
     torch.cuda.synchronize()
