@@ -1,0 +1,56 @@
+"""BASELINE cfg5 driver (pertrenderer_amd/pose_opt.py, mirroring eval.py:320-409, 576-690) at
+reduced size: the pose optimisation converges towards the true pose for both of eval.py's
+default renderers ("softras", "gaussian"), eagerly and as captured graphs, and the result
+tables have the reference's json layout.  The full run (100 problems x 800 iterations at 256^2)
+is profiles/r2_cfg5.json."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from pertrenderer_amd import pose_opt
+from pertrenderer_amd.results import compare_pose_results
+
+pytestmark = pytest.mark.gpu
+NOISE = ("softras", "gaussian")
+
+
+@pytest.fixture(scope="module")
+def problems(device):
+    torch.manual_seed(0)
+    scene = pose_opt.Scene(device, 128)
+    return scene, pose_opt.make_problems(scene, 3, NOISE, 20.0)
+
+
+@pytest.mark.parametrize("mode", ["graph", "eager"])
+def test_pose_optimisation_converges(problems, mode):
+    scene, probs = problems
+    torch.manual_seed(1)
+    niter = 200 if mode == "graph" else 120
+    per = [pose_opt.run_problem(scene, p, NOISE, 1e-3, 1e-2, 8, 20.0, niter, True, (1.1, 1.1), mode) for p in probs]
+    for nt in NOISE:
+        init = np.array([r[nt]["init_error"] for r in per])
+        final = np.array([r[nt]["final_error"] for r in per])
+        print(mode, nt, "init", init.round(2), "final", final.round(2))
+        assert np.all(np.isfinite(final))
+        assert np.allclose(init, 20.0, atol=1e-3)  # pert_init_intensity: a 20 degree rotation
+        assert final.mean() < 0.6 * init.mean(), (nt, final)
+        assert (final < init).sum() >= 2, (nt, final)
+    tab = pose_opt.tables(per, NOISE, dict(niter=niter), dict(mode=mode))
+    json.dumps(tab)  # eval.py writes these tables with json.dump
+    assert set(tab["mean_solved"]["gaussian"]) == set(pose_opt.THRESHOLDS)
+
+
+def test_graph_and_eager_runs_compare(problems):
+    """results.compare_pose_results over two runs of the same problems: per-problem error
+    differences are reported for every noise type."""
+    scene, probs = problems
+    runs = []
+    for mode in ("graph", "eager"):
+        torch.manual_seed(2)
+        per = [pose_opt.run_problem(scene, p, NOISE, 1e-3, 1e-2, 8, 20.0, 60, False, (1.1, 1.1), mode)
+               for p in probs[:2]]
+        runs.append(pose_opt.tables(per, NOISE, dict(niter=60), dict(mode=mode)))
+    cmp = compare_pose_results(runs[0], runs[1])
+    assert set(NOISE) <= set(cmp)
