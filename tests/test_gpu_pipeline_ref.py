@@ -1,0 +1,110 @@
+"""The GPU renderer of eval.py's pose benchmark against its CPU oracle composition
+(oracle/pipeline_ref.py: C rasterizer oracle + blend oracle + torch TexturesUV / Phong
+restatements), fed the reference's own noise draws (set_noise_source("torch"), the same global
+CPU generator state on both sides): one frame's image and pose gradient, then a short pose
+optimisation run on both, compared per iteration and through results.compare_pose_results."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import pertrenderer_amd as pa
+from oracle import pipeline_ref
+from pertrenderer_amd import pose_opt
+from pertrenderer_amd.renderer import Rotate, so3_exponential_map
+from pertrenderer_amd.results import compare_pose_results
+
+pytestmark = pytest.mark.gpu
+H, K, SIGMA, GAMMA, SR, SA = 64, 50, 1e-3, 1e-2, 16, 8
+
+
+@pytest.fixture
+def setup(device):
+    old = pa.noise.get_noise_source()
+    pa.set_noise_source("torch")
+    torch.manual_seed(0)
+    gpu = pose_opt.Scene(device, H)
+    cpu = pose_opt.Scene(torch.device("cpu"), H)
+    target, R_true = gpu.target()
+    _, (renderer,) = pose_opt.init_renderers(gpu, R_true, sigma=SIGMA, gamma=GAMMA, nb_samples=SA,
+                                             noise_type=("gaussian",))
+    log_rot0 = pose_opt.so3_log_map(R_true @ so3_exponential_map(torch.tensor([[0.2, -0.15, 0.1]], device=device)))
+    tex = cpu.meshes.textures
+    texture = (tex.faces_uvs_list()[0], tex.verts_uvs_list()[0], tex.maps_padded())
+    yield gpu, cpu, renderer, target[0], R_true, log_rot0, texture
+    pa.set_noise_source(old)
+
+
+def _gpu_loss(gpu, renderer, target, log_rot):
+    R = so3_exponential_map(log_rot)
+    m = gpu.meshes.update_padded(Rotate(R).transform_points(gpu.meshes.verts_padded()))
+    img = renderer(m, cameras=gpu.cameras[0], lights=gpu.lights)
+    return ((img[..., :3] - target) ** 2).mean(), img
+
+
+def _cpu_loss(cpu, texture, target, log_rot):
+    R = so3_exponential_map(log_rot)
+    m = cpu.meshes.update_padded(Rotate(R).transform_points(cpu.meshes.verts_padded()))
+    noise_r = torch.randn((SR, 1, H, H, K))  # smoothrast.py:21, then smoothagg.py:21
+    noise_a = torch.randn((SA, 1, H, H, K + 1))
+    img = pipeline_ref.render(m, cpu.cameras[0], cpu.lights.location[0], texture, H, K,
+                              math.log(1.0 / 1e-4 - 1.0) * SIGMA, torch.tensor(SIGMA), torch.tensor(GAMMA),
+                              torch.tensor(1.0), noise_r, noise_a)
+    return ((img[..., :3] - target) ** 2).mean(), img
+
+
+def test_frame_and_pose_gradient_match_cpu_oracle(setup):
+    gpu, cpu, renderer, target, R_true, log_rot0, texture = setup
+    lg = log_rot0.clone().requires_grad_(True)
+    torch.manual_seed(7)
+    lossg, imgg = _gpu_loss(gpu, renderer, target, lg)
+    lossg.backward()
+    lc = log_rot0.detach().cpu().clone().requires_grad_(True)
+    torch.manual_seed(7)
+    lossc, imgc = _cpu_loss(cpu, texture, target.cpu(), lc)
+    lossc.backward()
+    a, e = imgg.detach().cpu().double(), imgc.detach().double()
+    assert float((a - e).abs().max()) < 2e-5, float((a - e).abs().max())
+    assert abs(float(lossg) - float(lossc)) <= 1e-5 * abs(float(lossc))
+    ga, gc = lg.grad.cpu().double(), lc.grad.double()
+    assert float((ga - gc).abs().max()) <= 1e-3 * float(gc.abs().max()), (ga, gc)
+
+
+def _run(step_loss, log_rot0, niter, seed):
+    """eval.py:343-376's iteration (Adam 5e-2, MSE, best-loss pose) with one seed for the run."""
+    log_rot = log_rot0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([log_rot], lr=5e-2)
+    torch.manual_seed(seed)
+    losses, best, best_rot = [], np.inf, log_rot.detach().clone()
+    for _ in range(niter):
+        loss, _ = step_loss(log_rot)
+        opt.zero_grad()
+        loss.backward()
+        lv = float(loss)
+        losses.append(lv)
+        if lv < best:
+            best, best_rot = lv, log_rot.detach().clone()
+        opt.step()
+    return np.array(losses), best_rot
+
+
+def test_pose_runs_match_cpu_oracle(setup):
+    gpu, cpu, renderer, target, R_true, log_rot0, texture = setup
+    n = 25
+    lg, rg = _run(lambda r: _gpu_loss(gpu, renderer, target, r), log_rot0, n, 11)
+    lc, rc = _run(lambda r: _cpu_loss(cpu, texture, target.cpu(), r), log_rot0.cpu(), n, 11)
+    # the first iterations coincide to fp32 rounding; later ones may part where a Monte-Carlo
+    # count flips on a sample at its threshold, so the run is compared at the table level
+    np.testing.assert_allclose(lg[:5], lc[:5], rtol=1e-4)
+    errs = {}
+    for name, rot in (("gpu", rg), ("cpu", rc)):
+        errs[name] = pose_opt.angle_deg(rot.to(R_true.device), R_true)
+    tabs = [dict(mean_errors={"gaussian": [errs[k]]},
+                 mean_solved={"gaussian": {th: [1.0 if errs[k] < th else 0.0] for th in pose_opt.THRESHOLDS}})
+            for k in ("gpu", "cpu")]
+    rep = compare_pose_results(tabs[0], tabs[1])
+    init = pose_opt.angle_deg(log_rot0, R_true)
+    print("init", init, "gpu", errs["gpu"], "cpu", errs["cpu"], rep)
+    assert errs["gpu"] < init and errs["cpu"] < init
+    assert rep["gaussian"]["max_abs_mean_error_diff"] < 0.25 * init
