@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 11
+#define PR_ABI_VERSION 12
 
 /* error codes */
 #define PR_OK 0
@@ -180,6 +180,14 @@ typedef struct PRRastArgs {
   /* Forward: written.  Backward: if set (the forward's), pix_to_face is read only below it.    */
   int32_t* pix_count;
   int32_t flags;                    /* PR_GRAD_PREZEROED: pr_rast_bwd does not zero grad_face_verts */
+  /* Coarse binning (forward; PyTorch3D RasterizationSettings.bin_size / max_faces_per_bin,      */
+  /* rasterize_meshes.py).  bin_size > 0: the face pass appends every face to the bins of        */
+  /* bin_size^2 pixels (rounded up to a multiple of 8) its blur-grown box overlaps, and each      */
+  /* tile culls only its bin's list.  max_faces_per_bin bounds a bin's list; a bin that overflows */
+  /* falls back to culling the whole mesh (PyTorch3D 0.4.0 writes past the list instead), so the  */
+  /* fragments never depend on either knob.  bin_size <= 0: every tile culls the whole mesh.      */
+  int32_t bin_size;
+  int32_t max_faces_per_bin;
 } PRRastArgs;
 
 typedef struct PRInterpArgs {

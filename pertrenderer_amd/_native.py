@@ -74,7 +74,8 @@ class PRRastArgs(C.Structure):
                 ("pix_to_face", _vp), ("zbuf", _vp), ("bary", _vp), ("dists", _vp),
                 ("grad_zbuf", _vp), ("grad_bary", _vp), ("grad_dists", _vp),
                 ("grad_face_verts", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
-                ("pix_count", _vp), ("flags", C.c_int32)]
+                ("pix_count", _vp), ("flags", C.c_int32), ("bin_size", C.c_int32),
+                ("max_faces_per_bin", C.c_int32)]
 
 
 class PRInterpArgs(C.Structure):
@@ -144,7 +145,7 @@ EXPORTS = {
     "pr_shade_fwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
     "pr_shade_bwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
 }
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lib = None
 

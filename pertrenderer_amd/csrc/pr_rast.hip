@@ -151,13 +151,94 @@ PR_DEV void write_face_rec(const float v[9], float blur, int cull_backfaces, Fac
   *bbox = pack_box(xmin, xmax, ymin, ymax);
 }
 
+// ---- coarse bins (PyTorch3D's bin_size / max_faces_per_bin, rasterize_meshes.py): bins of
+//      bs x bs pixels (bs a multiple of every tile shape), per mesh.  The face pass appends
+//      each face to the bins its blur-grown box overlaps (an atomic per (face, bin)); a tile
+//      culls only its bin's list, or the whole mesh if the bin overflowed its capacity.
+struct BinGrid {
+  int bs, nx, ny, cap;  // bin side (pixels), bins per row / column, list capacity per bin
+  int* count;           // (N, ny, nx) list lengths (may exceed cap: overflow); null = no bins
+  int* list;            // (N, ny, nx, cap) face ids (any order)
+  int H, W;
+};
+
+// the bin's rectangle in NDC (its extreme pixel centres; a tile's rectangle lies inside)
+PR_DEV void bin_rect(const BinGrid& g, int bx, int by, float& xmin, float& xmax, float& ymin, float& ymax) {
+  const int c0 = bx * g.bs, c1 = min(c0 + g.bs - 1, g.W - 1), r0 = by * g.bs, r1 = min(r0 + g.bs - 1, g.H - 1);
+  xmax = ndc(g.W - 1 - c0, g.W, g.H); xmin = ndc(g.W - 1 - c1, g.W, g.H);
+  ymax = ndc(g.H - 1 - r0, g.H, g.W); ymin = ndc(g.H - 1 - r1, g.H, g.W);
+}
+
+// pixel index range [lo, hi] (one pixel of margin) whose NDC centres can lie in [vmin, vmax]
+// along an axis of S1 pixels (ndc's inverse, clamped), as columns/rows counted from the far edge
+PR_DEV void pix_range(float vmin, float vmax, int S1, int S2, int& lo, int& hi) {
+  float range = 2.0f;
+  if (S1 > S2) range = ((float)S1 * range) / (float)S2;
+  const float off = range / 2.0f;
+  const float ilo = fminf(fmaxf(((vmin + off) * (float)S1 - off) / range, -2.f), (float)S1 + 1.f);
+  const float ihi = fminf(fmaxf(((vmax + off) * (float)S1 - off) / range, -2.f), (float)S1 + 1.f);
+  // ndc index i maps to pixel S1 - 1 - i
+  lo = max(0, (int)floorf((float)(S1 - 1) - ihi) - 1);
+  hi = min(S1 - 1, (int)ceilf((float)(S1 - 1) - ilo) + 1);
+}
+
+PR_DEV void bin_face(const BinGrid& g, int n, int64_t f, uint2 packed) {
+  const float4 bb = unpack_box(packed);  // the tiles' cull box: bins select a superset
+  if (!(bb.x <= bb.y && bb.z <= bb.w)) return;  // culled face (empty box) or NaN
+  int c0, c1, r0, r1;
+  pix_range(bb.x, bb.y, g.W, g.H, c0, c1);
+  pix_range(bb.z, bb.w, g.H, g.W, r0, r1);
+  if (c0 > c1 || r0 > r1) return;
+  const int bx0 = c0 / g.bs, nbx = c1 / g.bs - bx0 + 1, by0 = r0 / g.bs, nby = r1 / g.bs - by0 + 1;
+  auto hits = [&](int bx, int by) {
+    float xmin, xmax, ymin, ymax;
+    bin_rect(g, bx, by, xmin, xmax, ymin, ymax);
+    return !(bb.x > xmax || bb.y < xmin || bb.z > ymax || bb.w < ymin);
+  };
+  if (nbx * nby <= 16) {
+    // every append's atomic in flight at once (one round trip per face, not one per bin)
+    int b[16], c[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int bx = bx0 + k % nbx, by = by0 + k / nbx;
+      b[k] = k < nbx * nby && hits(bx, by) ? (n * g.ny + by) * g.nx + bx : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c[k] = b[k] >= 0 ? atomicAdd(g.count + b[k], 1) : g.cap;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (c[k] < g.cap) g.list[(int64_t)b[k] * g.cap + c[k]] = (int)f;
+    return;
+  }
+  for (int by = by0; by < by0 + nby; ++by) {
+    for (int bx = bx0; bx < bx0 + nbx; ++bx) {
+      if (!hits(bx, by)) continue;
+      const int bi = (n * g.ny + by) * g.nx + bx;
+      const int c = atomicAdd(g.count + bi, 1);
+      if (c < g.cap) g.list[(int64_t)bi * g.cap + c] = (int)f;
+    }
+  }
+}
+
+// mesh of packed face f (meshes are packed in order: mesh_first_face ascending)
+PR_DEV int mesh_of_sorted(const int64_t* first, int N, int64_t f) {
+  int lo = 0, hi = N - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first[mid] <= f) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 __global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cull_backfaces, FaceRec* out,
-                                 uint2* bbox) {
+                                 uint2* bbox, BinGrid bins, const int64_t* mesh_first, int N) {
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < F; f += (int64_t)gridDim.x * blockDim.x) {
     float v[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) v[i] = fv[f * 9 + i];
     write_face_rec(v, blur, cull_backfaces, out + f, bbox + f);
+    if (bins.count) bin_face(bins, mesh_of_sorted(mesh_first, N, f), f, bbox[f]);
   }
 }
 
@@ -334,6 +415,9 @@ template <int SL> struct RastCfg {
   static constexpr int CH = SL >= 4 ? PR_RAST_CH4 : 64;
   static_assert(CAP <= 8 * 64, "suffix-min pass holds CAP / 64 <= 8 entries per lane");
 };
+#ifndef PR_RAST_MERGE  // 0: candidates landing inside a queue are inserted slice by slice (r1 path)
+#define PR_RAST_MERGE 1
+#endif
 #ifndef PR_RAST_CULLU  // sweeps: 8 measured equal, 4 slower (+10 us)
 #define PR_RAST_CULLU 16
 #endif
@@ -501,7 +585,7 @@ PR_DEV void ring_tile(int b, int m, int& tx, int& ty) {
 #endif
 template <int SL, bool PERSP, bool CLIP, bool FRAG>
 __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces,
-                                                      const uint2* __restrict__ fbox, int ring) {
+                                                      const uint2* __restrict__ fbox, int ring, BinGrid bins) {
   constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
   constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
   extern __shared__ float smem[];
@@ -537,14 +621,22 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
   const float txmax = ndc(W - 1 - col0, W, H), txmin = ndc(W - 1 - c1, W, H);
   const float tymax = ndc(H - 1 - row0, H, W), tymin = ndc(H - 1 - r1, H, W);
   const float tcx = 0.5f * (txmin + txmax), tcy = 0.5f * (tymin + tymax);
-  const int64_t fb = a.mesh_first_face[n], fe = fb + a.mesh_num_faces[n];
+  const int64_t fb = a.mesh_first_face[n];
+  // the faces to cull: the tile's bin list, or the whole mesh (no bins, or the bin overflowed)
+  const int* ids = nullptr;
+  int64_t fe = a.mesh_num_faces[n];
+  if (bins.count) {
+    const int b = (n * bins.ny + row0 / bins.bs) * bins.nx + col0 / bins.bs;
+    const int c = bins.count[b];
+    if (c <= bins.cap) { ids = bins.list + (int64_t)b * bins.cap; fe = c; }
+  }
   constexpr bool clip = CLIP;
   const float blur = a.blur_radius;
   // the pixel's queue state, replicated in its SL lanes
   int qs = 0;
   float qlast_z = __builtin_inff();
   int qlast_f = 0x7fffffff;
-  int64_t base = fb;
+  int64_t base = 0;  // position in the cull list (face fb + base, or ids[base])
 #ifdef PR_RAST_PROFILE
   long long stamp[6] = {0, 0, 0, 0, 0, 0}, t_ = __builtin_amdgcn_s_memtime();
   const long long rt0 = __builtin_amdgcn_s_memrealtime();
@@ -557,23 +649,27 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     int nl = 0;
     while (base < fe && nl <= kCap - 64) {
       uint2 pb[kCullU];  // packed fp16 boxes: half the registers of unpacked ones
+      int fi[kCullU];
 #pragma unroll
       for (int u = 0; u < kCullU; ++u) {
-        const int64_t f = base + u * 64 + lane;
-        pb[u] = fbox[f < fe ? f : fe - 1];
+        const int64_t i = base + u * 64 + lane;
+        const int64_t ic = i < fe ? i : fe - 1;
+        fi[u] = ids ? ids[ic] : (int)(fb + ic);
       }
+#pragma unroll
+      for (int u = 0; u < kCullU; ++u) pb[u] = fbox[fi[u]];
       int64_t next = base + 64 * kCullU;
       bool stop = false;  // wave-uniform; no break, so bb[] stays in registers
 #pragma unroll
       for (int u = 0; u < kCullU; ++u) {
-        const int64_t f = base + u * 64 + lane;
+        const int64_t i = base + u * 64 + lane;
         const float4 bb = unpack_box(pb[u]);
-        const bool keep = f < fe && !(bb.x > txmax || bb.y < txmin || bb.z > tymax || bb.w < tymin);
+        const bool keep = i < fe && !(bb.x > txmax || bb.y < txmin || bb.z > tymax || bb.w < tymin);
         const uint64_t bal = __ballot(keep);
         const int cnt = __popcll(bal);
         if (!stop && nl + cnt > kCap) { stop = true; next = base + u * 64; }
         if (!stop) {
-          if (keep) lfid[nl + __popcll(bal & ((1ull << lane) - 1ull))] = (int)f;
+          if (keep) lfid[nl + __popcll(bal & ((1ull << lane) - 1ull))] = fi[u];
           nl += cnt;
         }
       }
@@ -727,14 +823,21 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
           if constexpr (SL > 1) {
             // ---- batch path: when every candidate of the wave is an append (the common
             //      case, faces arrive in depth order), a pixel's SL candidates enter its
-            //      queue together, each at qs + its rank among them; else the slices insert
-            //      in turn below.  Same queue either way (the K smallest keys, sorted).
+            //      queue together, each at qs + its rank among them; else the candidates
+            //      merge into the queues (PR_RAST_MERGE; the r1 path inserted slice by slice
+            //      below).  Same queue either way (the K smallest keys, sorted).
             if (ok[j] && clip && qs == K && zk > qlast_z + fabsf(qlast_z) * 1e-6f) done = true;
             const float pz = pzv[j];
             const bool enter = ok[j] && !done && cand[j] && (qs < K || key_less(pz, fid, qlast_z, qlast_f));
             const bool app = enter && (qs == 0 || key_less(qlast_z, qlast_f, pz, fid));
-            if (__ballot(enter && !app) == 0) {
+            const bool slow = __ballot(enter && !app) != 0;
+#if PR_RAST_MERGE
+            if (__ballot(enter) == 0) continue;
+            {
+#else
+            if (!slow) {
               if (__ballot(enter) == 0) continue;
+#endif
               bool oe[SL - 1];
               float oz[SL - 1];
               int of[SL - 1];
@@ -747,6 +850,58 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
                 nq += oe[r - 1] ? 1 : 0;
                 rank += (enter && oe[r - 1] && key_less(oz[r - 1], of[r - 1], pz, fid)) ? 1 : 0;
               }
+#if PR_RAST_MERGE
+              if (slow) {
+                // ---- merge path: some candidate of the wave lands inside its pixel's queue.
+                //      Each candidate's final position is (queue keys below it) + (its rank
+                //      among the pixel's entering candidates); the queue entries at or above
+                //      the lowest landing point move up by the number of candidates below
+                //      them, the pixel's SL lanes sharing the moves (top down: every write
+                //      lands at or above the reads still to come).  Entries pushed to K or
+                //      beyond drop off.  Same queue as inserting one candidate at a time.
+                int below = qs;
+                if (enter && !app) {  // key below the queue's last: binary search in [0, qs - 1]
+                  int lo = 0, hi = qs - 1;
+                  while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    const float2 e = q[mid * TP + pix];
+                    if (key_less(e.x, __float_as_int(e.y), pz, fid)) lo = mid + 1;
+                    else hi = mid;
+                  }
+                  below = lo;
+                }
+                int pmin = enter ? below : qs;
+#pragma unroll
+                for (int r = 1; r < SL; ++r) pmin = min(pmin, quad_rot<SL>(pmin, r));
+                for (int i = qs - 1 - slice; i >= pmin; i -= 2 * SL) {
+                  const bool two = i - SL >= pmin;
+                  const float2 e0 = q[i * TP + pix];
+                  const float2 e1 = q[(two ? i - SL : i) * TP + pix];
+                  int s0 = enter && key_less(pz, fid, e0.x, __float_as_int(e0.y)) ? 1 : 0;
+                  int s1 = enter && key_less(pz, fid, e1.x, __float_as_int(e1.y)) ? 1 : 0;
+#pragma unroll
+                  for (int r = 0; r < SL - 1; ++r) {
+                    s0 += oe[r] && key_less(oz[r], of[r], e0.x, __float_as_int(e0.y)) ? 1 : 0;
+                    s1 += oe[r] && key_less(oz[r], of[r], e1.x, __float_as_int(e1.y)) ? 1 : 0;
+                  }
+                  if (i + s0 < K) q[(i + s0) * TP + pix] = e0;
+                  if (two && i - SL + s1 < K) q[(i - SL + s1) * TP + pix] = e1;
+                }
+                const int pos = below + rank;
+                if (enter && pos < K) q[pos * TP + pix] = make_float2(pz, __int_as_float(fid));
+                qs = min(qs + nq, K);
+                if (qs > 0) {
+                  const float2 last = q[(qs - 1) * TP + pix];
+                  qlast_z = last.x;
+                  qlast_f = __float_as_int(last.y);
+                }
+#ifdef PR_RAST_PROFILE
+                n_ins += enter && !app ? 1 : 0;
+                n_app += enter && app ? 1 : 0;
+#endif
+                continue;
+              }
+#endif
               const int nkept = min(nq, K - qs);  // the largest ones drop off a full queue
               if (enter && rank < nkept) q[(qs + rank) * TP + pix] = make_float2(pz, __int_as_float(fid));
               if (nkept > 0) {  // new last key: the entered one of rank nkept - 1
@@ -908,7 +1063,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
 
 template <int SL, bool PERSP, bool CLIP>
 void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, bool frag, size_t lds,
-                        hipStream_t st) {
+                        const BinGrid& bins, hipStream_t st) {
   constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW;
   dim3 grid((a.W + TW - 1) / TW, (a.H + TH - 1) / TH, a.N);
   // centre-out tile order on square grids of even side (PR_RAST_ORDER bit 0; 0: row-major)
@@ -918,26 +1073,26 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb,
   static const int prio_t = getenv("PR_RAST_PRIO_T") ? atoi(getenv("PR_RAST_PRIO_T")) & 255 : 40;
   const bool sq = grid.x % 2 == 0 && (grid.y == grid.x || grid.y == 2 * grid.x);
   const int ring = (ring_env && sq ? 1 : 0) | (prio_env ? 2 : 0) | (prio_t << 8);
-  if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring);
-  else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring);
+  if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring, bins);
+  else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring, bins);
 }
 
 template <bool PERSP, bool CLIP>
 void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, int sl, bool frag, size_t lds,
-                        hipStream_t st) {
-  if (sl == 8) launch_rast_fwd_sl<8, PERSP, CLIP>(a, fr, fb, frag, lds, st);
-  else if (sl == 4) launch_rast_fwd_sl<4, PERSP, CLIP>(a, fr, fb, frag, lds, st);
-  else if (sl == 2) launch_rast_fwd_sl<2, PERSP, CLIP>(a, fr, fb, frag, lds, st);
-  else launch_rast_fwd_sl<1, PERSP, CLIP>(a, fr, fb, frag, lds, st);
+                        const BinGrid& bins, hipStream_t st) {
+  if (sl == 8) launch_rast_fwd_sl<8, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st);
+  else if (sl == 4) launch_rast_fwd_sl<4, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st);
+  else if (sl == 2) launch_rast_fwd_sl<2, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st);
+  else launch_rast_fwd_sl<1, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st);
 }
 
 void launch_rast_fwd(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, int sl, bool frag, size_t lds,
-                     hipStream_t st) {
+                     const BinGrid& bins, hipStream_t st) {
   const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
-  if (persp && clip) launch_rast_fwd_pc<true, true>(a, fr, fb, sl, frag, lds, st);
-  else if (persp) launch_rast_fwd_pc<true, false>(a, fr, fb, sl, frag, lds, st);
-  else if (clip) launch_rast_fwd_pc<false, true>(a, fr, fb, sl, frag, lds, st);
-  else launch_rast_fwd_pc<false, false>(a, fr, fb, sl, frag, lds, st);
+  if (persp && clip) launch_rast_fwd_pc<true, true>(a, fr, fb, sl, frag, lds, bins, st);
+  else if (persp) launch_rast_fwd_pc<true, false>(a, fr, fb, sl, frag, lds, bins, st);
+  else if (clip) launch_rast_fwd_pc<false, true>(a, fr, fb, sl, frag, lds, bins, st);
+  else launch_rast_fwd_pc<false, false>(a, fr, fb, sl, frag, lds, bins, st);
 }
 
 // Forward, pass 2: barycentrics (perspective-corrected, clipped) and signed squared
@@ -1341,7 +1496,7 @@ __global__ void project_fwd_kernel(PRProjectArgs a) {
 // thread per face, project_fwd_kernel's operations per corner), plus the zeroing of the
 // backward's accumulators (grad_face_verts, grad_verts) so the backward needs no memset.
 __global__ void project_prep_kernel(PRProjectArgs a, float blur, int cull_backfaces, FaceRec* recs, uint2* bbox,
-                                    float* zero_fv, float* zero_v) {
+                                    float* zero_fv, float* zero_v, BinGrid bins) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.F; f += stride) {
     const int n = mesh_of(a.mesh_first_face, a.mesh_num_faces, a.N, f);
@@ -1360,6 +1515,7 @@ __global__ void project_prep_kernel(PRProjectArgs a, float blur, int cull_backfa
 #pragma unroll
     for (int i = 0; i < 9; ++i) a.face_verts[f * 9 + i] = fv[i];
     write_face_rec(fv, blur, cull_backfaces, recs + f, bbox + f);
+    if (bins.count) bin_face(bins, n, f, bbox[f]);
   }
   if (zero_fv)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.F * 9; i += stride) zero_fv[i] = 0.f;
@@ -1422,12 +1578,51 @@ extern "C" int pr_rast_prof_dump(void* dst, size_t bytes) {
 }
 #endif
 
-extern "C" size_t pr_rast_fwd_workspace_size(const PRRastArgs* a) {
-  if (!a) return 0;
-  return (size_t)(a->F > 0 ? a->F : 1) * (sizeof(FaceRec) + sizeof(uint2));  // records + fp16 cull boxes
+// the coarse bin grid of a forward call (no bins: count == nullptr); pointers into the
+// workspace after the face records and cull boxes when ws is given
+static BinGrid bin_grid(const PRRastArgs& a, void* ws) {
+  BinGrid g{};
+  g.H = a.H; g.W = a.W;
+  if (a.bin_size <= 0 || a.N <= 0 || a.H <= 0 || a.W <= 0) return g;
+  g.bs = (a.bin_size + 7) / 8 * 8;  // a multiple of every tile shape
+  g.nx = (a.W + g.bs - 1) / g.bs;
+  g.ny = (a.H + g.bs - 1) / g.bs;
+  // PyTorch3D's default cap (rasterize_meshes.py: max(10000, F / 5)), never above F
+  const int64_t F = a.F > 0 ? a.F : 1;
+  const int64_t mfpb = a.max_faces_per_bin > 0 ? a.max_faces_per_bin : std::max<int64_t>(10000, F / 5);
+  g.cap = (int)std::min<int64_t>(mfpb, F);
+  if (ws) {
+    char* p = reinterpret_cast<char*>(ws) + (size_t)F * (sizeof(FaceRec) + sizeof(uint2));
+    g.count = reinterpret_cast<int*>(p);
+    g.list = g.count + (size_t)a.N * g.ny * g.nx;
+  }
+  return g;
 }
 
-static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2* fbox, hipStream_t st);
+static size_t bin_bytes(const PRRastArgs& a) {
+  const BinGrid g = bin_grid(a, nullptr);
+  if (g.bs == 0) return 0;
+  const size_t nb = (size_t)a.N * g.ny * g.nx;
+  return nb * sizeof(int) * (1 + (size_t)g.cap);
+}
+
+extern "C" size_t pr_rast_fwd_workspace_size(const PRRastArgs* a) {
+  if (!a) return 0;
+  // records + fp16 cull boxes + bin counts and lists
+  return (size_t)(a->F > 0 ? a->F : 1) * (sizeof(FaceRec) + sizeof(uint2)) + bin_bytes(*a);
+}
+
+// bins of this call, their counters zeroed on the stream (before the face pass appends)
+static int bins_begin(const PRRastArgs& a, BinGrid& g, hipStream_t st) {
+  g = bin_grid(a, a.workspace);
+  if (!g.count) return PR_OK;
+  if (hipMemsetAsync(g.count, 0, (size_t)a.N * g.ny * g.nx * sizeof(int), st) != hipSuccess)
+    return set_error(PR_ERR_HIP, "rast_fwd: bin counter memset failed");
+  return PR_OK;
+}
+
+static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2* fbox, const BinGrid& bins,
+                             hipStream_t st);
 
 extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "rast_fwd: null args");
@@ -1439,15 +1634,19 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   FaceRec* fr = reinterpret_cast<FaceRec*>(a.workspace);
   uint2* fbox = reinterpret_cast<uint2*>(fr + (a.F > 0 ? a.F : 1));
+  BinGrid bins;
+  if (int e = bins_begin(a, bins, st)) return e;
   if (a.F > 0) {
     const int nb = (int)std::min<int64_t>((a.F + kThreads - 1) / kThreads, 1024);
-    face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr, fbox);
+    face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr, fbox, bins,
+                                              a.mesh_first_face, a.N);
     if (int e = check_launch("rast_face_prep")) return e;
   }
-  return rast_fwd_prepared(a, fr, fbox, st);
+  return rast_fwd_prepared(a, fr, fbox, bins, st);
 }
 
-static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2* fbox, hipStream_t st) {
+static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2* fbox, const BinGrid& bins,
+                             hipStream_t st) {
   // face slices per pixel (tile 8x8 / 8x4 / 4x4): 4 measured fastest on the bench frame
   // with the two-stage face test (107 us vs 118-123 at 2 and 157 at 1); PR_RAST_SLICES=1|2|4
   // overrides (sweeps).  FRAG: barycentrics / distances written by the rasterizer itself
@@ -1461,7 +1660,7 @@ static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2
   if (const char* e = getenv("PR_RAST_FRAG")) frag = atoi(e) != 0;
   const size_t lds = rast_fwd_lds(a.K, sl);
   if (lds > 160 * 1024) return set_error(PR_ERR_ARG, "rast_fwd: faces_per_pixel too large for the LDS queue (max 300)");
-  launch_rast_fwd(a, fr, fbox, sl, frag, lds, st);
+  launch_rast_fwd(a, fr, fbox, sl, frag, lds, bins, st);
   if (int e = check_launch("rast_fwd")) return e;
   if (frag) return PR_OK;
   const int64_t total = (int64_t)a.N * a.H * a.W * a.K;
@@ -1564,13 +1763,15 @@ extern "C" int pr_project_rast_fwd(const PRProjectArgs* pa, const PRRastArgs* ra
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   FaceRec* fr = reinterpret_cast<FaceRec*>(a.workspace);
   uint2* fbox = reinterpret_cast<uint2*>(fr + (a.F > 0 ? a.F : 1));
+  BinGrid bins;
+  if (int e = bins_begin(a, bins, st)) return e;
   const int64_t work = std::max<int64_t>(std::max<int64_t>(a.F, a.grad_face_verts ? a.F * 9 : 0),
                                          pa->grad_verts ? pa->V * 3 : 0);
   if (work > 0) {
     const int nb = (int)std::min<int64_t>((work + kThreads - 1) / kThreads, 1024);
     project_prep_kernel<<<nb, kThreads, 0, st>>>(*pa, a.blur_radius, a.cull_backfaces, fr, fbox, a.grad_face_verts,
-                                                 pa->grad_verts);
+                                                 pa->grad_verts, bins);
     if (int e = check_launch("project_prep")) return e;
   }
-  return rast_fwd_prepared(a, fr, fbox, st);
+  return rast_fwd_prepared(a, fr, fbox, bins, st);
 }

@@ -8,6 +8,7 @@ pix_to_face (N,H,W,K) int64 packed face ids (-1 padded), zbuf, bary_coords
 (N,H,W,K,3), dists (signed squared distance, negative inside).  Called by the
 reference at experiments/eval.py:165-168 (RasterizationSettings at :135-141).
 """
+import os
 from typing import NamedTuple, Optional
 
 import torch
@@ -36,8 +37,8 @@ class RasterizationSettings:
         self.image_size = image_size
         self.blur_radius = blur_radius
         self.faces_per_pixel = faces_per_pixel
-        self.bin_size = bin_size                  # accepted for API parity; the kernel bins per tile
-        self.max_faces_per_bin = max_faces_per_bin  # no overflow: candidate lists are unbounded
+        self.bin_size = bin_size                  # coarse bins (0: every tile culls the whole mesh)
+        self.max_faces_per_bin = max_faces_per_bin  # bin list capacity; an overflowing bin culls the mesh
         self.perspective_correct = perspective_correct
         self.clip_barycentric_coords = clip_barycentric_coords
         self.cull_backfaces = cull_backfaces
@@ -47,6 +48,26 @@ def _hw(image_size):
     if isinstance(image_size, (tuple, list)):
         return int(image_size[0]), int(image_size[1])
     return int(image_size), int(image_size)
+
+
+def bin_params(bin_size, max_faces_per_bin, H, W, F, N=1):
+    """(bin_size, max_faces_per_bin) for the native rasterizer.  An explicit bin_size > 0 bins
+    with PyTorch3D 0.4.0's meaning (rasterize_meshes.py; the dependency is not vendored, restated)
+    and max_faces_per_bin (None: max(10000, F / 5)) is the list capacity; an overflowing bin falls
+    back to the whole mesh, so the fragments never depend on either knob.  bin_size None or 0 runs
+    the tiles' whole-mesh cull: measured faster than bins on the cfg 2 frame (1280 faces) and on
+    an 81 920-face sphere at 256^2 (tools/rast_bins_bench.py).
+    PR_RAST_BINS=0 forces the naive path, PR_RAST_BINS=1 resolves None as PyTorch3D does (bins of
+    8 / 16 / 32 / 64 pixels up to 64 / 256 / 512 / 1024-pixel images)."""
+    env = os.environ.get("PR_RAST_BINS")
+    if env == "0" or (bin_size is None and env != "1"):
+        return 0, 0
+    if bin_size is None:
+        size = max(H, W)
+        bin_size = 8 if size <= 64 else 16 if size <= 256 else 32 if size <= 512 else 64
+    if max_faces_per_bin is None:
+        max_faces_per_bin = int(max(10000, F / 5))
+    return int(bin_size), int(min(max_faces_per_bin, 2**31 - 1))
 
 
 def attach_valid_counts(pix_to_face, counts):
@@ -66,7 +87,7 @@ def valid_counts(pix_to_face):
 
 class _RasterizeFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, face_verts, first, nfaces, H, W, K, blur, persp, clip, cull):
+    def forward(ctx, face_verts, first, nfaces, H, W, K, blur, persp, clip, cull, bins=(0, 0)):
         nat.require_device(face_verts, first, nfaces)
         lib = nat.load()
         fv = face_verts.detach().to(F32).contiguous()
@@ -77,6 +98,7 @@ class _RasterizeFn(torch.autograd.Function):
         a.F, a.N, a.H, a.W, a.K = fv.shape[0], N, H, W, K
         a.blur_radius, a.perspective_correct = float(blur), int(persp)
         a.clip_barycentric_coords, a.cull_backfaces = int(clip), int(cull)
+        a.bin_size, a.max_faces_per_bin = bins
         p2f = torch.empty((N, H, W, K), dtype=torch.int64, device=dev)
         zbuf = torch.empty((N, H, W, K), dtype=F32, device=dev)
         bary = torch.empty((N, H, W, K, 3), dtype=F32, device=dev)
@@ -122,7 +144,7 @@ class _RasterizeFn(torch.autograd.Function):
         nat.check(lib.pr_rast_bwd(a, nat.stream_of(fv)), "pr_rast_bwd")
         if timing is not None:
             timing.stop("rast_bwd")
-        return gfv, None, None, None, None, None, None, None, None, None
+        return gfv, None, None, None, None, None, None, None, None, None, None
 
 
 class _ProjectRasterizeFn(torch.autograd.Function):
@@ -132,7 +154,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
     forward kernel (no memsets).  Same values as project_faces followed by _RasterizeFn."""
 
     @staticmethod
-    def forward(ctx, verts, faces, first, nfaces, w2v, proj, H, W, K, blur, persp, clip, cull):
+    def forward(ctx, verts, faces, first, nfaces, w2v, proj, H, W, K, blur, persp, clip, cull, bins=(0, 0)):
         from .project import _per_mesh
         nat.require_device(verts, faces, first, nfaces, w2v, proj)
         lib = nat.load()
@@ -154,6 +176,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         a.F, a.N, a.H, a.W, a.K = F, N, H, W, K
         a.blur_radius, a.perspective_correct = float(blur), int(persp)
         a.clip_barycentric_coords, a.cull_backfaces = int(clip), int(cull)
+        a.bin_size, a.max_faces_per_bin = bins
         p2f = torch.empty((N, H, W, K), dtype=torch.int64, device=dev)
         zbuf = torch.empty((N, H, W, K), dtype=F32, device=dev)
         bary = torch.empty((N, H, W, K, 3), dtype=F32, device=dev)
@@ -180,7 +203,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
     def backward(ctx, gp2f, gzbuf, gbary, gdists, gcounts):
         v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv = ctx.saved_tensors
         if gfv is None:
-            return (None,) * 13
+            return (None,) * 14
         H, W, K, blur, persp, clip, cull = ctx.cfg
         # a second backward (retain_graph) finds the accumulators used: zero them again
         flags = nat.PR_GRAD_PREZEROED if ctx.prezeroed else 0
@@ -210,7 +233,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         pa.V, pa.F, pa.N = v.shape[0], f.shape[0], first.shape[0]
         pa.grad_face_verts, pa.grad_verts, pa.flags = nat.ptr(gfv), nat.ptr(gv), flags
         nat.check(lib.pr_project_bwd(pa, nat.stream_of(gv)), "pr_project_bwd")
-        return (gv,) + (None,) * 12
+        return (gv,) + (None,) * 13
 
 
 def rasterize_meshes(meshes, image_size=256, blur_radius=0.0, faces_per_pixel=8, bin_size=None,
@@ -222,12 +245,14 @@ def rasterize_meshes(meshes, image_size=256, blur_radius=0.0, faces_per_pixel=8,
     first = meshes.mesh_to_faces_packed_first_idx().to(verts.device)
     nfaces = meshes.num_faces_per_mesh().to(verts.device)
     H, W = _hw(image_size)
+    bins = bin_params(bin_size, max_faces_per_bin, H, W, face_verts.shape[0], first.shape[0])
     return _rasterize(face_verts, first, nfaces, H, W, int(faces_per_pixel), float(blur_radius),
-                      bool(perspective_correct), bool(clip_barycentric_coords), bool(cull_backfaces))
+                      bool(perspective_correct), bool(clip_barycentric_coords), bool(cull_backfaces), bins)
 
 
-def _rasterize(face_verts, first, nfaces, H, W, K, blur, persp, clip, cull):
-    p2f, zbuf, bary, dists, counts = _RasterizeFn.apply(face_verts, first, nfaces, H, W, K, blur, persp, clip, cull)
+def _rasterize(face_verts, first, nfaces, H, W, K, blur, persp, clip, cull, bins=(0, 0)):
+    p2f, zbuf, bary, dists, counts = _RasterizeFn.apply(face_verts, first, nfaces, H, W, K, blur, persp, clip, cull,
+                                                        bins)
     return attach_valid_counts(p2f, counts), zbuf, bary, dists
 
 
@@ -266,10 +291,12 @@ class MeshRasterizer(torch.nn.Module):
             first = meshes_world.mesh_to_faces_packed_first_idx()
             nfaces = meshes_world.num_faces_per_mesh()
             H, W = _hw(rs.image_size)
+            faces = meshes_world.faces_packed()
             p2f, zbuf, bary, dists, counts = _ProjectRasterizeFn.apply(
-                meshes_world.verts_packed(), meshes_world.faces_packed(), first, nfaces,
+                meshes_world.verts_packed(), faces, first, nfaces,
                 cameras.world_to_view_matrix(), cameras.projection_matrix(), H, W, int(rs.faces_per_pixel),
-                float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces))
+                float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces),
+                bin_params(rs.bin_size, rs.max_faces_per_bin, H, W, faces.shape[0], first.shape[0]))
             return Fragments(pix_to_face=attach_valid_counts(p2f, counts), zbuf=zbuf, bary_coords=bary, dists=dists)
         meshes_screen = self.transform(meshes_world, **kwargs)
         p2f, zbuf, bary, dists = rasterize_meshes(

@@ -42,9 +42,26 @@ def _batch(device, n=16):
     return Meshes(vl, fl), FoVPerspectiveCameras(R=R, T=T, device=device)
 
 
-def _fragments(mesh, cams, size, K):
-    rs = RasterizationSettings(image_size=size, blur_radius=BLUR, faces_per_pixel=K, perspective_correct=False)
+def _fragments(mesh, cams, size, K, **kw):
+    rs = RasterizationSettings(image_size=size, blur_radius=BLUR, faces_per_pixel=K, perspective_correct=False, **kw)
     return MeshRasterizer(cameras=cams, raster_settings=rs)(mesh)
+
+
+@pytest.mark.parametrize("bin_size,mfpb", [(8, None), (64, 200)])
+def test_cfg4_coarse_bins_do_not_change_fragments(bin_size, mfpb, device):
+    """The whole cfg 4 batch: PyTorch3D's default bins (32 px at 512^2), 8-px bins and 64-px bins
+    whose 200-face capacity overflows (those tiles cull the whole mesh) all give the naive path's
+    fragments bit for bit."""
+    size, K = 512, 150
+    mesh, cams = _batch(device)
+    with torch.no_grad():
+        ref = _fragments(mesh, cams, size, K, bin_size=0)
+        for f in (_fragments(mesh, cams, size, K), _fragments(mesh, cams, size, K, bin_size=bin_size,
+                                                               max_faces_per_bin=mfpb)):
+            assert torch.equal(f.pix_to_face, ref.pix_to_face)
+            assert torch.equal(valid_counts(f.pix_to_face), valid_counts(ref.pix_to_face))
+            for a, b in ((f.zbuf, ref.zbuf), (f.bary_coords, ref.bary_coords), (f.dists, ref.dists)):
+                assert torch.equal(a.view(torch.int32), b.view(torch.int32))
 
 
 def test_cfg4_rasterizer_batch(device):

@@ -65,11 +65,11 @@ def _soup(F, seed, zmin=0.5, spread=1.2, size=0.4):
     return fv
 
 
-def _run_native(fv, first, nf, H, W, K, blur, persp, clip, cull, dev):
+def _run_native(fv, first, nf, H, W, K, blur, persp, clip, cull, dev, bins=(0, 0)):
     from pertrenderer_amd.renderer.rasterizer import _rasterize
     fvt = torch.tensor(fv, device=dev, requires_grad=True)
     out = _rasterize(fvt, torch.tensor(first, device=dev), torch.tensor(nf, device=dev), H, W, K, blur,
-                             persp, clip, cull)
+                     persp, clip, cull, bins)
     return fvt, out
 
 
@@ -79,11 +79,14 @@ def _run_native(fv, first, nf, H, W, K, blur, persp, clip, cull, dev):
     dict(H=24, W=40, K=5, blur=2e-3, persp=True, clip=True, cull=True),
     dict(H=16, W=16, K=70, blur=5e-2, persp=False, clip=True, cull=False),
 ])
-def test_rasterizer_forward_matches_oracle_bitwise(cfg, device):
+@pytest.mark.parametrize("bins", [(0, 0), (8, 10000), (16, 6)])
+def test_rasterizer_forward_matches_oracle_bitwise(cfg, bins, device):
+    """bins: no coarse bins; 8-pixel bins; 16-pixel bins of capacity 6, so that most bins overflow
+    and their tiles fall back to the whole mesh.  The fragments are the same bits every way."""
     fv = np.concatenate([_soup(150, 1), _soup(90, 2)])
     first, nf = np.array([0, 150]), np.array([150, 90])
     _, (p2f, zbuf, bary, dists) = _run_native(fv, first, nf, cfg["H"], cfg["W"], cfg["K"], cfg["blur"],
-                                              cfg["persp"], cfg["clip"], cfg["cull"], device)
+                                              cfg["persp"], cfg["clip"], cfg["cull"], device, bins)
     rp, rz, rb, rd = rast_ref.rast_fwd(fv, first, nf, cfg["H"], cfg["W"], cfg["K"], cfg["blur"], cfg["persp"],
                                        cfg["clip"], cfg["cull"])
     assert (rp >= 0).sum() > 100
@@ -239,3 +242,32 @@ def test_fused_projection_rasterizer_matches_separate_ops(device):
     ((zbuf * gz).sum() + (bary * gb).sum() + (dists * gd).sum()).backward()
     assert_close(g1, v2.grad, rtol=1e-4, atol_rel=1e-5, name="d verts")
     assert_close(g1b, v2.grad, rtol=1e-4, atol_rel=1e-5, name="d verts (second backward)")
+
+
+@pytest.mark.parametrize("bin_size,mfpb", [(8, None), (16, 300), (None, None)])
+def test_rasterizer_large_mesh_bins_match_oracle(bin_size, mfpb, device):
+    """An 81 920-face sphere (sphere_642 subdivided 3x) through MeshRasterizer at 64x64, K=20 with
+    blur: PyTorch3D's bins for this size (8 px, capacity max(10000, F/5)), 16-px bins with a
+    300-face capacity that the central bins overflow, and the naive path (None) -- all bit-exact
+    against the C oracle."""
+    import meshgen
+    from pertrenderer_amd.renderer.rasterizer import valid_counts
+    v, f = meshgen.fine_sphere(3)
+    assert f.shape[0] == 81920
+    mesh = Meshes([torch.tensor(v, device=device)], [torch.tensor(f, device=device)])
+    R, T = look_at_view_transform(2.7, 30.0, 120.0, device=device)
+    cams = FoVPerspectiveCameras(R=R, T=T, device=device)
+    H, K, blur = 64, 20, 2e-4
+    rs = RasterizationSettings(image_size=H, blur_radius=blur, faces_per_pixel=K, bin_size=bin_size,
+                               max_faces_per_bin=mfpb)
+    with torch.no_grad():
+        frag = MeshRasterizer(cameras=cams, raster_settings=rs)(mesh)
+    fv = project_faces(mesh.verts_packed(), mesh.faces_packed(), mesh.mesh_to_faces_packed_first_idx(),
+                       mesh.num_faces_per_mesh(), cams.world_to_view_matrix(), cams.projection_matrix())
+    rp, rz, rb, rd = rast_ref.rast_fwd(fv.cpu().numpy(), [0], [f.shape[0]], H, H, K, blur, False, True, False)
+    assert (rp >= 0).sum(-1).max() == K  # deep pixels: the K-truncation is exercised
+    np.testing.assert_array_equal(frag.pix_to_face.cpu().numpy(), rp)
+    np.testing.assert_array_equal(valid_counts(frag.pix_to_face).cpu().numpy(), (rp >= 0).sum(-1))
+    np.testing.assert_array_equal(frag.zbuf.cpu().numpy(), rz)
+    np.testing.assert_array_equal(frag.dists.cpu().numpy(), rd)
+    np.testing.assert_array_equal(frag.bary_coords.cpu().numpy(), rb)

@@ -12,16 +12,17 @@ from pertrenderer_amd.renderer.rasterizer import _rasterize, valid_counts
 pytestmark = pytest.mark.gpu
 
 
-def _native(case, dev, requires_grad=False):
+def _native(case, dev, requires_grad=False, bins=(0, 0)):
     fv = torch.tensor(case["fv"], dtype=torch.float32, device=dev, requires_grad=requires_grad)
     out = _rasterize(fv, torch.tensor(case["first"], device=dev), torch.tensor(case["nfaces"], device=dev),
-                     case["H"], case["W"], case["K"], case["blur"], case["persp"], case["clip"], case["cull"])
+                     case["H"], case["W"], case["K"], case["blur"], case["persp"], case["clip"], case["cull"], bins)
     return fv, out
 
 
+@pytest.mark.parametrize("bins", [(0, 0), (8, 10000)], ids=["naive", "bins8"])
 @pytest.mark.parametrize("case", rast_kat.CASES, ids=[c["name"] for c in rast_kat.CASES])
-def test_hip_rasterizer_known_answers(case, device):
-    _, (p2f, zbuf, bary, dists) = _native(case, device)
+def test_hip_rasterizer_known_answers(case, bins, device):
+    _, (p2f, zbuf, bary, dists) = _native(case, device, bins=bins)
     rast_kat.check(case, p2f.cpu().numpy(), zbuf.cpu().numpy(), bary.cpu().numpy(), dists.cpu().numpy())
     np.testing.assert_array_equal(valid_counts(p2f).cpu().numpy(), (case["p2f"] >= 0).sum(-1))
 

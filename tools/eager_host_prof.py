@@ -22,7 +22,7 @@ def main():
     dev = torch.device("cuda:0")
     pa.native_library()
     wl = bench.Workload(dev)
-    step = bench.build_step(wl, 1, "eager", dev)
+    step = bench.build_step(wl, 1, "eager", dev, None)
     for _ in range(10):
         step()
     torch.cuda.synchronize()
