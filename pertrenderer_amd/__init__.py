@@ -8,6 +8,7 @@ gfx950 (libpertrender.so, C ABI in include/pertrender.h).
 """
 from . import _native
 from .blend import perturbed_aggregate, perturbed_blend, perturbed_blend_vertex, perturbed_heaviside, soft_blend
+from .multidevice import sample_devices, set_sample_devices
 from .noise import Noise, get_noise_source, set_noise_source
 from .random_rasterizer import (RandomPhongShader, RandomSimpleShader, SimpleShader, SoftSimpleShader,
                                 smooth_rgb_blend)

@@ -181,11 +181,18 @@ def check(code, what):
 
 
 def ptr(t):
-    return None if t is None else C.c_void_p(t.data_ptr())
+    """Device address of `t` (None for a missing optional buffer).  A plain int: ctypes takes it
+    for c_void_p fields and arguments without a wrapper object per pointer."""
+    return None if t is None else t.data_ptr()
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def stream_of(t):
     """The current torch stream of `t`'s device, as the hipStream_t handle."""
+    if _raw_stream is not None:
+        return C.c_void_p(_raw_stream(t.device.index if t.device.index is not None else torch.cuda.current_device()))
     return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 

@@ -1,0 +1,151 @@
+"""In-process multi-device Monte-Carlo sample sharding (SURVEY.md §5 "Distributed comm
+backend", §8(e) exact mode) for callers that stay one process, as eval.py does (it pins
+``cuda:0``, experiments/eval.py:112-114).
+
+    import pertrenderer_amd as pa
+    pa.set_sample_devices(["cuda:0", "cuda:1", ...])   # eval.py unchanged otherwise
+
+Every ``smooth_rgb_blend`` of a native Monte-Carlo pair (GaussianRast / ArctanRast /
+*_wovr x GaussianAgg / CauchyAgg / *_wovr) then splits its Sr rast and Sa agg samples over
+the devices (``parallel.sample_shard``: global sample indices, one Philox key per operator as
+on one device) and assembles the full-S estimator with in-process collectives:
+
+  forward : fragments broadcast to the devices; each device's perturbed Heaviside counts
+            over its rast shard are sum-reduced to the primary (P = sum_i n_i/Sr * P_i) and
+            P is broadcast back; each device's perturbed argmax counts over its agg shard are
+            sum-reduced (W); the colour mix and alpha on the primary (random_rasterizer.py:47-54);
+  backward: the adjoints of the same collectives (broadcast <-> sum-reduce), so d dists,
+            d zbuf and the smoothing scalars' gradients are the full-S ones.
+
+P and W are exact counts, so the image is the one-device image bit for bit; gradients differ
+only by the summation order of the shards' partials.  The collectives are
+``torch.cuda.comm`` broadcast / reduce_add, i.e. RCCL (ncclCommInitAll) over xGMI when the
+devices are distinct GPUs; logical shards on one device (tests, one-GPU boxes) copy instead.
+This is the north star's sample partition without torchrun; the torchrun paths
+(``parallel.py``, bench.py) remain the measured multi-GPU configuration.
+"""
+import torch
+import torch.cuda.comm as _comm
+
+from . import _native as nat
+from . import noise as noise_mod
+from .noise import Noise
+from .parallel import sample_shard
+
+_DEVICES = None
+
+
+def set_sample_devices(devices):
+    """Shard every native Monte-Carlo blend's samples over `devices` (None or one device: off).
+    The first device is the primary: fragments, colours and the image live there."""
+    global _DEVICES
+    if devices is None:
+        _DEVICES = None
+        return
+    devs = [torch.device(d) for d in devices]
+    if any(d.type != "cuda" for d in devs):
+        raise ValueError("sample devices must be ROCm devices")
+    devs = [torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device()) for d in devs]
+    _DEVICES = devs if len(devs) > 1 else None
+
+
+def sample_devices():
+    return _DEVICES
+
+
+def _distinct(devs):
+    return len(set(devs)) == len(devs)
+
+
+def _broadcast(x, devices):
+    if len(devices) > 1 and _distinct(devices) and x.device in devices:
+        src = devices.index(x.device)
+        order = [devices[src]] + [d for i, d in enumerate(devices) if i != src]
+        outs = _comm.broadcast(x.contiguous(), devices=order)  # RCCL broadcast
+        back = dict(zip(order, outs))
+        return [back[d] for d in devices]
+    return [x.view_as(x) if d == x.device else x.to(d) for d in devices]  # distinct outputs
+
+
+def _reduce_add(xs, dst):
+    devs = [x.device for x in xs]
+    if len(devs) > 1 and _distinct(devs) and dst in devs:
+        return _comm.reduce_add([x.contiguous() for x in xs], destination=dst)  # RCCL reduce
+    out = xs[0].to(dst, copy=True)
+    for x in xs[1:]:
+        out.add_(x.to(dst))
+    return out
+
+
+class _Broadcast(torch.autograd.Function):
+    """x -> one copy per device; backward: the sum of the copies' gradients on x's device."""
+
+    @staticmethod
+    def forward(ctx, devices, x):
+        ctx.src = x.device
+        return tuple(_broadcast(x.detach(), devices))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        gs = [g for g in gs if g is not None]
+        return None, (_reduce_add(gs, ctx.src) if gs else None)
+
+
+class _WeightedReduce(torch.autograd.Function):
+    """(x_i on device i) -> sum_i w_i x_i on dst; backward: w_i * g broadcast to device i."""
+
+    @staticmethod
+    def forward(ctx, dst, weights, *xs):
+        ctx.devs, ctx.weights = [x.device for x in xs], weights
+        return _reduce_add([x.detach() * w for x, w in zip(xs, weights)], dst)
+
+    @staticmethod
+    def backward(ctx, g):
+        gs = _broadcast(g.detach(), ctx.devs)
+        return (None, None) + tuple(gi * w for gi, w in zip(gs, ctx.weights))
+
+
+def sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_samples_rast, nb_samples_agg,
+                  devices=None, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0, zfar=100.0, fixed_noise=False,
+                  rast_kind="gaussian", rast_vr=True, agg_kind="gaussian", agg_vr=True):
+    """smooth_rgb_blend (random_rasterizer.py:34-56) of a native Monte-Carlo pair with its samples
+    split over `devices` (default: set_sample_devices) -- see the module docstring."""
+    from .blend import perturbed_aggregate, perturbed_heaviside
+    from .random_rasterizer import _background_tensor
+    from .variants import prod_last
+    devices = [torch.device(d) for d in (devices or _DEVICES or [pix_to_face.device])]
+    primary = pix_to_face.device
+    if devices[0] != primary:
+        raise ValueError(f"the first sample device ({devices[0]}) must hold the fragments ({primary})")
+    shape = tuple(pix_to_face.shape)
+    N, H, W, K = shape
+    # one key per operator, drawn as the one-device path draws them (rast, then agg)
+    nr = noise_mod.draw_rast(shape, nb_samples_rast, primary, rast_kind)
+    na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, primary, fixed_noise, agg_kind)
+    if nr.mode != nat.PR_NOISE_PHILOX or na.mode != nat.PR_NOISE_PHILOX or nr.seeds is not None \
+            or na.seeds is not None:
+        raise NotImplementedError("sample sharding over devices needs host-keyed Philox noise (not the "
+                                  "'torch' noise source or a graph-mode DeviceSeed)")
+    n = len(devices)
+    sh_r = [sample_shard(nb_samples_rast, i, n) for i in range(n)]
+    sh_a = [sample_shard(nb_samples_agg, i, n) for i in range(n)]
+    if any(c == 0 for _, c in sh_r + sh_a):
+        raise ValueError(f"{n} sample devices need >= {n} rast and agg samples "
+                         f"(Sr={nb_samples_rast}, Sa={nb_samples_agg})")
+    mask = pix_to_face >= 0
+    m_b = _broadcast(mask, devices)
+    d_b = _Broadcast.apply(devices, dists)
+    z_b = _Broadcast.apply(devices, zbuf)
+    P_i = [perturbed_heaviside(d_b[i], sigma, sh_r[i][1],
+                               noise=Noise.philox(seed_r=nr.seed_r, offset_r=nr.offset_r + sh_r[i][0]),
+                               kind=rast_kind, variance_reduction=rast_vr) * m_b[i] for i in range(n)]
+    P = _WeightedReduce.apply(primary, [c / nb_samples_rast for _, c in sh_r], *P_i)
+    P_b = _Broadcast.apply(devices, P)
+    W_i = [perturbed_aggregate(z_b[i], zfar, znear, P_b[i], m_b[i], gamma, alpha, sh_a[i][1], eps=eps,
+                               noise=Noise.philox(seed_a=na.seed_a, offset_a=na.offset_a + sh_a[i][0]),
+                               kind=agg_kind, variance_reduction=agg_vr) for i in range(n)]
+    Wt = _WeightedReduce.apply(primary, [c / nb_samples_agg for _, c in sh_a], *W_i)
+    bg = _background_tensor(background, primary)
+    rgb = (Wt[..., :K, None] * colors).sum(dim=-2) + Wt[..., K:K + 1] * bg  # random_rasterizer.py:50-53
+    a = 1.0 - prod_last(1.0 - P)  # :48, :54
+    return torch.cat([rgb, a[..., None]], dim=-1)

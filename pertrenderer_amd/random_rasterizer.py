@@ -15,6 +15,8 @@ import torch
 import torch.nn as nn
 
 from . import blend as _blend
+from . import multidevice as _multidevice
+from . import noise as _noise
 from . import variants as _variants
 from .renderer.cameras import OpenGLPerspectiveCameras, look_at_view_transform
 from .renderer.blending import hard_rgb_blend, sigmoid_alpha_blend, softmax_rgb_blend  # noqa: F401
@@ -57,6 +59,13 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
     device = fragments.pix_to_face.device
     background = blend_params.background_color
     if _is_fusable(smoothrast, smoothagg, fragments):
+        if _multidevice.sample_devices() is not None and _noise.get_noise_source() == "philox":
+            # samples split over the devices of set_sample_devices (in-process RCCL collectives)
+            return _multidevice.sharded_blend(
+                colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
+                smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
+                eps=smoothagg.eps, background=background, znear=znear, zfar=zfar,
+                fixed_noise=smoothagg.fixed_noise, **_variant_kw(smoothrast, smoothagg))
         return _blend.perturbed_blend(
             colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
             smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
@@ -180,7 +189,8 @@ class RandomSimpleShader(_RandomShaderBase):
         blend_params = kwargs.get("blend_params", self.blend_params)
         znear, zfar = _planes_from(cameras, kwargs)
         vc = _vertex_colors(meshes)
-        if vc is not None and _is_fusable(self.smoothrast, self.smoothagg, fragments):
+        if vc is not None and _is_fusable(self.smoothrast, self.smoothagg, fragments) \
+                and _multidevice.sample_devices() is None:
             # TexturesVertex sampling fused into the blend (no (N,H,W,K,3) texel tensor)
             sr, sa = self.smoothrast, self.smoothagg
             return _blend.perturbed_blend_vertex(
