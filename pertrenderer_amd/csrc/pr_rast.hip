@@ -998,56 +998,8 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     const int ncols = min(TW, W - col0), nrows = min(TH, H - row0);
     const int per_row = ncols * K, total = nrows * per_row;
     const float inv_row = 1.f / (float)per_row, inv_k = 1.f / (float)K;
-    // vector stores: a lane writes 4 consecutive slots of a row with 16-B stores (2 for
-    // pix_to_face, 1 each for zbuf / dists, 3 for bary) instead of 6 narrow stores per slot.
-    // Needs rows of whole 16-B groups (per_row and W*K multiples of 4) and aligned buffers.
-    const bool vec = FRAG && (per_row & 3) == 0 && ((int64_t)W * K) % 4 == 0 &&
-                     ((reinterpret_cast<uintptr_t>(a.pix_to_face) | reinterpret_cast<uintptr_t>(a.zbuf) |
-                       reinterpret_cast<uintptr_t>(a.dists) | reinterpret_cast<uintptr_t>(a.bary)) & 15) == 0;
-    if (vec) {
-      for (int base = 0; base < total; base += 256) {
-        const int i0 = base + lane * 4;  // a multiple of 4: the group never straddles a row
-        if (i0 >= total) break;
-        int rem;
-        const int r = divmod_small(i0, per_row, inv_row, rem);
-        const int64_t o = (((int64_t)n * H + row0 + r) * W + col0) * K + rem;
-        int pf[4];
-        float zz[4], dd[4], bb[12];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int kk;
-          const int c = divmod_small(rem + j, K, inv_k, kk);
-          const int tl = r * TW + c;
-          const float2 e = q[kk * TP + tl];
-          const bool valid = kk < qsz[tl];
-          const int fid = __float_as_int(e.y);
-          pf[j] = valid ? fid : -1;
-          zz[j] = valid ? e.x : -1.f;
-          float bc[3] = {-1.f, -1.f, -1.f}, dist = -1.f;
-          if (valid) {
-            const V2 pp{ndc(W - 1 - (col0 + c), W, H), ndc(H - 1 - (row0 + r), H, W)};
-            const FaceRec rec = faces[fid];
-            float pz, d;
-            bool inside;
-            face_eval<PERSP, CLIP>(rec, pp, bc, pz, inside, d);
-            dist = inside ? -d : d;
-          }
-          dd[j] = dist;
-          bb[3 * j] = bc[0]; bb[3 * j + 1] = bc[1]; bb[3 * j + 2] = bc[2];
-        }
-        int4* p2 = reinterpret_cast<int4*>(a.pix_to_face + o);  // int64 = (lo, hi = sign)
-        p2[0] = make_int4(pf[0], pf[0] >> 31, pf[1], pf[1] >> 31);
-        p2[1] = make_int4(pf[2], pf[2] >> 31, pf[3], pf[3] >> 31);
-        *reinterpret_cast<float4*>(a.zbuf + o) = make_float4(zz[0], zz[1], zz[2], zz[3]);
-        *reinterpret_cast<float4*>(a.dists + o) = make_float4(dd[0], dd[1], dd[2], dd[3]);
-        float4* b4 = reinterpret_cast<float4*>(a.bary + o * 3);
-        b4[0] = make_float4(bb[0], bb[1], bb[2], bb[3]);
-        b4[1] = make_float4(bb[4], bb[5], bb[6], bb[7]);
-        b4[2] = make_float4(bb[8], bb[9], bb[10], bb[11]);
-      }
-    }
     constexpr int U = 4;
-    for (int base = 0; !vec && base < total; base += 64 * U) {
+    for (int base = 0; base < total; base += 64 * U) {
       float2 e[U];
       int sz[U], kk[U], cc[U], rr[U];
       int64_t o[U];
