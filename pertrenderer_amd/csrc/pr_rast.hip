@@ -409,8 +409,8 @@ template <int SL> struct RastCfg {
 #define PR_RAST_G4 2
 #endif
   static constexpr int G = SL == 1 ? 4 : (SL >= 4 ? PR_RAST_G4 : 2);
-#ifndef PR_RAST_CH4  // sweeps: 16 measured equal (84 vs 86 us, noise)
-#define PR_RAST_CH4 32
+#ifndef PR_RAST_CH4  // sweeps (r2): 16 vs 32 equal at cfg 2 (80.6 vs 81.0 us), 11 % faster at cfg 4
+#define PR_RAST_CH4 16  // (5.26 vs 5.94 ms: less LDS per wave, more waves resident at K = 150)
 #endif
   static constexpr int CH = SL >= 4 ? PR_RAST_CH4 : 64;
   static_assert(CAP <= 8 * 64, "suffix-min pass holds CAP / 64 <= 8 entries per lane");
@@ -1651,7 +1651,10 @@ static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2
   // with the two-stage face test (107 us vs 118-123 at 2 and 157 at 1); PR_RAST_SLICES=1|2|4
   // overrides (sweeps).  FRAG: barycentrics / distances written by the rasterizer itself
   // (no second pass over pix_to_face); PR_RAST_FRAG=0 selects the separate pass.
-  int sl = 4;
+  // Deep queues (K > 128: more than 16 KB of 4x4-tile queue per wave) take 8 slices on 4x2 tiles,
+  // half the queue LDS per wave, so more waves stay resident: cfg 4 (K = 150) 5.27 -> 5.01 ms;
+  // at cfg 3 (K = 100) 4 slices stay faster (1.04 vs 1.14 ms).
+  int sl = (int64_t)a.K * 16 * 8 > 16 * 1024 ? 8 : 4;
   if (const char* e = getenv("PR_RAST_SLICES")) {
     const int v = atoi(e);
     if (v == 1 || v == 2 || v == 4 || v == 8) sl = v;
