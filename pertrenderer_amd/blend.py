@@ -123,8 +123,15 @@ def _merge(nr, na):
 
 
 def _scalar_grads(gs, needs, refs):
-    return [gs[i].to(dtype=ref.dtype) if (need and torch.is_tensor(ref)) else None
-            for i, (need, ref) in enumerate(zip(needs, refs))]
+    """The smoothing scalars' gradients from the kernel's (3,) device buffer.  For the
+    reference's CPU 0-d leaves the three values come to the host in ONE copy (autograd would
+    otherwise copy each 0-d device grad separately: three host synchronisations per backward)."""
+    want = [need and torch.is_tensor(ref) for need, ref in zip(needs, refs)]
+    if any(w and ref.device.type == "cpu" for w, ref in zip(want, refs)) and gs.is_cuda:
+        host = gs.detach().to("cpu")
+        return [(host[i] if ref.device.type == "cpu" else gs[i]).to(dtype=ref.dtype) if w else None
+                for i, (w, ref) in enumerate(zip(want, refs))]
+    return [gs[i].to(dtype=ref.dtype) if w else None for i, (w, ref) in enumerate(zip(want, refs))]
 
 
 def _counts_for(pix_to_face):
