@@ -377,6 +377,52 @@ def run_problem(scene, problem, noise_type, sigma, gamma, nb_mc, pert, niter, ad
     return out
 
 
+def compare_runtime(scene, num_prob, noise_type, smoothing_list, mc_list, pert=20.0, niter=800, adapt_reg=True,
+                    adapt_params=(1.1, 1.1), lr_list=(5e-2,), mode="eager", out=None):
+    """eval.py compare_runtime (experiments/eval.py:506-574) on the cube scene (ShapeNet is not
+    available here; eval.py's pose benchmark uses the same cube): for every (lr, (sigma, gamma),
+    MC) setting and test problem, the wall time of one whole optimize_pose run and the peak
+    device memory (torch.cuda.max_memory_allocated, MB) per noise type.  Returns (mean_runtimes,
+    mean_memory, params) shaped as eval.py's runtimes.txt / memory.txt: {noise: [[per problem]
+    per setting]}; writes them (results.write_runtime_results) when `out` is given."""
+    device = scene.device
+    problems = make_problems(scene, num_prob, noise_type, pert)
+    mean_runtimes = {nt: [] for nt in noise_type}
+    mean_memory = {nt: [] for nt in noise_type}
+    params = {"lr-smoothing-MC": [], "lr": [], "sigma": [], "gamma": [], "MC": [], "adapt_params": []}
+    for lr in lr_list:
+        for sigma, gamma in smoothing_list:
+            for nb_mc in mc_list:
+                runtimes = {nt: [] for nt in noise_type}
+                memory = {nt: [] for nt in noise_type}
+                for target_rgb, R_true, log_rot_init in problems:
+                    _, renderers = init_renderers(scene, R_true, pert_init_intensity=pert, sigma=sigma, gamma=gamma,
+                                                  nb_samples=nb_mc, noise_type=noise_type)
+                    for nt, renderer in zip(noise_type, renderers):
+                        torch.cuda.synchronize(device)
+                        torch.cuda.reset_peak_memory_stats(device)  # eval.py:548
+                        t0 = time.perf_counter()
+                        run = optimize_pose_graph if mode == "graph" else optimize_pose
+                        run(scene, log_rot_init, renderer, target_rgb, lr_init=lr, Niter=niter, adapt_reg=adapt_reg,
+                            adapt_params=adapt_params)
+                        torch.cuda.synchronize(device)
+                        runtimes[nt].append(time.perf_counter() - t0)
+                        memory[nt].append(torch.cuda.max_memory_allocated(device) * 1e-6)  # MB, eval.py:555
+                for nt in noise_type:
+                    mean_runtimes[nt].append(runtimes[nt])
+                    mean_memory[nt].append(memory[nt])
+                params["lr-smoothing-MC"].append((lr, sigma, gamma, nb_mc))
+                params["lr"].append(lr)
+                params["sigma"].append(sigma)
+                params["gamma"].append(gamma)
+                params["MC"].append(nb_mc)
+                params["adapt_params"].append(adapt_params)
+    if out:
+        from . import results as res
+        res.write_runtime_results(out, mean_runtimes, mean_memory)
+    return mean_runtimes, mean_memory, params
+
+
 def tables(per_problem, noise_type, params, exp_setup):
     """compare_pose_opt's json tables (eval.py:632-661) for one parameter setting."""
     mean_errors, var_errors, init_errors, final_errors = {}, {}, {}, {}
@@ -405,7 +451,21 @@ def main(argv=None):
     ap.add_argument("-s", "--seed", type=int, default=1)
     ap.add_argument("--mode", choices=["eager", "graph"], default="eager")
     ap.add_argument("--out", default=None, help="directory for eval.py's tables + summary.json")
+    ap.add_argument("--runtime", action="store_true",
+                    help="eval.py compare_runtime instead: runtimes.txt / memory.txt per MC setting")
+    ap.add_argument("-mcl", "--mc-list", type=int, nargs="+", default=None, help="--runtime: MC settings")
     args = ap.parse_args(argv)
+    if args.runtime:
+        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(device)
+        torch.manual_seed(args.seed)
+        scene = Scene(device, args.image_size)
+        rt, mem, params = compare_runtime(scene, args.num_prob, list(args.smoothing_noise), [tuple(args.smoothing)],
+                                          args.mc_list or [args.mc_samples], pert=args.initial_perturbation,
+                                          niter=args.num_iterations, adapt_reg=bool(args.adaptive_regularization),
+                                          mode=args.mode, out=args.out)
+        print(json.dumps({"runtimes": rt, "memory_mb": mem, "params": params}), flush=True)
+        return 0
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

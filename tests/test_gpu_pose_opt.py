@@ -54,3 +54,22 @@ def test_graph_and_eager_runs_compare(problems):
         runs.append(pose_opt.tables(per, NOISE, dict(niter=60), dict(mode=mode)))
     cmp = compare_pose_results(runs[0], runs[1])
     assert set(NOISE) <= set(cmp)
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+def test_compare_runtime_tables(tmp_path, device, mode):
+    """eval.py compare_runtime (:506-574) mirror: per (lr, smoothing, MC) setting and problem, the
+    wall time of a whole optimize_pose run and its peak device memory, written as runtimes.txt /
+    memory.txt with the reference's {noise: [[per problem] per setting]} layout."""
+    torch.manual_seed(2)
+    scene = pose_opt.Scene(device, 64)
+    rt, mem, params = pose_opt.compare_runtime(scene, 2, list(NOISE), [(1e-3, 1e-2)], [4, 8], niter=12,
+                                               mode=mode, out=str(tmp_path))
+    for table in (rt, mem):
+        assert set(table) == set(NOISE)
+        for nt in NOISE:
+            assert len(table[nt]) == 2 and all(len(per) == 2 for per in table[nt])
+            assert all(v > 0 for per in table[nt] for v in per)
+    assert params["MC"] == [4, 8] and params["lr-smoothing-MC"] == [(5e-2, 1e-3, 1e-2, 4), (5e-2, 1e-3, 1e-2, 8)]
+    on_disk = json.load(open(tmp_path / "runtimes.txt")), json.load(open(tmp_path / "memory.txt"))
+    assert on_disk[0] == rt and on_disk[1] == mem
