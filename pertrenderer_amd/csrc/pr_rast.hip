@@ -415,6 +415,9 @@ template <int SL> struct RastCfg {
   static constexpr int CH = SL >= 4 ? PR_RAST_CH4 : 64;
   static_assert(CAP <= 8 * 64, "suffix-min pass holds CAP / 64 <= 8 entries per lane");
 };
+#ifndef PR_RAST_QPAD  // queue row padding in entries (sweep knob)
+#define PR_RAST_QPAD 0
+#endif
 #ifndef PR_RAST_MERGE  // 0: candidates landing inside a queue are inserted slice by slice (r1 path)
 #define PR_RAST_MERGE 1
 #endif
@@ -501,7 +504,7 @@ PR_DEV bool ekey_less(float2 x, float2 y) { return key_less(x.x, __float_as_int(
 template <int SL>
 size_t rast_fwd_lds_sl(int K) {
   using C = RastCfg<SL>;
-  return C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL) * 8 + (size_t)C::CAP * 12 + 64 * 4 + C::CH * 8 + 16;
+  return C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL + PR_RAST_QPAD) * 8 + (size_t)C::CAP * 12 + 64 * 4 + C::CH * 8 + 16;
 }
 
 size_t rast_fwd_lds(int K, int SL) {
@@ -588,12 +591,13 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
                                                       const uint2* __restrict__ fbox, int ring, BinGrid bins) {
   constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
   constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
+  constexpr int QS = TP + PR_RAST_QPAD;  // queue row stride (entries): padding spreads a pixel's rows over banks
   extern __shared__ float smem[];
   const int K = a.K;
   const int lane = threadIdx.x, pix = lane / SL, slice = lane % SL;
   FaceRec* lrec = reinterpret_cast<FaceRec*>(smem);                // [CH] staged chunk
-  float2* q = reinterpret_cast<float2*>(lrec + CH);                 // [K][TP] per-pixel queues
-  int* lfid = reinterpret_cast<int*>(q + (size_t)K * TP);           // [kCap] tile face list (cull order)
+  float2* q = reinterpret_cast<float2*>(lrec + CH);                 // [K][QS] per-pixel queues
+  int* lfid = reinterpret_cast<int*>(q + (size_t)K * QS);           // [kCap] tile face list (cull order)
   float* lkey = reinterpret_cast<float*>(lfid + kCap);              // [kCap] sort key, then
   float* lsuf = lkey;                                               //   suffix min of z_min
   int* lidx = reinterpret_cast<int*>(lkey + kCap);                  // [kCap] sorted -> cull order
@@ -864,7 +868,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
                   int lo = 0, hi = qs - 1;
                   while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
-                    const float2 e = q[mid * TP + pix];
+                    const float2 e = q[mid * QS + pix];
                     if (key_less(e.x, __float_as_int(e.y), pz, fid)) lo = mid + 1;
                     else hi = mid;
                   }
@@ -875,8 +879,8 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
                 for (int r = 1; r < SL; ++r) pmin = min(pmin, quad_rot<SL>(pmin, r));
                 for (int i = qs - 1 - slice; i >= pmin; i -= 2 * SL) {
                   const bool two = i - SL >= pmin;
-                  const float2 e0 = q[i * TP + pix];
-                  const float2 e1 = q[(two ? i - SL : i) * TP + pix];
+                  const float2 e0 = q[i * QS + pix];
+                  const float2 e1 = q[(two ? i - SL : i) * QS + pix];
                   int s0 = enter && key_less(pz, fid, e0.x, __float_as_int(e0.y)) ? 1 : 0;
                   int s1 = enter && key_less(pz, fid, e1.x, __float_as_int(e1.y)) ? 1 : 0;
 #pragma unroll
@@ -884,14 +888,14 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
                     s0 += oe[r] && key_less(oz[r], of[r], e0.x, __float_as_int(e0.y)) ? 1 : 0;
                     s1 += oe[r] && key_less(oz[r], of[r], e1.x, __float_as_int(e1.y)) ? 1 : 0;
                   }
-                  if (i + s0 < K) q[(i + s0) * TP + pix] = e0;
-                  if (two && i - SL + s1 < K) q[(i - SL + s1) * TP + pix] = e1;
+                  if (i + s0 < K) q[(i + s0) * QS + pix] = e0;
+                  if (two && i - SL + s1 < K) q[(i - SL + s1) * QS + pix] = e1;
                 }
                 const int pos = below + rank;
-                if (enter && pos < K) q[pos * TP + pix] = make_float2(pz, __int_as_float(fid));
+                if (enter && pos < K) q[pos * QS + pix] = make_float2(pz, __int_as_float(fid));
                 qs = min(qs + nq, K);
                 if (qs > 0) {
-                  const float2 last = q[(qs - 1) * TP + pix];
+                  const float2 last = q[(qs - 1) * QS + pix];
                   qlast_z = last.x;
                   qlast_f = __float_as_int(last.y);
                 }
@@ -903,7 +907,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
               }
 #endif
               const int nkept = min(nq, K - qs);  // the largest ones drop off a full queue
-              if (enter && rank < nkept) q[(qs + rank) * TP + pix] = make_float2(pz, __int_as_float(fid));
+              if (enter && rank < nkept) q[(qs + rank) * QS + pix] = make_float2(pz, __int_as_float(fid));
               if (nkept > 0) {  // new last key: the entered one of rank nkept - 1
                 const bool last = enter && rank == nkept - 1;
                 float lz = pz;
@@ -934,7 +938,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
               if (enter) {
                 if (qs == 0 || key_less(qlast_z, qlast_f, pz, fid)) {
                   // append (the common case: faces arrive roughly in depth order)
-                  q[qs * TP + pix] = make_float2(pz, __int_as_float(fid));
+                  q[qs * QS + pix] = make_float2(pz, __int_as_float(fid));
                   ++qs;
                   qlast_z = pz;
                   qlast_f = fid;
@@ -952,20 +956,20 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
                   while (pos > 0) {
                     float2 e[4];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) e[i] = q[max(pos - 1 - i, 0) * TP + pix];
+                    for (int i = 0; i < 4; ++i) e[i] = q[max(pos - 1 - i, 0) * QS + pix];
                     int sh = 0;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                       if (sh == i && pos - 1 - i >= 0 && key_less(pz, fid, e[i].x, __float_as_int(e[i].y))) {
-                        q[(pos - i) * TP + pix] = e[i];
+                        q[(pos - i) * QS + pix] = e[i];
                         sh = i + 1;
                       }
                     }
                     pos -= sh;
                     if (sh < 4) break;
                   }
-                  q[pos * TP + pix] = make_float2(pz, __int_as_float(fid));
-                  const float2 last = q[(qs - 1) * TP + pix];
+                  q[pos * QS + pix] = make_float2(pz, __int_as_float(fid));
+                  const float2 last = q[(qs - 1) * QS + pix];
                   qlast_z = last.x;
                   qlast_f = __float_as_int(last.y);
                 }
@@ -1011,7 +1015,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
         cc[u] = divmod_small(rem, K, inv_k, kk[u]);
         const int tl = rr[u] * TW + cc[u];
         o[u] = (((int64_t)n * H + row0 + rr[u]) * W + col0) * K + rem;
-        e[u] = q[kk[u] * TP + tl];  // read with the size (stale beyond it, unused)
+        e[u] = q[kk[u] * QS + tl];  // read with the size (stale beyond it, unused)
         sz[u] = qsz[tl];
       }
 #pragma unroll
@@ -1686,9 +1690,12 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
       return set_error(PR_ERR_HIP, "rast_bwd: memset failed");
   }
   // rows per 8-wide workgroup tile: 2 measured fastest on the bench frame (more, smaller
-  // workgroups hide the per-round latency chain); PR_RAST_BWD_ROWS=4|8 overrides (sweeps)
+  // workgroups hide the per-round latency chain), 4 on large batches (>= 2^18 pixels: cfg 3
+  // 0.53 -> 0.45 ms, cfg 4 2.01 -> 1.71 ms); PR_RAST_BWD_ROWS=1|2|4|8 overrides (sweeps)
   const char* er = getenv("PR_RAST_BWD_ROWS");
-  const int rows = er && (atoi(er) == 1 || atoi(er) == 4 || atoi(er) == 8) ? atoi(er) : 2;
+  const int64_t npix = (int64_t)a.N * a.H * a.W;
+  const int rows = er && (atoi(er) == 1 || atoi(er) == 2 || atoi(er) == 4 || atoi(er) == 8) ? atoi(er)
+                                                                                            : (npix >= (1 << 18) ? 4 : 2);
   dim3 grid((a.W + kBwdTile - 1) / kBwdTile, (a.H + rows - 1) / rows, a.N);
   // tile rows dispatched centre-out (PR_RAST_ORDER bit 1; 0: row-major)
   static const int order = (getenv("PR_RAST_ORDER") ? atoi(getenv("PR_RAST_ORDER")) : 3) >> 1 & 1;
