@@ -60,7 +60,7 @@ def bin_params(bin_size, max_faces_per_bin, H, W, F, N=1):
     PR_RAST_BINS=0 forces the naive path, PR_RAST_BINS=1 resolves None as PyTorch3D does (bins of
     8 / 16 / 32 / 64 pixels up to 64 / 256 / 512 / 1024-pixel images)."""
     env = os.environ.get("PR_RAST_BINS")
-    if env == "0" or (bin_size is None and env != "1"):
+    if env == "0" or (bin_size is None and env != "1") or (bin_size is not None and bin_size <= 0):
         return 0, 0
     if bin_size is None:
         size = max(H, W)

@@ -77,3 +77,42 @@ def test_ops_refuse_cpu_tensors():
     from pertrenderer_amd import perturbed_heaviside
     with pytest.raises(nat.NativeError):
         perturbed_heaviside(torch.zeros(1, 2, 2, 3), torch.tensor(1e-3), 4)
+
+
+def test_rast_workspace_counts_the_bin_lists():
+    """pr_rast_fwd_workspace_size (host-only): face records + fp16 boxes, plus with bin_size > 0
+    the bin counters and lists: N * ceil(H/b) * ceil(W/b) * (1 + cap) ints, b = bin_size rounded
+    up to a multiple of 8, cap = min(max_faces_per_bin or max(10000, F/5), F)."""
+    lib = nat.load()
+    a = nat.PRRastArgs()
+    a.F, a.N, a.H, a.W, a.K = 1000, 2, 256, 200, 8
+    base = lib.pr_rast_fwd_workspace_size(a)
+    assert base == 1000 * (96 + 8)
+    a.bin_size, a.max_faces_per_bin = 16, 0
+    assert lib.pr_rast_fwd_workspace_size(a) == base + 2 * 16 * 13 * 4 * (1 + 1000)
+    a.bin_size, a.max_faces_per_bin = 12, 300  # 12 -> 16-pixel bins, cap 300
+    assert lib.pr_rast_fwd_workspace_size(a) == base + 2 * 16 * 13 * 4 * (1 + 300)
+    a.bin_size = 0
+    assert lib.pr_rast_fwd_workspace_size(a) == base
+
+
+def test_bin_params_resolve_like_pytorch3d():
+    from pertrenderer_amd.renderer.rasterizer import bin_params
+    os.environ.pop("PR_RAST_BINS", None)
+    assert bin_params(None, None, 256, 256, 5000) == (0, 0)  # None: the naive cull (measured faster)
+    assert bin_params(0, 100, 256, 256, 5000) == (0, 0)
+    assert bin_params(32, None, 512, 512, 5000) == (32, 10000)
+    assert bin_params(8, 77, 64, 64, 5000) == (8, 77)
+    os.environ["PR_RAST_BINS"] = "1"
+    try:
+        assert bin_params(None, None, 64, 64, 100000) == (8, 20000)
+        assert bin_params(None, None, 256, 256, 10) == (16, 10000)
+        assert bin_params(None, None, 512, 512, 10) == (32, 10000)
+        assert bin_params(None, None, 1024, 1024, 10) == (64, 10000)
+    finally:
+        os.environ.pop("PR_RAST_BINS")
+    os.environ["PR_RAST_BINS"] = "0"
+    try:
+        assert bin_params(16, 50, 256, 256, 10) == (0, 0)
+    finally:
+        os.environ.pop("PR_RAST_BINS")
