@@ -1441,8 +1441,11 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   while (lpp > 8 && lpp * PB > kThreads) lpp >>= 1;
   g.lpp = lpp;
   g.lsh = 31 - __builtin_clz(g.lpp);
-  // centre-out block order (PR_BLEND_ORDER bit 0: forward, bit 1: backward; 0 = linear)
-  static const int order = getenv("PR_BLEND_ORDER") ? atoi(getenv("PR_BLEND_ORDER")) : 1;
+  // centre-out block order (PR_BLEND_ORDER bit 0: forward, bit 1: backward; 0 = linear).
+  // Default: the forward of a single frame only (cfg 2); on batches linear order is faster
+  // (cfg 4 blend_fwd 5.16 -> 4.72 ms, cfg 3 equal), and the backward is linear everywhere.
+  static const int order_env = getenv("PR_BLEND_ORDER") ? atoi(getenv("PR_BLEND_ORDER")) : -1;
+  const int order = order_env >= 0 ? order_env : (p.N == 1 ? 1 : 0);
   g.bpi = (order >> (bwd ? 1 : 0) & 1) && g.HW % PB == 0 ? g.HW / PB : 0;
   static const int tail = getenv("PR_BLEND_TAIL") ? atoi(getenv("PR_BLEND_TAIL")) : 1;
   g.tail = tail;
