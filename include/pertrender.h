@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 12
+#define PR_ABI_VERSION 13
 
 /* error codes */
 #define PR_OK 0
@@ -277,6 +277,26 @@ typedef struct PRShadeArgs {
 
 int pr_shade_fwd(const PRShadeArgs* args, void* stream);
 int pr_shade_bwd(const PRShadeArgs* args, void* stream);
+
+/* Area-weighted vertex normals of a packed mesh: PyTorch3D Meshes.verts_normals_packed (the
+ * normals phong_shading interpolates for RandomPhongShader, random_rasterizer.py:60-116 via
+ * eval.py's renderer).  Forward: normals = normalize(sum over each vertex's face corners of
+ * cross(v_next - v_c, v_prev - v_c)), F.normalize's max(||n||, 1e-6); `raw` (nullable) keeps
+ * the unnormalised sums for the backward.  Backward: grad_verts (overwritten) from
+ * grad_normals, through grad_raw (caller scratch, (V,3)). */
+typedef struct PRNormalsArgs {
+  const float* verts;          /* (V,3) */
+  const int64_t* faces;        /* (F,3) */
+  int64_t V, F;
+  float* normals;              /* fwd out (V,3) */
+  float* raw;                  /* fwd out (V,3), nullable; bwd in */
+  const float* grad_normals;   /* bwd in (V,3) */
+  float* grad_raw;             /* bwd scratch (V,3) */
+  float* grad_verts;           /* bwd out (V,3), overwritten */
+} PRNormalsArgs;
+
+int pr_vert_normals_fwd(const PRNormalsArgs* args, void* stream);
+int pr_vert_normals_bwd(const PRNormalsArgs* args, void* stream);
 
 /* the backward's gradient accumulator was zeroed by the forward (pr_project_rast_fwd) */
 #define PR_GRAD_PREZEROED 1

@@ -117,6 +117,11 @@ class PRShadeArgs(C.Structure):
                 ("grad_light", _vp), ("grad_camera", _vp)]
 
 
+class PRNormalsArgs(C.Structure):
+    _fields_ = [("verts", _vp), ("faces", _vp), ("V", C.c_int64), ("F", C.c_int64), ("normals", _vp),
+                ("raw", _vp), ("grad_normals", _vp), ("grad_raw", _vp), ("grad_verts", _vp)]
+
+
 # every symbol include/pertrender.h declares, with its argument struct (None = no args)
 EXPORTS = {
     "pr_abi_version": (C.c_int, []),
@@ -144,8 +149,10 @@ EXPORTS = {
     "pr_philox": (C.c_int, [_vp, _vp, C.c_int64, _vp, _vp, _vp, _vp]),
     "pr_shade_fwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
     "pr_shade_bwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
+    "pr_vert_normals_fwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
+    "pr_vert_normals_bwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
 }
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lib = None
 

@@ -14,7 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpertrender.so")
-SOURCES = ["pr_capi.hip", "pr_blend.hip", "pr_rast.hip", "pr_pose.hip", "pr_shade.hip", "pr_softblend.hip"]
+SOURCES = ["pr_capi.hip", "pr_blend.hip", "pr_rast.hip", "pr_pose.hip", "pr_shade.hip", "pr_softblend.hip",
+           "pr_normals.hip"]
 HEADERS = ["pr_common.h", os.path.join("..", "..", "include", "pertrender.h")]
 ARCH = os.environ.get("PR_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-munsafe-fp-atomics",

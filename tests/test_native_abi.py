@@ -49,6 +49,7 @@ STRUCTS = {
     "PRBlendBwdArgs": nat.PRBlendBwdArgs, "PRHeavisideArgs": nat.PRHeavisideArgs,
     "PRRastArgs": nat.PRRastArgs, "PRInterpArgs": nat.PRInterpArgs, "PRProjectArgs": nat.PRProjectArgs,
     "PRSO3Args": nat.PRSO3Args, "PRRotateArgs": nat.PRRotateArgs, "PRShadeArgs": nat.PRShadeArgs,
+    "PRNormalsArgs": nat.PRNormalsArgs,
 }
 
 
