@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _both(verts, faces):
-    out = []
+    out, keep = [], mesh_mod.NATIVE_NORMALS
     for native in (True, False):
         mesh_mod.NATIVE_NORMALS = native
         try:
@@ -25,7 +25,7 @@ def _both(verts, faces):
             (gv,) = torch.autograd.grad((n * g).sum(), v)
             out.append((n.detach(), gv))
         finally:
-            mesh_mod.NATIVE_NORMALS = True
+            mesh_mod.NATIVE_NORMALS = keep
     return out
 
 
