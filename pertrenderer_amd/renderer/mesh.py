@@ -7,6 +7,8 @@ faces, per-mesh face offsets/counts as device tensors).  Meshes derived by
 builds no index tensor and does no host->device copy: it is safe to capture in a
 HIP graph.  ``sample_textures`` runs the native face-attribute interpolation.
 """
+import os
+
 import torch
 
 from . import interp as _interp
@@ -227,7 +229,7 @@ class Meshes:
 
 # Meshes.verts_normals_packed on the native kernels when the mesh is on the GPU (set False for
 # the torch composition above; tests/test_gpu_normals.py compares the two)
-NATIVE_NORMALS = False
+NATIVE_NORMALS = os.environ.get("PR_NATIVE_NORMALS", "0") == "1"
 
 
 class _VertNormalsFn(torch.autograd.Function):
