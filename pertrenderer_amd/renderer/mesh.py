@@ -227,9 +227,9 @@ class Meshes:
         return self.textures.sample_textures(fragments, faces_packed=self.faces_packed())
 
 
-# Meshes.verts_normals_packed on the native kernels when the mesh is on the GPU (set False for
+# Meshes.verts_normals_packed on the native kernels when the mesh is on the GPU (PR_NATIVE_NORMALS=0 or False for
 # the torch composition above; tests/test_gpu_normals.py compares the two)
-NATIVE_NORMALS = os.environ.get("PR_NATIVE_NORMALS", "0") == "1"
+NATIVE_NORMALS = os.environ.get("PR_NATIVE_NORMALS", "1") == "1"
 
 
 class _VertNormalsFn(torch.autograd.Function):
