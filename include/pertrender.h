@@ -30,6 +30,9 @@
  *   pr_interp_fwd / pr_interp_bwd
  *       PyTorch3D interpolate_face_attributes used by Meshes.sample_textures
  *       for TexturesVertex (random_rasterizer.py:170, experiments/eval.py:251).
+ *   pr_vert_normals_fwd / pr_vert_normals_bwd
+ *       PyTorch3D Meshes.verts_normals_packed, the vertex normals phong_shading
+ *       interpolates for RandomPhongShader (random_rasterizer.py:60-116).
  */
 #ifndef PERTRENDER_H_
 #define PERTRENDER_H_
