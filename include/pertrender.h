@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 13
+#define PR_ABI_VERSION 14
 
 /* error codes */
 #define PR_OK 0
@@ -182,7 +182,8 @@ typedef struct PRRastArgs {
   /* nullable (N,H,W) valid-prefix counts: slots 0..count-1 of a pixel hold faces, the rest -1.  */
   /* Forward: written.  Backward: if set (the forward's), pix_to_face is read only below it.    */
   int32_t* pix_count;
-  int32_t flags;                    /* PR_GRAD_PREZEROED: pr_rast_bwd does not zero grad_face_verts */
+  int32_t flags;                    /* PR_GRAD_PREZEROED: pr_rast_bwd does not zero grad_face_verts; */
+                                    /* PR_DETERMINISTIC: slot-order face sums (needs the workspace)  */
   /* Coarse binning (forward; PyTorch3D RasterizationSettings.bin_size / max_faces_per_bin,      */
   /* rasterize_meshes.py).  bin_size > 0: the face pass appends every face to the bins of        */
   /* bin_size^2 pixels (rounded up to a multiple of 8) its blur-grown box overlaps, and each      */
@@ -225,6 +226,13 @@ typedef struct PRProjectArgs {
   const float* grad_face_verts;/* bwd in (F,3,3) */
   float* grad_verts;           /* bwd out (V,3), overwritten */
   int32_t flags;               /* PR_GRAD_PREZEROED: pr_project_bwd does not zero grad_verts */
+  /* nullable vertex -> face-corner index (CSR): the corners t = 3 f + i of vertex v are        */
+  /* vert_corners[vert_corner_start[v] .. vert_corner_start[v+1]), in increasing t.  When set,   */
+  /* pr_project_bwd gathers each vertex's corner gradients in that order (the order of the       */
+  /* verts[faces] backward, PyTorch3D's face gather) and applies the projection Jacobian once    */
+  /* per vertex: deterministic, no atomics.  Else one float atomic per corner component.         */
+  const int64_t* vert_corner_start; /* (V+1) */
+  const int64_t* vert_corners;      /* (3F) */
 } PRProjectArgs;
 
 /* Phong shading of every fragment slot: PyTorch3D 0.4.0 phong_shading (+ the texel lookup of
@@ -248,6 +256,10 @@ typedef struct PRShadeArgs {
   const float* bary;           /* (N,H,W,K,3) */
   const int64_t* faces;        /* (F,3) packed vertex indices */
   const float* verts;          /* (V,3) world positions */
+  int32_t flags;               /* PR_DETERMINISTIC: the backward's per-vertex / per-texel / per-batch */
+                               /* sums in slot order (pr_shade_bwd_workspace_size bytes of workspace) */
+  void* workspace;
+  size_t workspace_bytes;
   const float* normals;        /* (V,3) vertex normals */
   int64_t V, F;
   int32_t texture;             /* PR_TEX_* */
@@ -279,6 +291,7 @@ typedef struct PRShadeArgs {
 } PRShadeArgs;
 
 int pr_shade_fwd(const PRShadeArgs* args, void* stream);
+size_t pr_shade_bwd_workspace_size(const PRShadeArgs* args);
 int pr_shade_bwd(const PRShadeArgs* args, void* stream);
 
 /* Area-weighted vertex normals of a packed mesh: PyTorch3D Meshes.verts_normals_packed (the
@@ -296,6 +309,12 @@ typedef struct PRNormalsArgs {
   const float* grad_normals;   /* bwd in (V,3) */
   float* grad_raw;             /* bwd scratch (V,3) */
   float* grad_verts;           /* bwd out (V,3), overwritten */
+  /* nullable vertex -> face-corner index (CSR, as in PRProjectArgs) listing each vertex's corners */
+  /* in PyTorch3D's accumulation order: all corner-1 entries by face, then corner 2, then corner 0 */
+  /* (its three index_adds).  When set, both passes gather per vertex in that order: one kernel    */
+  /* per pass, deterministic, no atomics.  Else one thread per face with float atomics.            */
+  const int64_t* vert_corner_start; /* (V+1) */
+  const int64_t* vert_corners;      /* (3F) */
 } PRNormalsArgs;
 
 int pr_vert_normals_fwd(const PRNormalsArgs* args, void* stream);
@@ -303,6 +322,12 @@ int pr_vert_normals_bwd(const PRNormalsArgs* args, void* stream);
 
 /* the backward's gradient accumulator was zeroed by the forward (pr_project_rast_fwd) */
 #define PR_GRAD_PREZEROED 1
+/* deterministic-order backward (PRRastArgs.flags, PRShadeArgs.flags): the sums that
+ * the fast path scatters with float atomics are formed by a stable sort of the contributions by
+ * target and in-order sums instead (pr_*_bwd_workspace_size reports the workspace they need).
+ * pr_rast_bwd then sums every face's slot gradients in slot order, sequentially: the
+ * accumulation order of PyTorch3D's CPU backward (and of oracle/rast_oracle.c), bit for bit. */
+#define PR_DETERMINISTIC 2
 
 int pr_project_fwd(const PRProjectArgs* args, void* stream);
 /* MeshRasterizer.forward's projection (eval.py:165-168: world -> view -> NDC with view z, face

@@ -25,6 +25,7 @@ PR_BLEND_RAST_WOVR = 32
 PR_BLEND_AGG_WOVR = 64
 PR_BLEND_SOFT = 128
 PR_GRAD_PREZEROED = 1
+PR_DETERMINISTIC = 2
 
 _vp = C.c_void_p
 
@@ -87,7 +88,8 @@ class PRInterpArgs(C.Structure):
 class PRProjectArgs(C.Structure):
     _fields_ = [("verts", _vp), ("faces", _vp), ("mesh_first_face", _vp), ("mesh_num_faces", _vp),
                 ("world_to_view", _vp), ("proj", _vp), ("V", C.c_int64), ("F", C.c_int64), ("N", C.c_int32),
-                ("face_verts", _vp), ("grad_face_verts", _vp), ("grad_verts", _vp), ("flags", C.c_int32)]
+                ("face_verts", _vp), ("grad_face_verts", _vp), ("grad_verts", _vp), ("flags", C.c_int32),
+                ("vert_corner_start", _vp), ("vert_corners", _vp)]
 
 
 class PRSO3Args(C.Structure):
@@ -108,7 +110,7 @@ PR_TEX_VERTEX = 2
 class PRShadeArgs(C.Structure):
     _fields_ = [("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("K", C.c_int32),
                 ("pix_to_face", _vp), ("pix_count", _vp), ("bary", _vp), ("faces", _vp), ("verts", _vp),
-                ("normals", _vp), ("V", C.c_int64), ("F", C.c_int64), ("texture", C.c_int32), ("texels", _vp),
+                ("flags", C.c_int32), ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("normals", _vp), ("V", C.c_int64), ("F", C.c_int64), ("texture", C.c_int32), ("texels", _vp),
                 ("vert_colors", _vp), ("face_uvs", _vp), ("maps", _vp), ("Hm", C.c_int32), ("Wm", C.c_int32),
                 ("directional", C.c_int32), ("light", _vp), ("ambient", _vp), ("diffuse_color", _vp),
                 ("specular_color", _vp), ("mat_diffuse", _vp), ("mat_specular", _vp), ("shininess", _vp),
@@ -119,7 +121,8 @@ class PRShadeArgs(C.Structure):
 
 class PRNormalsArgs(C.Structure):
     _fields_ = [("verts", _vp), ("faces", _vp), ("V", C.c_int64), ("F", C.c_int64), ("normals", _vp),
-                ("raw", _vp), ("grad_normals", _vp), ("grad_raw", _vp), ("grad_verts", _vp)]
+                ("raw", _vp), ("grad_normals", _vp), ("grad_raw", _vp), ("grad_verts", _vp),
+                ("vert_corner_start", _vp), ("vert_corners", _vp)]
 
 
 # every symbol include/pertrender.h declares, with its argument struct (None = no args)
@@ -148,11 +151,12 @@ EXPORTS = {
     "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_philox": (C.c_int, [_vp, _vp, C.c_int64, _vp, _vp, _vp, _vp]),
     "pr_shade_fwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
+    "pr_shade_bwd_workspace_size": (C.c_size_t, [C.POINTER(PRShadeArgs)]),
     "pr_shade_bwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
     "pr_vert_normals_fwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
     "pr_vert_normals_bwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
 }
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lib = None
 
@@ -201,6 +205,20 @@ def stream_of(t):
     if _raw_stream is not None:
         return C.c_void_p(_raw_stream(t.device.index if t.device.index is not None else torch.cuda.current_device()))
     return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def deterministic():
+    """Deterministic-order backward passes (PR_DETERMINISTIC), switched with torch's own
+    ``torch.use_deterministic_algorithms(True)``: the sums the fast kernels scatter with float
+    atomics (rasterizer, shading) are formed by a stable sort and in-order sums instead, and the
+    rasterizer backward then reproduces the CPU oracle's (PyTorch3D's CPU) accumulation bit for
+    bit.  Gathers over the mesh topology (projection, vertex normals) are deterministic always."""
+    return torch.are_deterministic_algorithms_enabled()
+
+
+def workspace(nbytes, device):
+    """A caller-owned scratch buffer for a native call (the library allocates nothing)."""
+    return torch.empty(max(1, int(nbytes)), dtype=torch.uint8, device=device)
 
 
 def require_device(*tensors):

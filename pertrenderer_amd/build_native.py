@@ -6,6 +6,7 @@ The shared library lands next to this file so it travels with the repository
 snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
 """
 import argparse
+import concurrent.futures
 import os
 import subprocess
 import sys
@@ -15,7 +16,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpertrender.so")
 SOURCES = ["pr_capi.hip", "pr_blend.hip", "pr_rast.hip", "pr_pose.hip", "pr_shade.hip", "pr_softblend.hip",
-           "pr_normals.hip"]
+           "pr_normals.hip", "pr_detsum.hip"]
 HEADERS = ["pr_common.h", os.path.join("..", "..", "include", "pertrender.h")]
 ARCH = os.environ.get("PR_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-munsafe-fp-atomics",
@@ -44,15 +45,20 @@ def build(force=False, verbose=True, out=None, defines=()):
     if out is None and not defines and not force and not _stale():
         return LIB
     hipcc = _hipcc()
-    objs = []
     tag = "" if out is None else "_" + os.path.basename(out).replace(".", "_")
+    objs, cmds = [], []
     for src in SOURCES:
         obj = os.path.join(CSRC, src.replace(".hip", tag + ".o"))
-        cmd = [hipcc] + FLAGS + [f"-D{d}" for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.check_call(cmd)
+        cmds.append([hipcc] + FLAGS + [f"-D{d}" for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
+    # one hipcc per translation unit, in parallel (bounded: each holds ~1-2 GB while compiling)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
+    with concurrent.futures.ThreadPoolExecutor(jobs) as pool:
+        for cmd, rc in zip(cmds, pool.map(lambda c: subprocess.call(c), cmds)):
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            if rc != 0:
+                raise subprocess.CalledProcessError(rc, cmd)
     tmp = lib + ".tmp"
     cmd = [hipcc, "-shared", f"--offload-arch={ARCH}", "-o", tmp] + objs
     if verbose:

@@ -815,7 +815,6 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
         const int pl = bt.pl[u], k = bt.k[u], li = i0 + u * kThreads;  // entry index
         DW[li] = dw[u];
         if (k == K) continue;
-        const int64_t gp = pix0 + pl, gs = gp * K + k;
         const bool m = mk[u];
         const float mf = m ? 1.f : 0.f;
         float prob = pg[u].x, gm = pg[u].y;
@@ -960,7 +959,6 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
   // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0] (win counts: B1, CM 2's dW: B2)
   PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
     const int s = k;
-    const int64_t gp = pix0 + pl;
     const int e0 = ea[pl] - eb, c = cl[pl];
     const int jw = WN[pl * Sa + s];
     const int j0 = (int)PX[pl * 12 + 3];

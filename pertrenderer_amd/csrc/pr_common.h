@@ -106,4 +106,32 @@ int check_launch(const char* what);
 size_t soft_blend_workspace(const PRBlendParams& p);
 int soft_blend_fwd(const PRBlendFwdArgs& a, hipStream_t st);
 int soft_blend_bwd(const PRBlendBwdArgs& a, hipStream_t st);
+
+// Deterministic ordered scatter-add (pr_detsum.hip), the PR_DETERMINISTIC mode of the passes
+// that scatter with float atomics: out[k] = sum of the C components of the entries with key k,
+// in entry order.  Caller: detsum_layout on a workspace of detsum_workspace bytes, fill
+// keys[0..n) (keys >= M are dropped), detsum_sort, then write each entry's components at its
+// sorted position (vals_sorted[i * C + c] for the entry idx_sorted[i]) -- or fill vals in entry
+// order and detsum_gather -- and detsum_reduce.  chunk <= 0: one sequential pass per key (the
+// order of a serial loop); chunk > 0: sequential chunk sums of `chunk` entries, then the chunk
+// sums in order (long segments).
+struct DetSum {
+  int64_t n = 0, M = 0;
+  int C = 0, end_bit = 0;
+  uint32_t* keys = nullptr;
+  uint32_t* keys_sorted = nullptr;
+  uint32_t* idx = nullptr;
+  uint32_t* idx_sorted = nullptr;
+  float* vals = nullptr;
+  float* vals_sorted = nullptr;
+  uint32_t* start = nullptr;
+  uint32_t* end = nullptr;
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+};
+size_t detsum_workspace(int64_t n, int64_t M, int C);
+int detsum_layout(void* ws, size_t bytes, int64_t n, int64_t M, int C, DetSum& d);
+int detsum_sort(const DetSum& d, hipStream_t st);
+int detsum_gather(const DetSum& d, hipStream_t st);
+int detsum_reduce(const DetSum& d, float* out, int64_t chunk, bool accumulate, hipStream_t st);
 }  // namespace pr

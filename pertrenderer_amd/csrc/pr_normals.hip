@@ -83,6 +83,56 @@ __global__ void face_cross_bwd_kernel(PRNormalsArgs a) {
   }
 }
 
+// ---- CSR form (vert_corner_start / vert_corners): one thread per vertex, its corners in
+// PyTorch3D's index_add order (corner-1 entries by face, then corner 2, then corner 0), so the
+// sums are sequential in that order; no atomics, no memset, deterministic.
+PR_DEV F3 corner_cross(const PRNormalsArgs& a, int64_t t) {
+  const int64_t f = t / 3;
+  const int c = (int)(t - f * 3);
+  const F3 v0 = load3(a.verts, a.faces[f * 3]), v1 = load3(a.verts, a.faces[f * 3 + 1]),
+           v2 = load3(a.verts, a.faces[f * 3 + 2]);
+  return c == 1 ? cross(sub(v2, v1), sub(v0, v1)) : (c == 2 ? cross(sub(v0, v2), sub(v1, v2)) : cross(sub(v1, v0), sub(v2, v0)));
+}
+
+__global__ void normals_gather_kernel(PRNormalsArgs a) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.V; v += (int64_t)gridDim.x * blockDim.x) {
+    F3 n{0.f, 0.f, 0.f};
+    for (int64_t j = a.vert_corner_start[v]; j < a.vert_corner_start[v + 1]; ++j) {
+      const F3 c = corner_cross(a, a.vert_corners[j]);
+      n.x += c.x; n.y += c.y; n.z += c.z;
+    }
+    if (a.raw) { a.raw[v * 3] = n.x; a.raw[v * 3 + 1] = n.y; a.raw[v * 3 + 2] = n.z; }
+    const float d = fmaxf(norm3(n), 1e-6f);
+    a.normals[v * 3] = n.x / d; a.normals[v * 3 + 1] = n.y / d; a.normals[v * 3 + 2] = n.z / d;
+  }
+}
+
+// d verts of vertex v: for every face it is a corner of, the three corner crosses' partials
+// with respect to v (dp = q x g, dq = g x p, and -dp - dq for the corner vertex itself)
+__global__ void normals_bwd_gather_kernel(PRNormalsArgs a) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.V; v += (int64_t)gridDim.x * blockDim.x) {
+    F3 acc{0.f, 0.f, 0.f};
+    for (int64_t j = a.vert_corner_start[v]; j < a.vert_corner_start[v + 1]; ++j) {
+      const int64_t t = a.vert_corners[j], f = t / 3;
+      const int sv = (int)(t - f * 3);  // v's slot in face f
+      const int64_t id[3] = {a.faces[f * 3], a.faces[f * 3 + 1], a.faces[f * 3 + 2]};
+      const F3 vx[3] = {load3(a.verts, id[0]), load3(a.verts, id[1]), load3(a.verts, id[2])};
+      // corners in face_cross_bwd_kernel's order: (c, a, b) = (1, 2, 0), (2, 0, 1), (0, 1, 2)
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int c = (r + 1) % 3, sa = (r + 2) % 3, sb = r;
+        const F3 g = load3(a.grad_raw, id[c]);
+        const F3 p = sub(vx[sa], vx[c]), q = sub(vx[sb], vx[c]);
+        const F3 dp = cross(q, g), dq = cross(g, p);
+        if (sv == sa) { acc.x += dp.x; acc.y += dp.y; acc.z += dp.z; }
+        else if (sv == sb) { acc.x += dq.x; acc.y += dq.y; acc.z += dq.z; }
+        else { acc.x += -dp.x - dq.x; acc.y += -dp.y - dq.y; acc.z += -dp.z - dq.z; }
+      }
+    }
+    a.grad_verts[v * 3] = acc.x; a.grad_verts[v * 3 + 1] = acc.y; a.grad_verts[v * 3 + 2] = acc.z;
+  }
+}
+
 int normals_check(const PRNormalsArgs* a) {
   if (!a || a->V < 0 || a->F < 0 || (a->F > 0 && (!a->verts || !a->faces)))
     return set_error(PR_ERR_ARG, "vert_normals: bad args");
@@ -102,6 +152,10 @@ extern "C" int pr_vert_normals_fwd(const PRNormalsArgs* args, void* stream) {
   const PRNormalsArgs& a = *args;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (a.V == 0) return PR_OK;
+  if (a.vert_corner_start && a.vert_corners) {
+    normals_gather_kernel<<<blocks_for(a.V), kThreads, 0, st>>>(a);
+    return check_launch("normals_gather");
+  }
   if (hipMemsetAsync(a.normals, 0, (size_t)a.V * 3 * sizeof(float), st) != hipSuccess)
     return set_error(PR_ERR_HIP, "vert_normals_fwd: memset failed");
   if (a.F > 0) {
@@ -119,10 +173,15 @@ extern "C" int pr_vert_normals_bwd(const PRNormalsArgs* args, void* stream) {
     return set_error(PR_ERR_ARG, "vert_normals_bwd: buffers missing");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (a.V == 0) return PR_OK;
-  if (hipMemsetAsync(a.grad_verts, 0, (size_t)a.V * 3 * sizeof(float), st) != hipSuccess)
+  const bool csr = a.vert_corner_start && a.vert_corners;
+  if (!csr && hipMemsetAsync(a.grad_verts, 0, (size_t)a.V * 3 * sizeof(float), st) != hipSuccess)
     return set_error(PR_ERR_HIP, "vert_normals_bwd: memset failed");
   normalize_bwd_kernel<<<blocks_for(a.V), kThreads, 0, st>>>(a);
   if (int e = check_launch("normalize_bwd")) return e;
+  if (csr) {
+    normals_bwd_gather_kernel<<<blocks_for(a.V), kThreads, 0, st>>>(a);
+    return check_launch("normals_bwd_gather");
+  }
   if (a.F > 0) {
     face_cross_bwd_kernel<<<blocks_for(a.F), kThreads, 0, st>>>(a);
     if (int e = check_launch("face_cross_bwd")) return e;

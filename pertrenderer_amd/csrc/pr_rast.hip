@@ -1250,6 +1250,132 @@ PR_DEV void slot_grad(const PRRastArgs& a, V2 p, const float* v, int64_t o, floa
   g[6] = gbv[2].x + gdv[2].x; g[7] = gbv[2].y + gdv[2].y; g[8] = gzb * bc[2] + gz[2];
 }
 
+// ---- exact slot gradient: oracle/rast_oracle.c rast_bwd's operations in its order (PyTorch3D's
+// CPU backward): IEEE divisions, one accumulator per vertex component with the distance terms
+// first, then the barycentric terms edge by edge, then the area terms.  A slot's contribution is
+// the oracle's bit for bit; summed per face in slot order (PR_DETERMINISTIC) the face gradients
+// are the oracle's bits.
+PR_DEV void acc_edge(V2 p, V2 a, V2 b, float g, float* ga, float* gb) {  // edge_fn(p, a, b) partials
+  ga[0] += g * (p.y - b.y); ga[1] += g * (b.x - p.x);
+  gb[0] += g * (a.y - p.y); gb[1] += g * (p.x - a.x);
+}
+
+PR_DEV void acc_seg(V2 p, V2 a, V2 b, float g, float* ga, float* gb) {  // squared segment distance
+  const float bax = b.x - a.x, bay = b.y - a.y;
+  const float l2 = bax * bax + bay * bay;
+  float t = 1.f;
+  if (!(l2 <= kEps)) {
+    t = (bax * (p.x - a.x) + bay * (p.y - a.y)) / l2;
+    t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+  }
+  const float qx = (1.f - t) * a.x + t * b.x, qy = (1.f - t) * a.y + t * b.y;
+  const float dx = qx - p.x, dy = qy - p.y;
+  ga[0] += g * (1.f - t) * 2.f * dx; ga[1] += g * (1.f - t) * 2.f * dy;
+  gb[0] += g * t * 2.f * dx;         gb[1] += g * t * 2.f * dy;
+}
+
+PR_DEV void slot_grad_exact(const PRRastArgs& a, V2 p, const float* v, int64_t o, float out[9]) {
+  const V2 v0{v[0], v[1]}, v1{v[3], v[4]}, v2{v[6], v[7]};
+  const float z0 = v[2], z1 = v[5], z2 = v[8];
+  const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
+  const float gzb = a.grad_zbuf ? a.grad_zbuf[o] : 0.f;
+  const float gd = a.grad_dists ? a.grad_dists[o] : 0.f;
+  float gbu[3] = {0.f, 0.f, 0.f};
+  if (a.grad_bary) { gbu[0] = a.grad_bary[o * 3]; gbu[1] = a.grad_bary[o * 3 + 1]; gbu[2] = a.grad_bary[o * 3 + 2]; }
+  float bw[3], bp[3], bc[3];
+  bary_fwd(p, v0, v1, v2, bw);
+  if (persp) persp_fwd(bw, z0, z1, z2, bp); else { bp[0] = bw[0]; bp[1] = bw[1]; bp[2] = bw[2]; }
+  if (clip) clip_fwd(bp, bc); else { bc[0] = bp[0]; bc[1] = bp[1]; bc[2] = bp[2]; }
+  const bool inside = bp[0] > 0.f && bp[1] > 0.f && bp[2] > 0.f;
+  float gv[3][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+  {
+    const float g = inside ? -gd : gd;
+    const float e01 = seg_dist2(p, v0, v1), e02 = seg_dist2(p, v0, v2), e12 = seg_dist2(p, v1, v2);
+    if (e01 <= e02 && e01 <= e12) acc_seg(p, v0, v1, g, gv[0], gv[1]);
+    else if (e02 <= e01 && e02 <= e12) acc_seg(p, v0, v2, g, gv[0], gv[2]);
+    else acc_seg(p, v1, v2, g, gv[1], gv[2]);
+  }
+  const float gsum[3] = {gbu[0] + gzb * z0, gbu[1] + gzb * z1, gbu[2] + gzb * z2};
+  float gpp[3] = {gsum[0], gsum[1], gsum[2]};
+  if (clip) {
+    const float w0 = bp[0] > 0.f ? bp[0] : 0.f, w1 = bp[1] > 0.f ? bp[1] : 0.f, w2 = bp[2] > 0.f ? bp[2] : 0.f;
+    const float s = w0 + w1 + w2;
+    float gw[3];
+    if (s > 1e-5f) {
+      const float dot = (gsum[0] * w0 + gsum[1] * w1 + gsum[2] * w2) / (s * s);
+      gw[0] = gsum[0] / s - dot; gw[1] = gsum[1] / s - dot; gw[2] = gsum[2] / s - dot;
+    } else {
+      gw[0] = gsum[0] / 1e-5f; gw[1] = gsum[1] / 1e-5f; gw[2] = gsum[2] / 1e-5f;
+    }
+    gpp[0] = bp[0] > 0.f ? gw[0] : 0.f; gpp[1] = bp[1] > 0.f ? gw[1] : 0.f; gpp[2] = bp[2] > 0.f ? gw[2] : 0.f;
+  }
+  float gw[3] = {gpp[0], gpp[1], gpp[2]}, gzp[3] = {0.f, 0.f, 0.f};
+  if (persp) {
+    const float t0 = bw[0] * z1 * z2, t1 = z0 * bw[1] * z2, t2 = z0 * z1 * bw[2];
+    const float s = t0 + t1 + t2;
+    float gt[3];
+    if (s > kEps) {
+      const float dot = (gpp[0] * t0 + gpp[1] * t1 + gpp[2] * t2) / (s * s);
+      gt[0] = gpp[0] / s - dot; gt[1] = gpp[1] / s - dot; gt[2] = gpp[2] / s - dot;
+    } else {
+      gt[0] = gpp[0] / kEps; gt[1] = gpp[1] / kEps; gt[2] = gpp[2] / kEps;
+    }
+    gw[0] = gt[0] * z1 * z2; gw[1] = gt[1] * z0 * z2; gw[2] = gt[2] * z0 * z1;
+    gzp[0] = gt[1] * bw[1] * z2 + gt[2] * z1 * bw[2];
+    gzp[1] = gt[0] * bw[0] * z2 + gt[2] * z0 * bw[2];
+    gzp[2] = gt[0] * bw[0] * z1 + gt[1] * z0 * bw[1];
+  }
+  // barycentric terms: b_i = e_i / area, area = E(v2, v0, v1) + eps
+  const float area = edge_fn(v2, v0, v1) + kEps;
+  const float e0 = edge_fn(p, v1, v2), e1 = edge_fn(p, v2, v0), e2 = edge_fn(p, v0, v1);
+  const float darea = -(gw[0] * e0 + gw[1] * e1 + gw[2] * e2) / (area * area);
+  acc_edge(p, v1, v2, gw[0] / area, gv[1], gv[2]);
+  acc_edge(p, v2, v0, gw[1] / area, gv[2], gv[0]);
+  acc_edge(p, v0, v1, gw[2] / area, gv[0], gv[1]);
+  gv[2][0] += darea * (v1.y - v0.y);
+  gv[2][1] += darea * (v0.x - v1.x);
+  acc_edge(v2, v0, v1, darea, gv[0], gv[1]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    out[i * 3 + 0] = gv[i][0];
+    out[i * 3 + 1] = gv[i][1];
+    out[i * 3 + 2] = gzb * bc[i] + gzp[i];
+  }
+}
+
+template <bool EXACT>
+PR_DEV void slot_grad_any(const PRRastArgs& a, V2 p, const float* v, int64_t o, float g[9]) {
+  if constexpr (EXACT) slot_grad_exact(a, p, v, o, g);
+  else slot_grad(a, p, v, o, g);
+}
+
+// ---- deterministic mode (PR_DETERMINISTIC): key every slot by its face (padded slots by F),
+// stable-sort, exact slot gradients at their sorted positions, in-order face sums (pr_detsum.hip)
+__global__ void rast_bwd_keys_kernel(PRRastArgs a, uint32_t* keys, int64_t n) {
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = o / a.K;
+    const bool valid = a.pix_count ? (int)(o - pix * a.K) < a.pix_count[pix] : true;
+    const int64_t f = valid ? a.pix_to_face[o] : -1;
+    keys[o] = f >= 0 ? (uint32_t)f : (uint32_t)a.F;
+  }
+}
+
+__global__ void rast_bwd_sorted_grad_kernel(PRRastArgs a, const uint32_t* keys, const uint32_t* idx, float* vals,
+                                            int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t f = keys[i];
+    if ((int64_t)f >= a.F) continue;
+    const int64_t o = idx[i];
+    const int64_t pix = o / a.K;
+    const int col = (int)(pix % a.W), row = (int)((pix / a.W) % a.H);
+    const V2 p{ndc(a.W - 1 - col, a.W, a.H), ndc(a.H - 1 - row, a.H, a.W)};
+    float g[9];
+    slot_grad_exact(a, p, a.face_verts + (int64_t)f * 9, o, g);
+#pragma unroll
+    for (int c = 0; c < 9; ++c) vals[i * 9 + c] = g[c];
+  }
+}
+
 constexpr int kHash = 512;      // LDS hash entries per workgroup (distinct faces of one tile)
 constexpr int kBwdTile = 8;     // tile width; rows per tile (<= 8) chosen at launch
 constexpr int kBwdThreads = 256;
@@ -1277,7 +1403,7 @@ constexpr int kBwdFaces = 128;  // faces per tile reduced by the transpose; late
 //     Global float atomics).
 // Faces past the first kBwdFaces of a tile, and hash overflow, add their slots straight
 // to global memory (correct, slower; dense meshes under large tiles only).
-template <int ROWS>
+template <int ROWS, bool EXACT>
 __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int order) {
   constexpr int tile_rows = ROWS, TP = kBwdTile * ROWS;  // tile pixels
   __shared__ int hkey[kHash];
@@ -1372,7 +1498,7 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int
       const int64_t o = tile_o + r * row_stride + c * K + k;
       const V2 p{pxs[c], pys[r]};
       float g[9];
-      slot_grad(a, p, a.face_verts + (int64_t)fi * 9, o, g);
+      slot_grad_any<EXACT>(a, p, a.face_verts + (int64_t)fi * 9, o, g);
       uint32_t h = ((uint32_t)fi * 2654435761u) & (kHash - 1);
       int fl = kBwdFaces;  // not found (hash overflow): global path
       for (int probe = 0; probe < 32; ++probe) {
@@ -1527,6 +1653,52 @@ __global__ void project_prep_kernel(PRProjectArgs a, float blur, int cull_backfa
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.V * 3; i += stride) zero_v[i] = 0.f;
 }
 
+// d v_view -> d v_world through [v,1] @ M / w, and d NDC (x, y) + d view z -> d v_view
+PR_DEV void project_vertex_bwd(const float* M, const float* P, const float* v, float gx, float gy, float gz,
+                               float gout[3]) {
+  float o[4], c[4];
+  xform(M, v[0], v[1], v[2], o);
+  const float vv[3] = {o[0] / o[3], o[1] / o[3], o[2] / o[3]};
+  xform(P, vv[0], vv[1], vv[2], c);
+  const float i3 = 1.f / c[3], i33 = i3 * i3;
+  float gvv[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    gvv[k] = gx * (P[k * 4 + 0] * i3 - c[0] * P[k * 4 + 3] * i33) + gy * (P[k * 4 + 1] * i3 - c[1] * P[k * 4 + 3] * i33);
+  gvv[2] += gz;
+  const float j3 = 1.f / o[3], j33 = j3 * j3;
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    float g = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g += gvv[k] * (M[m * 4 + k] * j3 - o[k] * M[m * 4 + 3] * j33);
+    gout[m] = g;
+  }
+}
+
+// CSR form: each vertex sums its corners' d face_verts in corner order (the verts[faces]
+// backward), then one Jacobian per vertex.  Deterministic, no atomics, every row written.
+__global__ void project_bwd_gather_kernel(PRProjectArgs a) {
+  for (int64_t vi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; vi < a.V; vi += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = a.vert_corner_start[vi], e = a.vert_corner_start[vi + 1];
+    float g[3] = {0.f, 0.f, 0.f};
+    if (s < e) {
+      float gx = 0.f, gy = 0.f, gz = 0.f;
+      for (int64_t j = s; j < e; ++j) {
+        const int64_t t = a.vert_corners[j];
+        gx += a.grad_face_verts[t * 3];
+        gy += a.grad_face_verts[t * 3 + 1];
+        gz += a.grad_face_verts[t * 3 + 2];
+      }
+      const int n = mesh_of(a.mesh_first_face, a.mesh_num_faces, a.N, a.vert_corners[s] / 3);
+      project_vertex_bwd(a.world_to_view + n * 16, a.proj + n * 16, a.verts + vi * 3, gx, gy, gz, g);
+    }
+    a.grad_verts[vi * 3] = g[0];
+    a.grad_verts[vi * 3 + 1] = g[1];
+    a.grad_verts[vi * 3 + 2] = g[2];
+  }
+}
+
 __global__ void project_bwd_kernel(PRProjectArgs a) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.F * 3; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t f = t / 3;
@@ -1677,7 +1849,25 @@ static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2
   return check_launch("rast_frag");
 }
 
-extern "C" size_t pr_rast_bwd_workspace_size(const PRRastArgs*) { return 0; }
+extern "C" size_t pr_rast_bwd_workspace_size(const PRRastArgs* a) {
+  if (!a || !(a->flags & PR_DETERMINISTIC)) return 0;
+  return detsum_workspace((int64_t)a->N * a->H * a->W * a->K, a->F, 9);
+}
+
+// PR_DETERMINISTIC: every face's slot gradients (exact arithmetic) summed in slot order
+static int rast_bwd_deterministic(const PRRastArgs& a, hipStream_t st) {
+  const int64_t n = (int64_t)a.N * a.H * a.W * a.K;
+  DetSum d;
+  if (int e = detsum_layout(a.workspace, a.workspace_bytes, n, a.F, 9, d)) return e;
+  if (a.F == 0) return PR_OK;
+  const int nb = (int)std::min<int64_t>((n + kThreads - 1) / kThreads, 16384);
+  rast_bwd_keys_kernel<<<nb, kThreads, 0, st>>>(a, d.keys, n);
+  if (int e = check_launch("rast_bwd_keys")) return e;
+  if (int e = detsum_sort(d, st)) return e;
+  rast_bwd_sorted_grad_kernel<<<nb, kThreads, 0, st>>>(a, d.keys_sorted, d.idx_sorted, d.vals_sorted, n);
+  if (int e = check_launch("rast_bwd_sorted_grad")) return e;
+  return detsum_reduce(d, a.grad_face_verts, 0, false, st);
+}
 
 extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "rast_bwd: null args");
@@ -1685,6 +1875,7 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
   if (int e = rast_check(a)) return e;
   if (!a.pix_to_face || !a.grad_face_verts) return set_error(PR_ERR_ARG, "rast_bwd: buffer missing");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a.flags & PR_DETERMINISTIC) return rast_bwd_deterministic(a, st);
   if (a.F > 0 && !(a.flags & PR_GRAD_PREZEROED)) {
     if (hipMemsetAsync(a.grad_face_verts, 0, (size_t)a.F * 9 * sizeof(float), st) != hipSuccess)
       return set_error(PR_ERR_HIP, "rast_bwd: memset failed");
@@ -1699,10 +1890,19 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
   dim3 grid((a.W + kBwdTile - 1) / kBwdTile, (a.H + rows - 1) / rows, a.N);
   // tile rows dispatched centre-out (PR_RAST_ORDER bit 1; 0: row-major)
   static const int order = (getenv("PR_RAST_ORDER") ? atoi(getenv("PR_RAST_ORDER")) : 3) >> 1 & 1;
-  if (rows == 8) rast_bwd_kernel<8><<<grid, kBwdThreads, 0, st>>>(a, order);
-  else if (rows == 4) rast_bwd_kernel<4><<<grid, kBwdThreads, 0, st>>>(a, order);
-  else if (rows == 1) rast_bwd_kernel<1><<<grid, kBwdThreads, 0, st>>>(a, order);
-  else rast_bwd_kernel<2><<<grid, kBwdThreads, 0, st>>>(a, order);
+  // slot arithmetic: the oracle's exact operations (IEEE divisions, its accumulation order) by
+  // default; PR_RAST_BWD_EXACT=0 selects reciprocal-multiply (sweeps)
+  static const bool exact = !getenv("PR_RAST_BWD_EXACT") || atoi(getenv("PR_RAST_BWD_EXACT")) != 0;
+#define PR_RAST_BWD_LAUNCH(R)                                               \
+  do {                                                                      \
+    if (exact) rast_bwd_kernel<R, true><<<grid, kBwdThreads, 0, st>>>(a, order);  \
+    else rast_bwd_kernel<R, false><<<grid, kBwdThreads, 0, st>>>(a, order);       \
+  } while (0)
+  if (rows == 8) PR_RAST_BWD_LAUNCH(8);
+  else if (rows == 4) PR_RAST_BWD_LAUNCH(4);
+  else if (rows == 1) PR_RAST_BWD_LAUNCH(1);
+  else PR_RAST_BWD_LAUNCH(2);
+#undef PR_RAST_BWD_LAUNCH
   return check_launch("rast_bwd");
 }
 
@@ -1751,6 +1951,12 @@ extern "C" int pr_project_bwd(const PRProjectArgs* args, void* stream) {
   if (int e = project_check(args)) return e;
   if (!args->grad_face_verts || !args->grad_verts) return set_error(PR_ERR_ARG, "project_bwd: buffers missing");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (args->vert_corner_start && args->vert_corners) {
+    if (args->V == 0) return PR_OK;
+    const int nb = (int)std::min<int64_t>((args->V + kThreads - 1) / kThreads, 4096);
+    project_bwd_gather_kernel<<<nb, kThreads, 0, st>>>(*args);
+    return check_launch("project_bwd_gather");
+  }
   if (args->V > 0 && !(args->flags & PR_GRAD_PREZEROED) &&
       hipMemsetAsync(args->grad_verts, 0, (size_t)args->V * 3 * sizeof(float), st) != hipSuccess)
     return set_error(PR_ERR_HIP, "project_bwd: memset failed");

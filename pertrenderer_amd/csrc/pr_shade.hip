@@ -189,10 +189,24 @@ PR_DEV void acc(float* lds, bool use_lds, int off, float* global, int64_t gi, V3
   }
 }
 
-__global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int64_t PK, int64_t HW, Tab tab) {
+// PR_DETERMINISTIC: instead of scattering, every slot writes its contributions as entries of
+// three ordered scatter-adds (pr_detsum.hip): per-vertex (slot corner i: verts | normals |
+// vertex colours, 9 components), per-batch (light | camera, 6) and per-texel (bilinear corner,
+// 3); padded slots write dropped keys.
+struct ShadeDet {
+  DetSum v, b, m;  // n == 0: not requested
+};
+
+PR_DEV void put3(float* p, V3 g) { p[0] = g.x; p[1] = g.y; p[2] = g.z; }
+
+template <bool DET>
+__global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int64_t PK, int64_t HW, Tab tab,
+                                                             ShadeDet det) {
   extern __shared__ float lds[];
-  for (int i = threadIdx.x; i < tab.size; i += kThreads) lds[i] = 0.f;
-  __syncthreads();
+  if (!DET) {
+    for (int i = threadIdx.x; i < tab.size; i += kThreads) lds[i] = 0.f;
+    __syncthreads();
+  }
   for (int64_t s = (int64_t)blockIdx.x * kThreads + threadIdx.x; s < PK; s += (int64_t)gridDim.x * kThreads) {
     const Slot sl = load_slot(a, s, HW);
     const int n = sl.n;
@@ -204,6 +218,13 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
         const V3 g = v3(a.ambient + n * 3) * gc;
         float* o = a.grad_texels + s * 3;
         o[0] = g.x; o[1] = g.y; o[2] = g.z;
+      }
+      if (DET) {
+        if (det.v.n)
+          for (int i = 0; i < 3; ++i) det.v.keys[s * 3 + i] = (uint32_t)det.v.M;
+        if (det.b.n) det.b.keys[s] = (uint32_t)det.b.M;
+        if (det.m.n)
+          for (int c = 0; c < 4; ++c) det.m.keys[s * 4 + c] = (uint32_t)det.m.M;
       }
       continue;
     }
@@ -240,6 +261,16 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
     for (int i = 0; i < 3; ++i) {
       const int64_t vi = fv[i];
       gb[i] = dot(g_P, v3(a.verts + vi * 3)) + dot(g_Nn, v3(a.normals + vi * 3));
+      if (DET) {
+        if (det.v.n) {
+          det.v.keys[s * 3 + i] = (uint32_t)vi;
+          float* e = det.v.vals + (s * 3 + i) * 9;
+          put3(e, b[i] * g_P);
+          put3(e + 3, b[i] * g_Nn);
+          put3(e + 6, V3{0.f, 0.f, 0.f});
+        }
+        continue;
+      }
       if (a.grad_verts) acc(lds, tab.useV, tab.vOff + (int)vi * 3, a.grad_verts, vi, b[i] * g_P);
       if (a.grad_normals) acc(lds, tab.useV, tab.nOff + (int)vi * 3, a.grad_normals, vi, b[i] * g_Nn);
     }
@@ -253,6 +284,10 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
       for (int i = 0; i < 3; ++i) {
         const int64_t vi = fv[i];
         gb[i] += dot(g_tex, v3(a.vert_colors + vi * 3));
+        if (DET) {
+          if (det.v.n) put3(det.v.vals + (s * 3 + i) * 9 + 6, b[i] * g_tex);
+          continue;
+        }
         if (a.grad_vert_colors) acc(lds, tab.useV, tab.cOff + (int)vi * 3, a.grad_vert_colors, vi, b[i] * g_tex);
       }
     } else {
@@ -268,12 +303,18 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
       float gix = 0.f, giy = 0.f;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        if (cx[c] >= 0 && cx[c] < a.Wm && cy[c] >= 0 && cy[c] < a.Hm) {
+        const bool in = cx[c] >= 0 && cx[c] < a.Wm && cy[c] >= 0 && cy[c] < a.Hm;
+        if (DET && det.m.n) {
+          det.m.keys[s * 4 + c] = in ? (uint32_t)(((int64_t)n * a.Hm + (a.Hm - 1 - cy[c])) * a.Wm + cx[c])
+                                     : (uint32_t)det.m.M;
+          if (in) put3(det.m.vals + (s * 4 + c) * 3, w[c] * g_tex);
+        }
+        if (in) {
           const int64_t ti = ((int64_t)(a.Hm - 1 - cy[c]) * a.Wm + cx[c]) * 3;
           const float gv = dot(v3(map + ti), g_tex);
           gix += dwx[c] * gv;
           giy += dwy[c] * gv;
-          if (a.grad_maps) {
+          if (!DET && a.grad_maps) {
             float* gm = a.grad_maps + (int64_t)n * a.Hm * a.Wm * 3 + ti;
             atomicAdd(&gm[0], w[c] * g_tex.x); atomicAdd(&gm[1], w[c] * g_tex.y); atomicAdd(&gm[2], w[c] * g_tex.z);
           }
@@ -285,9 +326,18 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
       for (int i = 0; i < 3; ++i) gb[i] += gu * q[2 * i] + gvv * q[2 * i + 1];
     }
     if (a.grad_bary) { a.grad_bary[s * 3] = gb[0]; a.grad_bary[s * 3 + 1] = gb[1]; a.grad_bary[s * 3 + 2] = gb[2]; }
+    if (DET) {
+      if (det.b.n) {
+        det.b.keys[s] = (uint32_t)n;
+        put3(det.b.vals + s * 6, g_dir);
+        put3(det.b.vals + s * 6 + 3, g_vraw);
+      }
+      continue;
+    }
     if (a.grad_light) acc(lds, tab.useB, tab.lOff + n * 3, a.grad_light, n, g_dir);
     if (a.grad_camera) acc(lds, tab.useB, tab.camOff + n * 3, a.grad_camera, n, g_vraw);
   }
+  if (DET) return;
   __syncthreads();
   // flush the workgroup's partial sums: one global atomic per touched entry
   for (int i = threadIdx.x; i < tab.size; i += kThreads) {
@@ -322,6 +372,78 @@ int shade_check(const PRShadeArgs& a) {
 
 int shade_blocks(int64_t PK) { return (int)std::min<int64_t>((PK + kThreads - 1) / kThreads, 16384); }
 
+// ---- deterministic mode layout: [vertex scatter][batch scatter][texel scatter][V x 9][N x 6]
+constexpr int64_t kDetChunk = 1024;  // entries per sequential chunk (cube vertices hold ~10^5)
+
+struct DetPlan {
+  int64_t nv, nb, nm, Mv, Mb, Mm;
+  size_t wv, wb, wm, out9, out6;
+};
+
+size_t al(size_t b) { return (b + 255) / 256 * 256; }
+
+DetPlan det_plan(const PRShadeArgs& a) {
+  DetPlan p{};
+  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+  const bool vtx = a.grad_verts || a.grad_normals || (a.texture == PR_TEX_VERTEX && a.grad_vert_colors);
+  p.nv = vtx && a.V > 0 ? PK * 3 : 0;
+  p.Mv = a.V;
+  p.nb = a.grad_light || a.grad_camera ? PK : 0;
+  p.Mb = a.N;
+  p.nm = a.texture == PR_TEX_UV && a.grad_maps ? PK * 4 : 0;
+  p.Mm = (int64_t)a.N * a.Hm * a.Wm;
+  p.wv = al(detsum_workspace(p.nv, p.Mv, 9));
+  p.wb = al(detsum_workspace(p.nb, p.Mb, 6));
+  p.wm = al(detsum_workspace(p.nm, p.Mm, 3));
+  p.out9 = p.nv ? al((size_t)a.V * 9 * 4) : 0;
+  p.out6 = p.nb ? al((size_t)a.N * 6 * 4) : 0;
+  return p;
+}
+
+__global__ void split_kernel(const float* src, int64_t rows, int C, float* d0, float* d1, float* d2) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * C; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / C;
+    const int c = (int)(i - r * C), part = c / 3;
+    float* d = part == 0 ? d0 : (part == 1 ? d1 : d2);
+    if (d) d[r * 3 + c % 3] = src[i];
+  }
+}
+
+int shade_bwd_deterministic(const PRShadeArgs& a, hipStream_t st) {
+  const DetPlan p = det_plan(a);
+  const size_t need = p.wv + p.wb + p.wm + p.out9 + p.out6;
+  if (!a.workspace || a.workspace_bytes < need) return set_error(PR_ERR_WORKSPACE, "shade_bwd: workspace too small");
+  char* w = reinterpret_cast<char*>(a.workspace);
+  ShadeDet det;
+  if (int e = detsum_layout(w, p.wv, p.nv, p.Mv, 9, det.v)) return e;
+  if (int e = detsum_layout(w + p.wv, p.wb, p.nb, p.Mb, 6, det.b)) return e;
+  if (int e = detsum_layout(w + p.wv + p.wb, p.wm, p.nm, p.Mm, 3, det.m)) return e;
+  float* out9 = reinterpret_cast<float*>(w + p.wv + p.wb + p.wm);
+  float* out6 = reinterpret_cast<float*>(w + p.wv + p.wb + p.wm + p.out9);
+  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+  Tab tab{};
+  shade_bwd_kernel<true><<<shade_blocks(PK), kThreads, 0, st>>>(a, PK, (int64_t)a.H * a.W, tab, det);
+  if (int e = check_launch("shade_bwd_det")) return e;
+  const DetSum* ds[3] = {&det.v, &det.b, &det.m};
+  float* outs[3] = {out9, out6, a.grad_maps};
+  for (int i = 0; i < 3; ++i) {
+    if (ds[i]->n == 0) continue;
+    if (int e = detsum_sort(*ds[i], st)) return e;
+    if (int e = detsum_gather(*ds[i], st)) return e;
+    if (int e = detsum_reduce(*ds[i], outs[i], kDetChunk, false, st)) return e;
+  }
+  if (p.nv) {
+    split_kernel<<<shade_blocks(a.V * 9), kThreads, 0, st>>>(out9, a.V, 9, a.grad_verts, a.grad_normals,
+                                                             a.texture == PR_TEX_VERTEX ? a.grad_vert_colors : nullptr);
+    if (int e = check_launch("shade_split_v")) return e;
+  }
+  if (p.nb) {
+    split_kernel<<<1, kThreads, 0, st>>>(out6, a.N, 6, a.grad_light, a.grad_camera, nullptr);
+    if (int e = check_launch("shade_split_b")) return e;
+  }
+  return PR_OK;
+}
+
 }  // namespace
 }  // namespace pr
 
@@ -338,12 +460,19 @@ extern "C" int pr_shade_fwd(const PRShadeArgs* args, void* stream) {
   return check_launch("shade_fwd");
 }
 
+extern "C" size_t pr_shade_bwd_workspace_size(const PRShadeArgs* args) {
+  if (!args || !(args->flags & PR_DETERMINISTIC)) return 0;
+  const DetPlan p = det_plan(*args);
+  return p.wv + p.wb + p.wm + p.out9 + p.out6;
+}
+
 extern "C" int pr_shade_bwd(const PRShadeArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "shade_bwd: null args");
   const PRShadeArgs& a = *args;
   if (int e = shade_check(a)) return e;
   if (!a.grad_colors) return set_error(PR_ERR_ARG, "shade_bwd: grad_colors missing");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a.flags & PR_DETERMINISTIC) return shade_bwd_deterministic(a, st);
   struct Z { float* p; size_t n; } zs[] = {
       {a.grad_verts, (size_t)a.V * 3}, {a.grad_normals, (size_t)a.V * 3},
       {a.texture == PR_TEX_VERTEX ? a.grad_vert_colors : nullptr, (size_t)a.V * 3},
@@ -366,6 +495,7 @@ extern "C" int pr_shade_bwd(const PRShadeArgs* args, void* stream) {
   const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
   // fewer, fatter workgroups when the LDS table is large (its zero + flush is per workgroup)
   const int nb = std::min(shade_blocks(PK), tab.size > 1024 ? 1024 : 16384);
-  shade_bwd_kernel<<<nb, kThreads, (size_t)tab.size * sizeof(float), st>>>(a, PK, (int64_t)a.H * a.W, tab);
+  shade_bwd_kernel<false><<<nb, kThreads, (size_t)tab.size * sizeof(float), st>>>(a, PK, (int64_t)a.H * a.W, tab,
+                                                                                  ShadeDet{});
   return check_launch("shade_bwd");
 }

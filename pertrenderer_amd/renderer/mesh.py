@@ -70,6 +70,7 @@ class _Topology:
         self.device = device
         self._packed = None
         self._idx = None
+        self._csr = {}
 
     def faces_packed(self):
         if self._packed is None:
@@ -88,6 +89,26 @@ class _Topology:
             self._idx = dict(nfaces=nf.to(self.device), first=first.to(self.device), nverts=nv.to(self.device),
                              vfirst=(torch.cumsum(nv, 0) - nv).to(self.device))
         return self._idx
+
+    def corner_csr(self, kind="gather"):
+        """Vertex -> face-corner index (CSR) of the packed mesh: (start (V+1), corners (3F)) int64,
+        the corners t = 3 f + i of vertex v at corners[start[v]:start[v+1]].  "gather": in
+        increasing t (the order of the verts[faces] backward); "normals": PyTorch3D's normal
+        accumulation order (corner 1 of every face, then corner 2, then corner 0: its three
+        index_adds).  Built once per topology on the device (stable sort, no host sync), so the
+        native projection / normals passes gather per vertex without atomics."""
+        c = self._csr.get(kind)
+        if c is None:
+            f = self.faces_packed()
+            F, V = f.shape[0], sum(self.nverts)
+            t = torch.arange(3 * F, device=f.device).reshape(F, 3)
+            perm = [1, 2, 0] if kind == "normals" else [0, 1, 2]
+            keys = f[:, perm].t().reshape(-1) if kind == "normals" else f.reshape(-1)
+            vals = t[:, perm].t().reshape(-1) if kind == "normals" else t.reshape(-1)
+            order = torch.argsort(keys, stable=True)
+            start = torch.searchsorted(keys[order].contiguous(), torch.arange(V + 1, device=f.device))
+            c = self._csr[kind] = (start.contiguous(), vals[order].contiguous())
+        return c
 
 
 class Meshes:
@@ -139,6 +160,10 @@ class Meshes:
     def faces_packed(self):
         return self._topo.faces_packed()
 
+    def corner_csr(self, kind="gather"):
+        """Vertex -> face-corner CSR of the packed topology (_Topology.corner_csr); not PyTorch3D API."""
+        return self._topo.corner_csr(kind)
+
     def verts_padded(self):
         if len(self._verts) == 1:
             return self._verts[0][None]  # a view: no copy kernel
@@ -164,7 +189,7 @@ class Meshes:
         v = self.verts_packed()
         f = self.faces_packed()
         if NATIVE_NORMALS and v.is_cuda and v.dtype == torch.float32:
-            return _VertNormalsFn.apply(v, f)
+            return _VertNormalsFn.apply(v, f, *self._topo.corner_csr("normals"))
         fv = gather_faces(v, f)
         n = torch.zeros_like(v)
         # each corner's cross product is 2x the face area times its normal
@@ -233,10 +258,13 @@ NATIVE_NORMALS = os.environ.get("PR_NATIVE_NORMALS", "1") == "1"
 
 
 class _VertNormalsFn(torch.autograd.Function):
-    """verts -> area-weighted, normalised vertex normals (pr_vert_normals_fwd/bwd)."""
+    """verts -> area-weighted, normalised vertex normals (pr_vert_normals_fwd/bwd), gathered per
+    vertex over the topology's corner CSR (deterministic, no atomics).  Its backward runs on the
+    kernels' outputs, so it is once-differentiable: a double backward raises instead of returning
+    silent zeros."""
 
     @staticmethod
-    def forward(ctx, verts, faces):
+    def forward(ctx, verts, faces, csr_start=None, csr_corners=None):
         from .. import _native as nat
         lib = nat.load()
         v = verts.detach().contiguous()
@@ -246,11 +274,14 @@ class _VertNormalsFn(torch.autograd.Function):
         a = nat.PRNormalsArgs()
         a.verts, a.faces, a.V, a.F = nat.ptr(v), nat.ptr(f), v.shape[0], f.shape[0]
         a.normals, a.raw = nat.ptr(n), nat.ptr(raw)
+        a.vert_corner_start, a.vert_corners = nat.ptr(csr_start), nat.ptr(csr_corners)
         nat.check(lib.pr_vert_normals_fwd(a, nat.stream_of(v)), "pr_vert_normals_fwd")
         ctx.save_for_backward(v, f, raw)
+        ctx.csr = (csr_start, csr_corners)
         return n
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, g):
         from .. import _native as nat
         v, f, raw = ctx.saved_tensors
@@ -260,5 +291,6 @@ class _VertNormalsFn(torch.autograd.Function):
         a = nat.PRNormalsArgs()
         a.verts, a.faces, a.V, a.F = nat.ptr(v), nat.ptr(f), v.shape[0], f.shape[0]
         a.raw, a.grad_normals, a.grad_raw, a.grad_verts = nat.ptr(raw), nat.ptr(gc), nat.ptr(graw), nat.ptr(gv)
+        a.vert_corner_start, a.vert_corners = nat.ptr(ctx.csr[0]), nat.ptr(ctx.csr[1])
         nat.check(lib.pr_vert_normals_bwd(a, nat.stream_of(gc)), "pr_vert_normals_bwd")
-        return gv, None
+        return gv, None, None, None

@@ -24,7 +24,7 @@ def _per_mesh(m, N, name):
 
 class _ProjectFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, verts, faces, first, nfaces, w2v, proj):
+    def forward(ctx, verts, faces, first, nfaces, w2v, proj, csr_start=None, csr_corners=None):
         nat.require_device(verts, faces, w2v, proj)
         lib = nat.load()
         v = verts.detach().to(F32).contiguous()
@@ -39,13 +39,14 @@ class _ProjectFn(torch.autograd.Function):
         a.face_verts = nat.ptr(fv)
         nat.check(lib.pr_project_fwd(a, nat.stream_of(fv)), "pr_project_fwd")
         ctx.save_for_backward(v, f, first, nfaces, m1, m2)
+        ctx.csr = (csr_start, csr_corners)
         return fv
 
     @staticmethod
     def backward(ctx, g):
         v, f, first, nfaces, m1, m2 = ctx.saved_tensors
         if not ctx.needs_input_grad[0]:
-            return None, None, None, None, None, None
+            return (None,) * 8
         lib = nat.load()
         go = g.detach().to(F32).contiguous()
         gv = torch.empty_like(v)
@@ -54,10 +55,15 @@ class _ProjectFn(torch.autograd.Function):
         a.world_to_view, a.proj = nat.ptr(m1), nat.ptr(m2)
         a.V, a.F, a.N = v.shape[0], f.shape[0], first.shape[0]
         a.grad_face_verts, a.grad_verts = nat.ptr(go), nat.ptr(gv)
+        a.vert_corner_start, a.vert_corners = nat.ptr(ctx.csr[0]), nat.ptr(ctx.csr[1])
         nat.check(lib.pr_project_bwd(a, nat.stream_of(go)), "pr_project_bwd")
-        return gv, None, None, None, None, None
+        return (gv,) + (None,) * 7
 
 
-def project_faces(verts_packed, faces_packed, mesh_first_face, mesh_num_faces, world_to_view, proj):
-    """(V,3) world verts -> (F,3,3) face corners (x_ndc, y_ndc, z_view); matrices (N,4,4) row-vector."""
-    return _ProjectFn.apply(verts_packed, faces_packed, mesh_first_face, mesh_num_faces, world_to_view, proj)
+def project_faces(verts_packed, faces_packed, mesh_first_face, mesh_num_faces, world_to_view, proj, csr=None):
+    """(V,3) world verts -> (F,3,3) face corners (x_ndc, y_ndc, z_view); matrices (N,4,4) row-vector.
+    csr: the topology's vertex -> corner index (Meshes.corner_csr()), for the deterministic
+    per-vertex gather backward (else one float atomic per corner component)."""
+    start, corners = csr if csr is not None else (None, None)
+    return _ProjectFn.apply(verts_packed, faces_packed, mesh_first_face, mesh_num_faces, world_to_view, proj,
+                            start, corners)

@@ -85,6 +85,17 @@ def valid_counts(pix_to_face):
     return e[1] if e is not None and e[0] == pix_to_face._version else None
 
 
+def _bwd_workspace(lib, a, device):
+    """Deterministic mode (torch.use_deterministic_algorithms): PR_DETERMINISTIC and its sort
+    workspace on the rasterizer backward's args; None otherwise."""
+    if not nat.deterministic():
+        return None
+    a.flags = a.flags | nat.PR_DETERMINISTIC
+    ws = nat.workspace(lib.pr_rast_bwd_workspace_size(a), device)
+    a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
+    return ws
+
+
 class _RasterizeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, face_verts, first, nfaces, H, W, K, blur, persp, clip, cull, bins=(0, 0)):
@@ -138,12 +149,14 @@ class _RasterizeFn(torch.autograd.Function):
                 setattr(a, name, nat.ptr(g))
         gfv = torch.empty_like(fv)
         a.grad_face_verts = nat.ptr(gfv)
+        ws = _bwd_workspace(lib, a, fv.device)
         timing = _timing.active()
         if timing is not None:
             timing.start("rast_bwd")
         nat.check(lib.pr_rast_bwd(a, nat.stream_of(fv)), "pr_rast_bwd")
         if timing is not None:
             timing.stop("rast_bwd")
+        del ws
         return gfv, None, None, None, None, None, None, None, None, None, None
 
 
@@ -154,7 +167,8 @@ class _ProjectRasterizeFn(torch.autograd.Function):
     forward kernel (no memsets).  Same values as project_faces followed by _RasterizeFn."""
 
     @staticmethod
-    def forward(ctx, verts, faces, first, nfaces, w2v, proj, H, W, K, blur, persp, clip, cull, bins=(0, 0)):
+    def forward(ctx, verts, faces, first, nfaces, w2v, proj, H, W, K, blur, persp, clip, cull, bins=(0, 0),
+                csr_start=None, csr_corners=None):
         from .project import _per_mesh
         nat.require_device(verts, faces, first, nfaces, w2v, proj)
         lib = nat.load()
@@ -194,6 +208,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
             timing.stop("rast_fwd")
         ctx.save_for_backward(v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv)
         ctx.cfg = (H, W, K, float(blur), int(persp), int(clip), int(cull))
+        ctx.csr = (csr_start, csr_corners)
         ctx.prezeroed = True
         ctx.mark_non_differentiable(p2f, counts)
         ctx.set_materialize_grads(False)
@@ -203,7 +218,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
     def backward(ctx, gp2f, gzbuf, gbary, gdists, gcounts):
         v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv = ctx.saved_tensors
         if gfv is None:
-            return (None,) * 14
+            return (None,) * 16
         H, W, K, blur, persp, clip, cull = ctx.cfg
         # a second backward (retain_graph) finds the accumulators used: zero them again
         flags = nat.PR_GRAD_PREZEROED if ctx.prezeroed else 0
@@ -221,19 +236,22 @@ class _ProjectRasterizeFn(torch.autograd.Function):
                 keep.append(g)
                 setattr(a, name, nat.ptr(g))
         a.grad_face_verts = nat.ptr(gfv)
+        ws = _bwd_workspace(lib, a, fv.device)
         timing = _timing.active()
         if timing is not None:
             timing.start("rast_bwd")
         nat.check(lib.pr_rast_bwd(a, nat.stream_of(fv)), "pr_rast_bwd")
         if timing is not None:
             timing.stop("rast_bwd")
+        del ws
         pa = nat.PRProjectArgs()
         pa.verts, pa.faces, pa.mesh_first_face, pa.mesh_num_faces = nat.ptr(v), nat.ptr(f), nat.ptr(first), nat.ptr(nfaces)
         pa.world_to_view, pa.proj = nat.ptr(m1), nat.ptr(m2)
         pa.V, pa.F, pa.N = v.shape[0], f.shape[0], first.shape[0]
         pa.grad_face_verts, pa.grad_verts, pa.flags = nat.ptr(gfv), nat.ptr(gv), flags
+        pa.vert_corner_start, pa.vert_corners = nat.ptr(ctx.csr[0]), nat.ptr(ctx.csr[1])
         nat.check(lib.pr_project_bwd(pa, nat.stream_of(gv)), "pr_project_bwd")
-        return (gv,) + (None,) * 13
+        return (gv,) + (None,) * 15
 
 
 def rasterize_meshes(meshes, image_size=256, blur_radius=0.0, faces_per_pixel=8, bin_size=None,
@@ -296,7 +314,8 @@ class MeshRasterizer(torch.nn.Module):
                 meshes_world.verts_packed(), faces, first, nfaces,
                 cameras.world_to_view_matrix(), cameras.projection_matrix(), H, W, int(rs.faces_per_pixel),
                 float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces),
-                bin_params(rs.bin_size, rs.max_faces_per_bin, H, W, faces.shape[0], first.shape[0]))
+                bin_params(rs.bin_size, rs.max_faces_per_bin, H, W, faces.shape[0], first.shape[0]),
+                *meshes_world.corner_csr("gather"))
             return Fragments(pix_to_face=attach_valid_counts(p2f, counts), zbuf=zbuf, bary_coords=bary, dists=dists)
         meshes_screen = self.transform(meshes_world, **kwargs)
         p2f, zbuf, bary, dists = rasterize_meshes(

@@ -114,7 +114,13 @@ class _ShadeFn(torch.autograd.Function):
         else:
             a.grad_maps = nat.ptr(gt)
         a.grad_light, a.grad_camera = nat.ptr(gl), nat.ptr(gc)
+        ws = None
+        if nat.deterministic():  # torch.use_deterministic_algorithms: in-order sums, no float atomics
+            a.flags = nat.PR_DETERMINISTIC
+            ws = nat.workspace(lib.pr_shade_bwd_workspace_size(a), g.device)
+            a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         nat.check(lib.pr_shade_bwd(a, nat.stream_of(g)), "pr_shade_bwd")
+        del ws
         return gb, gv, gn, gt, gl, gc, None
 
 

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 import rast_kat
+from conftest import assert_close
 from oracle import rast_ref
 from pertrenderer_amd.renderer.rasterizer import _rasterize, valid_counts
 
@@ -44,6 +45,21 @@ def test_hip_rasterizer_backward_matches_fd_pinned_oracle(persp, clip, device):
     gd = rng.standard_normal((1, H, W, K)) * valid
     T = lambda a: torch.tensor(a, dtype=torch.float32, device=device)
     ((zbuf * T(gz)).sum() + (bary * T(gb)).sum() + (dists * T(gd)).sum()).backward()
+    got = fv.grad.cpu().numpy()
+    # the fp32 oracle, at the 1e-5 bar (the default backward sums faces with float atomics) and bit
+    # for bit in deterministic mode (slot-order face sums)
+    gz32, gb32, gd32 = (x.astype(np.float32) for x in (gz, gb, gd))
+    ref32 = rast_ref.rast_bwd(case["fv"], p, gz32, gb32, gd32, persp, clip)
+    assert_close(got, ref32, name="d face_verts vs fp32 oracle")
+    old = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        fvd, (_, zd, bd, dd) = _native(case, device, requires_grad=True)
+        (gdet,) = torch.autograd.grad((zd * T(gz)).sum() + (bd * T(gb)).sum() + (dd * T(gd)).sum(), fvd)
+    finally:
+        torch.use_deterministic_algorithms(old)
+    np.testing.assert_array_equal(gdet.cpu().numpy(), ref32)
+    # and the fp64 oracle (pinned by central differences, test_rast_oracle.py): the fp32 rounding of
+    # the same formulas (edge functions of nearby points cancel: the absolute bound is the scale)
     ref = rast_ref.rast_bwd(fv64, p, gz, gb, gd, persp, clip, dtype=np.float64)
-    got = fv.grad.cpu().numpy().astype(np.float64)
-    np.testing.assert_allclose(got, ref, rtol=1e-3, atol=1e-4 * np.abs(ref).max())
+    np.testing.assert_allclose(got.astype(np.float64), ref, rtol=1e-3, atol=1e-4 * np.abs(ref).max())

@@ -12,7 +12,7 @@ import pytest
 import torch
 import torch.nn.functional as Fn
 
-from conftest import ROOT
+from conftest import ROOT, assert_close
 from pertrenderer_amd.renderer import (FoVPerspectiveCameras, Materials, MeshRasterizer, Meshes, PointLights,
                                        RasterizationSettings, TexturesUV, TexturesVertex, load_obj,
                                        look_at_view_transform)
@@ -30,18 +30,18 @@ def _interp64(p2f, bary, attr, faces):
     return out * mask
 
 
-def _uv_sample64(p2f, bary, tex):
-    uv = _interp64(p2f, bary, torch.cat([tex.verts_uvs_list()[0]]), tex.faces_uvs_list()[0])
+def _uv_sample64(p2f, bary, tex, dtype=torch.float64):
+    uv = _interp64(p2f, bary, torch.cat([tex.verts_uvs_list()[0]]).to(dtype), tex.faces_uvs_list()[0])
     N, Ho, Wo, K = p2f.shape
-    maps = tex.maps_padded().double()
+    maps = tex.maps_padded().to(dtype)
     m = torch.flip(maps.permute(0, 3, 1, 2), [2])
     g = uv.reshape(N, Ho, Wo * K, 2) * 2.0 - 1.0
     t = Fn.grid_sample(m, g, align_corners=True, padding_mode="border")
     return t.reshape(N, 3, Ho, Wo, K).permute(0, 2, 3, 4, 1)
 
 
-def _reference64(mesh, frag, lights, cams, mats, texels):
-    d = lambda t: t.double()
+def _reference64(mesh, frag, lights, cams, mats, texels, dtype=torch.float64):
+    d = lambda t: t.to(dtype)
     verts, faces = d(mesh.verts_packed()), mesh.faces_packed()
     # area-weighted vertex normals in float64 (Meshes.verts_normals_packed)
     fv = verts[faces]
@@ -166,3 +166,35 @@ def test_renderer_uses_native_shading(device):
         shm._ShadeFn.apply = orig
     from pertrenderer_amd import _native as nat
     assert calls == [nat.PR_TEX_UV]
+
+
+@pytest.mark.parametrize("kind", ["vertex", "uv"])
+def test_native_shading_matches_float32_composition(kind, device):
+    """At the reference's own precision: the same torch composition in float32 (PyTorch3D's
+    phong_shading op order), with the deterministic-order backward (torch.use_deterministic_
+    algorithms: per-vertex / per-texel sums in slot order).  Colours and the shading's own
+    gradients (barycentrics, vertices, light, vertex colours / texture map) at the 1e-5 bar; the
+    fragments are fixed inputs here (the rasterizer backward has its own bitwise oracle tests:
+    composed with it, ulp-level d bary differences are amplified by the 1 / face-area factors)."""
+    from pertrenderer_amd.renderer.rasterizer import Fragments
+    old = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        mesh, frag, lights, cams, mats, verts, loc, extra = _scene(device, kind)
+        b = frag.bary_coords.detach().clone().requires_grad_(True)
+        fr = Fragments(frag.pix_to_face, frag.zbuf.detach(), b, frag.dists.detach())
+        vd = verts.detach().clone().requires_grad_(True)
+        m = Meshes([vd], [mesh.faces_packed()], mesh.textures)
+        out = sh.textured_phong_shading(m, fr, lights, cams, mats)
+        ref_tex = (_uv_sample64(fr.pix_to_face, b, m.textures, torch.float32) if kind == "uv"
+                   else _interp64(fr.pix_to_face, b, extra, m.faces_packed()))
+        ref = _reference64(m, fr, lights, cams, mats, ref_tex, dtype=torch.float32)
+        assert_close(out, ref, name="colors")
+        G = torch.randn(out.shape, device=device, generator=torch.Generator(device).manual_seed(5))
+        G = G * (frag.pix_to_face >= 0)[..., None]
+        leaves = [b, vd, loc, extra]
+        names = ("bary", "verts", "light", "texture" if kind == "uv" else "vertex colours")
+        for name, x, y in zip(names, _grads(out, G, leaves), _grads(ref, G, leaves)):
+            assert_close(x, y, name=name)
+    finally:
+        torch.use_deterministic_algorithms(old)
