@@ -8,6 +8,7 @@ gfx950 (libpertrender.so, C ABI in include/pertrender.h).
 """
 from . import _native
 from .blend import perturbed_aggregate, perturbed_blend, perturbed_blend_vertex, perturbed_heaviside, soft_blend
+from .multidevice import activate_from_env as _activate_sample_devices
 from .multidevice import sample_devices, set_sample_devices
 from .noise import Noise, get_noise_source, set_noise_source
 from .random_rasterizer import (RandomPhongShader, RandomSimpleShader, SimpleShader, SoftSimpleShader,
@@ -16,6 +17,10 @@ from .smoothagg import CauchyAgg, GaussianAgg, GaussianAgg_wovr, HardAgg, SoftAg
 from .smoothrast import AffineRast, ArctanRast, GaussianRast, GaussianRast_wovr, HardRast, SoftRast
 
 __version__ = "0.1.0"
+
+# PR_SAMPLE_DEVICES (e.g. "all"): shard every native Monte-Carlo blend's samples over the listed
+# devices from import on (multidevice.py), so eval.py runs unchanged on a multi-GPU node
+_activate_sample_devices()
 
 
 def native_library():

@@ -207,6 +207,25 @@ def stream_of(t):
     return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+_get_device = getattr(torch._C, "_cuda_getDevice", None) or torch.cuda.current_device
+
+
+def call(name, what, t, *args):
+    """Run C-ABI entry `name`(*args, stream) on `t`'s device: the stream is that device's current
+    torch stream, and when `t` lives on another device than the current one (in-process sample
+    sharding over devices, multidevice.py) the call runs under a device guard, so every launch,
+    memset and error query of the library addresses `t`'s device.  Raises NativeError on a
+    non-zero status."""
+    fn = getattr(load(), name)
+    idx = t.device.index
+    if idx is not None and idx != _get_device():
+        with torch.cuda.device(idx):
+            code = fn(*args, stream_of(t))
+    else:
+        code = fn(*args, stream_of(t))
+    check(code, what)
+
+
 def deterministic():
     """Deterministic-order backward passes (PR_DETERMINISTIC), switched with torch's own
     ``torch.use_deterministic_algorithms(True)``: the sums the fast kernels scatter with float

@@ -24,8 +24,18 @@ F32 = torch.float32
 _ABS = 1 << 63  # absolute-key marker (see PRBlendParams.seeds)
 
 
+_PLANE_CACHE = {}
+
+
 def _planes(z, N, device):
-    """znear / zfar as an (N,) float32 device tensor (accepts float, (N,), (N,1,1,1))."""
+    """znear / zfar as an (N,) float32 device tensor (accepts float, (N,), (N,1,1,1)).  Plain
+    floats (the cameras' defaults) are made once per (value, N, device): no fill kernel per render."""
+    if not torch.is_tensor(z):
+        key = (float(z), N, str(device))
+        t = _PLANE_CACHE.get(key)
+        if t is None:
+            t = _PLANE_CACHE[key] = torch.full((N,), float(z), dtype=F32, device=device)
+        return t
     if torch.is_tensor(z):
         z = z.detach().to(device=device, dtype=F32).reshape(-1)
         if z.numel() == 1:
@@ -193,7 +203,7 @@ class _FusedBlendFn(torch.autograd.Function):
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
         a.pix_count = nat.ptr(cfg["counts"])
-        _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
+        _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
         ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, cache)
         ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
@@ -222,7 +232,7 @@ class _FusedBlendFn(torch.autograd.Function):
         a.pix_count = nat.ptr(cfg["counts"])
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
-        _timed("blend_bwd", lambda: nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd"))
+        _timed("blend_bwd", lambda: nat.call("pr_blend_bwd", "pr_blend_bwd", g, a))
         need = ctx.needs_input_grad
         s_g, g_g, a_g = _scalar_grads(gsc, need[3:6], ctx.refs)
         return (gd if need[0] else None, gz if need[1] else None, gc if need[2] else None,
@@ -258,7 +268,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         a.bary, a.faces, a.vert_colors = nat.ptr(b_c), nat.ptr(f_c), nat.ptr(v_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
         a.pix_count = nat.ptr(cfg["counts"])
-        _timed("blend_fwd", lambda: nat.check(lib.pr_blend_fwd(a, nat.stream_of(image)), "pr_blend_fwd"))
+        _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
         ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache)
         ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc, ctx.flags = cfg, noise, sc, flags
@@ -290,7 +300,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         a.pix_count = nat.ptr(cfg["counts"])
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
-        _timed("blend_bwd", lambda: nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd"))
+        _timed("blend_bwd", lambda: nat.call("pr_blend_bwd", "pr_blend_bwd", g, a))
         s_g, g_g, a_g = _scalar_grads(gsc, need[4:7], ctx.refs)
         return (gd if need[0] else None, gz if need[1] else None, gb if need[2] else None, gv,
                 s_g, g_g, a_g, None, None, None, None, None)
@@ -388,7 +398,7 @@ class _HeavisideFn(torch.autograd.Function):
         a = _heaviside_args(tuple(d_c.shape), Sr, noise, sv, sdev, d_c, flags)
         prob = torch.empty_like(d_c)
         a.prob = nat.ptr(prob)
-        nat.check(lib.pr_heaviside_fwd(a, nat.stream_of(prob)), "pr_heaviside_fwd")
+        nat.call("pr_heaviside_fwd", "pr_heaviside_fwd", prob, a)
         ctx.save_for_backward(d_c)
         ctx.sdev = sdev
         ctx.noise, ctx.Sr, ctx.sv, ctx.sigma_ref, ctx.flags = noise, int(Sr), sv, sigma, flags
@@ -406,7 +416,7 @@ class _HeavisideFn(torch.autograd.Function):
         a.grad_prob, a.grad_dists, a.grad_sigma = nat.ptr(g), nat.ptr(gd), nat.ptr(gs)
         ws = torch.empty(max(1, lib.pr_heaviside_bwd_workspace_size(a)), dtype=torch.uint8, device=d_c.device)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
-        nat.check(lib.pr_heaviside_bwd(a, nat.stream_of(g)), "pr_heaviside_bwd")
+        nat.call("pr_heaviside_bwd", "pr_heaviside_bwd", g, a)
         need = ctx.needs_input_grad
         ref = ctx.sigma_ref
         sg = gs[0].to(ref.dtype) if (need[1] and torch.is_tensor(ref)) else None
@@ -446,7 +456,7 @@ class _AggregateFn(torch.autograd.Function):
         a.p = p
         a.mask, a.prob, a.zbuf = nat.ptr(m_c), nat.ptr(p_c), nat.ptr(z_c)
         a.weights, a.winners = nat.ptr(weights), nat.ptr(winners)
-        nat.check(lib.pr_blend_fwd(a, nat.stream_of(weights)), "pr_blend_fwd(aggregate)")
+        nat.call("pr_blend_fwd", "pr_blend_fwd(aggregate)", weights, a)
         ctx.save_for_backward(z_c, p_c, m_c, zn, zf, winners)
         ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc, ctx.refs = cfg, noise, sc, (gamma, alpha)
@@ -472,7 +482,7 @@ class _AggregateFn(torch.autograd.Function):
         a.grad_weights, a.grad_prob, a.grad_zbuf, a.grad_scalars = nat.ptr(g), nat.ptr(gp), nat.ptr(gz), nat.ptr(gsc)
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
-        nat.check(lib.pr_blend_bwd(a, nat.stream_of(g)), "pr_blend_bwd(aggregate)")
+        nat.call("pr_blend_bwd", "pr_blend_bwd(aggregate)", g, a)
         need = ctx.needs_input_grad
         _, g_g, a_g = _scalar_grads(gsc, (False, need[2], need[3]), (None,) + ctx.refs)
         return (gz if need[0] else None, gp if need[1] else None, g_g, a_g, None, None, None, None)

@@ -3,7 +3,8 @@ backend", §8(e) exact mode) for callers that stay one process, as eval.py does 
 ``cuda:0``, experiments/eval.py:112-114).
 
     import pertrenderer_amd as pa
-    pa.set_sample_devices(["cuda:0", "cuda:1", ...])   # eval.py unchanged otherwise
+    pa.set_sample_devices(["cuda:0", "cuda:1", ...])
+    # or, with eval.py's source unchanged:  PR_SAMPLE_DEVICES=all python experiments/eval.py
 
 Every ``smooth_rgb_blend`` of a native Monte-Carlo pair (GaussianRast / ArctanRast /
 *_wovr x GaussianAgg / CauchyAgg / *_wovr) then splits its Sr rast and Sa agg samples over
@@ -24,6 +25,8 @@ devices are distinct GPUs; logical shards on one device (tests, one-GPU boxes) c
 This is the north star's sample partition without torchrun; the torchrun paths
 (``parallel.py``, bench.py) remain the measured multi-GPU configuration.
 """
+import os
+
 import torch
 import torch.cuda.comm as _comm
 
@@ -51,6 +54,33 @@ def set_sample_devices(devices):
 
 def sample_devices():
     return _DEVICES
+
+
+def devices_from_env(value=None):
+    """The device list of PR_SAMPLE_DEVICES ("all", a count "8", or a list "0,1,2,3" /
+    "cuda:0,cuda:1"), or None when unset / empty.  Counting devices does not initialise HIP."""
+    value = os.environ.get("PR_SAMPLE_DEVICES", "") if value is None else value
+    value = value.strip()
+    if not value:
+        return None
+    if value.lower() == "all":
+        n = torch.cuda.device_count()
+        return [f"cuda:{i}" for i in range(n)] if n > 1 else None
+    if value.isdigit():
+        n = min(int(value), torch.cuda.device_count())
+        return [f"cuda:{i}" for i in range(n)] if n > 1 else None
+    items = [v.strip() for v in value.split(",") if v.strip()]
+    return [v if v.startswith("cuda") else f"cuda:{int(v)}" for v in items]
+
+
+def activate_from_env():
+    """set_sample_devices(PR_SAMPLE_DEVICES), run at import: eval.py (which pins cuda:0 and stays
+    one process, eval.py:112-116) shards its Monte-Carlo samples over the node's GPUs with no
+    change to its source -- `PR_SAMPLE_DEVICES=all python experiments/eval.py ...`."""
+    devs = devices_from_env()
+    if devs is not None:
+        set_sample_devices(devs)
+    return devs
 
 
 def _distinct(devs):

@@ -94,8 +94,7 @@ class DeviceSeed:
         return i
 
     def advance(self):
-        nat.check(nat.load().pr_seed_advance(nat.ptr(self.tensor), 1, nat.stream_of(self.tensor)),
-                  "pr_seed_advance")
+        nat.call("pr_seed_advance", "pr_seed_advance", self.tensor, nat.ptr(self.tensor), 1)
         self._next = 1
 
 

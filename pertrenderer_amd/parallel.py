@@ -128,7 +128,7 @@ def exact_sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, n
     `nb_samples_*` GLOBAL samples split across the ranks of `group` (sample_shard): the
     image and the gradients of colors, dists and zbuf equal the single-process full-S
     result up to fp summation order (P and W are exact: counts).  Call reduce_scalar_grads
-    after each backward for sigma / gamma / alpha (their leaves are CPU tensors: a collective
+    after each backward for sigma / gamma / alpha (tracked here; their leaves are CPU tensors: a collective
     inside their backward nodes would run on autograd's CPU thread, unordered against the
     device-thread collectives, so the ranks could disagree on the collective order)."""
     from .blend import perturbed_aggregate, perturbed_heaviside
@@ -140,6 +140,7 @@ def exact_sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, n
         raise ValueError(f"exact sharding needs >= 1 sample per rank (Sr={nb_samples_rast}, "
                          f"Sa={nb_samples_agg}, world={world})")
     K = dists.shape[-1]
+    track_scalar_grads([t for t in (sigma, gamma, alpha) if torch.is_tensor(t)])
     mask = pix_to_face >= 0
     d_in = _SumBackward.apply(dists, group)
     z_in = _SumBackward.apply(zbuf, group)
@@ -155,26 +156,50 @@ def exact_sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, n
     return torch.cat([rgb, a], dim=-1)
 
 
+def track_scalar_grads(params):
+    """Record, per smoothing leaf, the gradient each backward delivers to it (a tensor hook), so
+    reduce_scalar_grads completes exactly what arrived since its last call -- whatever the caller
+    did to ``.grad`` in between.  eval.py replaces sigma / gamma / alpha.grad with zeros after
+    every iteration past 100 (eval.py:386) and optimizer.zero_grad() resets grads too; a
+    subtraction of the last reduced total would then be wrong.  Idempotent;
+    exact_sharded_blend calls it for its leaves."""
+    for p in params:
+        if p is None or not p.requires_grad or not p.is_leaf or getattr(p, "_pr_tracked", False):
+            continue
+
+        def hook(g, p=p):
+            g = g.detach().reshape(()).to(torch.float32)
+            p._pr_pending = g.clone() if p._pr_pending is None else p._pr_pending + g.to(p._pr_pending.device)
+
+        p._pr_pending = None
+        p.register_hook(hook)
+        p._pr_tracked = True
+
+
 def reduce_scalar_grads(params, group=None):
     """Exact mode: complete the smoothing scalars' gradients after a backward.  Each rank holds
-    its shard's partial sum; only what was accumulated since this function last saw the leaf is
-    all-reduced (SUM), so a leaf that is never zeroed -- the reference's sigma / gamma / alpha
-    are not, eval.py:382-388 -- accumulates exactly the single-process gradient per backward
-    instead of re-reducing its history.  One collective for all leaves, staged on the device
-    for RCCL (the leaves are CPU 0-d tensors)."""
+    its shard's partial; the partials that backward delivered to a leaf since the last call
+    (track_scalar_grads) are all-reduced (SUM) and the other ranks' share is added to ``.grad``,
+    so the leaf ends as in one process whether it accumulates across iterations or is zeroed /
+    replaced in between (eval.py:382-388).  An untracked leaf's whole ``.grad`` counts as this
+    backward's partial.  One collective for all leaves, staged on the device for RCCL (the
+    leaves are CPU 0-d tensors)."""
     leaves = [p for p in params if p is not None and p.grad is not None]
     if not leaves:
         return
-    deltas = []
+    local = []
     for p in leaves:
-        seen = getattr(p, "_pr_reduced_grad", None)
-        g = p.grad.detach().reshape(()).to(torch.float32)
-        deltas.append(g - seen if seen is not None and seen.device == g.device else g)
-    flat = torch.stack(deltas)
+        if getattr(p, "_pr_tracked", False):
+            pend = p._pr_pending
+            local.append(pend if pend is not None else torch.zeros((), dtype=torch.float32))
+        else:
+            local.append(p.grad.detach().reshape(()).to(torch.float32))
+    dev = local[0].device
+    flat = torch.stack([t.to(dev) for t in local])
+    mine = flat.clone()
     _all_reduce_sum(flat, group)
-    for p, d in zip(leaves, flat):
-        seen = getattr(p, "_pr_reduced_grad", None)
-        base = seen if seen is not None and seen.device == p.grad.device else torch.zeros_like(d)
-        total = (base.to(d.device) + d).to(p.grad.dtype)
-        p.grad.copy_(total.reshape(p.grad.shape).to(p.grad.device))
-        p._pr_reduced_grad = p.grad.detach().reshape(()).to(torch.float32).clone()
+    for p, total, own in zip(leaves, flat, mine):
+        with torch.no_grad():
+            p.grad.add_((total - own).to(p.grad.device, p.grad.dtype).reshape(p.grad.shape))
+        if getattr(p, "_pr_tracked", False):
+            p._pr_pending = None

@@ -26,7 +26,7 @@ class _InterpFn(torch.autograd.Function):
         a.PK, a.D, a.out = p2f_c.numel(), D, nat.ptr(out)
         a.F = fc.shape[0] if fc is not None else fa.shape[0]
         a.faces, a.V = nat.ptr(fc), (fa.shape[0] if fc is not None else 0)
-        nat.check(lib.pr_interp_fwd(a, nat.stream_of(out)), "pr_interp_fwd")
+        nat.call("pr_interp_fwd", "pr_interp_fwd", out, a)
         ctx.save_for_backward(b_c, fa, p2f_c, fc)
         return out
 
@@ -46,7 +46,7 @@ class _InterpFn(torch.autograd.Function):
         a.F = fc.shape[0] if fc is not None else fa.shape[0]
         a.faces, a.V = nat.ptr(fc), (fa.shape[0] if fc is not None else 0)
         a.grad_out, a.grad_bary, a.grad_face_attr = nat.ptr(go), nat.ptr(gb), nat.ptr(gf)
-        nat.check(lib.pr_interp_bwd(a, nat.stream_of(go)), "pr_interp_bwd")
+        nat.call("pr_interp_bwd", "pr_interp_bwd", go, a)
         return gb, gf, None, None
 
 

@@ -275,7 +275,7 @@ class _VertNormalsFn(torch.autograd.Function):
         a.verts, a.faces, a.V, a.F = nat.ptr(v), nat.ptr(f), v.shape[0], f.shape[0]
         a.normals, a.raw = nat.ptr(n), nat.ptr(raw)
         a.vert_corner_start, a.vert_corners = nat.ptr(csr_start), nat.ptr(csr_corners)
-        nat.check(lib.pr_vert_normals_fwd(a, nat.stream_of(v)), "pr_vert_normals_fwd")
+        nat.call("pr_vert_normals_fwd", "pr_vert_normals_fwd", v, a)
         ctx.save_for_backward(v, f, raw)
         ctx.csr = (csr_start, csr_corners)
         return n
@@ -292,5 +292,5 @@ class _VertNormalsFn(torch.autograd.Function):
         a.verts, a.faces, a.V, a.F = nat.ptr(v), nat.ptr(f), v.shape[0], f.shape[0]
         a.raw, a.grad_normals, a.grad_raw, a.grad_verts = nat.ptr(raw), nat.ptr(gc), nat.ptr(graw), nat.ptr(gv)
         a.vert_corner_start, a.vert_corners = nat.ptr(ctx.csr[0]), nat.ptr(ctx.csr[1])
-        nat.check(lib.pr_vert_normals_bwd(a, nat.stream_of(gc)), "pr_vert_normals_bwd")
+        nat.call("pr_vert_normals_bwd", "pr_vert_normals_bwd", gc, a)
         return gv, None, None, None

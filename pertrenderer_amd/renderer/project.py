@@ -37,7 +37,7 @@ class _ProjectFn(torch.autograd.Function):
         a.V, a.F, a.N = v.shape[0], f.shape[0], N
         fv = torch.empty((f.shape[0], 3, 3), dtype=F32, device=v.device)
         a.face_verts = nat.ptr(fv)
-        nat.check(lib.pr_project_fwd(a, nat.stream_of(fv)), "pr_project_fwd")
+        nat.call("pr_project_fwd", "pr_project_fwd", fv, a)
         ctx.save_for_backward(v, f, first, nfaces, m1, m2)
         ctx.csr = (csr_start, csr_corners)
         return fv
@@ -56,7 +56,7 @@ class _ProjectFn(torch.autograd.Function):
         a.V, a.F, a.N = v.shape[0], f.shape[0], first.shape[0]
         a.grad_face_verts, a.grad_verts = nat.ptr(go), nat.ptr(gv)
         a.vert_corner_start, a.vert_corners = nat.ptr(ctx.csr[0]), nat.ptr(ctx.csr[1])
-        nat.check(lib.pr_project_bwd(a, nat.stream_of(go)), "pr_project_bwd")
+        nat.call("pr_project_bwd", "pr_project_bwd", go, a)
         return (gv,) + (None,) * 7
 
 

@@ -122,7 +122,7 @@ class _RasterizeFn(torch.autograd.Function):
         timing = _timing.active()
         if timing is not None:
             timing.start("rast_fwd")
-        nat.check(lib.pr_rast_fwd(a, nat.stream_of(fv)), "pr_rast_fwd")
+        nat.call("pr_rast_fwd", "pr_rast_fwd", fv, a)
         if timing is not None:
             timing.stop("rast_fwd")
         ctx.save_for_backward(fv, first, nfaces, p2f, counts)
@@ -153,7 +153,7 @@ class _RasterizeFn(torch.autograd.Function):
         timing = _timing.active()
         if timing is not None:
             timing.start("rast_bwd")
-        nat.check(lib.pr_rast_bwd(a, nat.stream_of(fv)), "pr_rast_bwd")
+        nat.call("pr_rast_bwd", "pr_rast_bwd", fv, a)
         if timing is not None:
             timing.stop("rast_bwd")
         del ws
@@ -203,7 +203,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         timing = _timing.active()
         if timing is not None:
             timing.start("rast_fwd")
-        nat.check(lib.pr_project_rast_fwd(pa, a, nat.stream_of(fv)), "pr_project_rast_fwd")
+        nat.call("pr_project_rast_fwd", "pr_project_rast_fwd", fv, pa, a)
         if timing is not None:
             timing.stop("rast_fwd")
         ctx.save_for_backward(v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv)
@@ -240,7 +240,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         timing = _timing.active()
         if timing is not None:
             timing.start("rast_bwd")
-        nat.check(lib.pr_rast_bwd(a, nat.stream_of(fv)), "pr_rast_bwd")
+        nat.call("pr_rast_bwd", "pr_rast_bwd", fv, a)
         if timing is not None:
             timing.stop("rast_bwd")
         del ws
@@ -250,7 +250,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         pa.V, pa.F, pa.N = v.shape[0], f.shape[0], first.shape[0]
         pa.grad_face_verts, pa.grad_verts, pa.flags = nat.ptr(gfv), nat.ptr(gv), flags
         pa.vert_corner_start, pa.vert_corners = nat.ptr(ctx.csr[0]), nat.ptr(ctx.csr[1])
-        nat.check(lib.pr_project_bwd(pa, nat.stream_of(gv)), "pr_project_bwd")
+        nat.call("pr_project_bwd", "pr_project_bwd", gv, pa)
         return (gv,) + (None,) * 15
 
 

@@ -88,7 +88,7 @@ class _ShadeFn(torch.autograd.Function):
         colors = torch.empty((N, H, W, K, 3), dtype=F32, device=bary.device)
         a = _args(cfg, keep)
         a.colors = nat.ptr(colors)
-        nat.check(lib.pr_shade_fwd(a, nat.stream_of(colors)), "pr_shade_fwd")
+        nat.call("pr_shade_fwd", "pr_shade_fwd", colors, a)
         ctx.save_for_backward(*keep.values())
         ctx.cfg = cfg
         return colors
@@ -119,7 +119,7 @@ class _ShadeFn(torch.autograd.Function):
             a.flags = nat.PR_DETERMINISTIC
             ws = nat.workspace(lib.pr_shade_bwd_workspace_size(a), g.device)
             a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
-        nat.check(lib.pr_shade_bwd(a, nat.stream_of(g)), "pr_shade_bwd")
+        nat.call("pr_shade_bwd", "pr_shade_bwd", g, a)
         del ws
         return gb, gv, gn, gt, gl, gc, None
 

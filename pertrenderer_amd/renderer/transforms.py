@@ -22,7 +22,7 @@ class _SO3ExpFn(torch.autograd.Function):
         R = torch.empty((w.shape[0], 3, 3), dtype=F32, device=w.device)
         a = nat.PRSO3Args()
         a.N, a.eps, a.log_rot, a.R = w.shape[0], float(eps), nat.ptr(w), nat.ptr(R)
-        nat.check(lib.pr_so3_exp_fwd(a, nat.stream_of(R)), "pr_so3_exp_fwd")
+        nat.call("pr_so3_exp_fwd", "pr_so3_exp_fwd", R, a)
         ctx.save_for_backward(w)
         ctx.eps = eps
         return R
@@ -35,7 +35,7 @@ class _SO3ExpFn(torch.autograd.Function):
         gw = torch.empty_like(w)
         a = nat.PRSO3Args()
         a.N, a.eps, a.log_rot, a.grad_R, a.grad_log_rot = w.shape[0], float(ctx.eps), nat.ptr(w), nat.ptr(g), nat.ptr(gw)
-        nat.check(lib.pr_so3_exp_bwd(a, nat.stream_of(gw)), "pr_so3_exp_bwd")
+        nat.call("pr_so3_exp_bwd", "pr_so3_exp_bwd", gw, a)
         return gw, None
 
 
@@ -49,7 +49,7 @@ class _RotateFn(torch.autograd.Function):
         a = nat.PRRotateArgs()
         a.N, a.P, a.R_batched = p.shape[0], p.shape[1], int(r.shape[0] > 1)
         a.points, a.R, a.out = nat.ptr(p), nat.ptr(r), nat.ptr(out)
-        nat.check(lib.pr_rotate_fwd(a, nat.stream_of(out)), "pr_rotate_fwd")
+        nat.call("pr_rotate_fwd", "pr_rotate_fwd", out, a)
         ctx.save_for_backward(p, r)
         return out
 
@@ -64,7 +64,7 @@ class _RotateFn(torch.autograd.Function):
         a = nat.PRRotateArgs()
         a.N, a.P, a.R_batched = p.shape[0], p.shape[1], int(r.shape[0] > 1)
         a.points, a.R, a.grad_out, a.grad_points, a.grad_R = nat.ptr(p), nat.ptr(r), nat.ptr(g), nat.ptr(gp), nat.ptr(gr)
-        nat.check(lib.pr_rotate_bwd(a, nat.stream_of(g)), "pr_rotate_bwd")
+        nat.call("pr_rotate_bwd", "pr_rotate_bwd", g, a)
         return gp, gr
 
 

@@ -53,12 +53,19 @@ def _worker(rank, world, port, S, out_path):
         reduce_scalar_grads([s, gm, al])
         out = dict(image=img.detach().cpu(), dists=d.grad.cpu(), zbuf=z.grad.cpu(), colors=c.grad.cpu(),
                    scalars=torch.stack([s.grad, gm.grad, al.grad]))
-        # a second backward without zeroing (eval.py never zeroes the smoothing leaves): the
-        # leaves accumulate exactly twice the one-backward gradient, as in one process
+        # a second backward without zeroing (eval.py's first 100 iterations accumulate the
+        # smoothing leaves, eval.py:382-385): exactly twice the one-backward gradient
         img = exact_sharded_blend(c, p2f, d, z, s, gm, al, S, S, SEEDS[0], SEEDS[1], background=(0.1, 0.2, 0.3))
         (img * gimg).sum().backward()
         reduce_scalar_grads([s, gm, al])
         out["scalars2"] = torch.stack([s.grad, gm.grad, al.grad])
+        # then eval.py:386's reset (grads replaced by zeros) before a third backward: one gradient
+        for t in (s, gm, al):
+            t.grad = torch.zeros_like(t)
+        img = exact_sharded_blend(c, p2f, d, z, s, gm, al, S, S, SEEDS[0], SEEDS[1], background=(0.1, 0.2, 0.3))
+        (img * gimg).sum().backward()
+        reduce_scalar_grads([s, gm, al])
+        out["scalars3"] = torch.stack([s.grad, gm.grad, al.grad])
         if world == 1:  # the fused kernel pair with the same keys
             p2f, d, z, c, gimg, (s, gm, al), S = _inputs(dev, S)
             img = perturbed_blend(c, p2f, d, z, s, gm, al, S, S, background=(0.1, 0.2, 0.3),
@@ -96,6 +103,7 @@ def test_exact_shards_match_single_process(world, S):
         _close(many[k], one[k], name=k)
     _close(many["scalars"], one["scalars"], rtol=2e-5, name="scalars")
     _close(many["scalars2"], 2 * one["scalars"], rtol=2e-5, name="accumulated scalars")
+    _close(many["scalars3"], one["scalars"], rtol=2e-5, name="scalars after the eval.py:386 reset")
 
 
 def test_exact_mode_composition_matches_fused_blend():

@@ -73,3 +73,29 @@ def test_compare_runtime_tables(tmp_path, device, mode):
     assert params["MC"] == [4, 8] and params["lr-smoothing-MC"] == [(5e-2, 1e-3, 1e-2, 4), (5e-2, 1e-3, 1e-2, 8)]
     on_disk = json.load(open(tmp_path / "runtimes.txt")), json.load(open(tmp_path / "memory.txt"))
     assert on_disk[0] == rt and on_disk[1] == mem
+
+
+def test_cfg5_full_size_graph_runs(device):
+    """BASELINE cfg 5 at its size: eval.py's pose benchmark (compare_pose_opt's problems,
+    optimize_pose with the adaptive schedule, eval.py:320-409, 576-690) at 256 x 256 for the full
+    800 iterations, graph mode, both default renderers, 2 problems: every run improves on its
+    20-degree start and the tables have the reference's layout (the 100-problem run is
+    profiles/r2_cfg5.json)."""
+    torch.manual_seed(0)
+    scene = pose_opt.Scene(device, 256)
+    probs = pose_opt.make_problems(scene, 2, NOISE, 20.0)
+    torch.manual_seed(1)
+    per = [pose_opt.run_problem(scene, p, NOISE, 1e-3, 1e-2, 8, 20.0, 800, True, (1.1, 1.1), "graph")
+           for p in probs]
+    for nt in NOISE:
+        init = np.array([r[nt]["init_error"] for r in per])
+        final = np.array([r[nt]["final_error"] for r in per])
+        print("cfg5", nt, "init", init.round(2), "final", final.round(3),
+              "S", [r[nt]["final_nb_samples"] for r in per], "s", [round(r[nt]["seconds"], 2) for r in per])
+        assert np.allclose(init, 20.0, atol=1e-3)
+        assert np.all(np.isfinite(final)) and np.all(final < init), (nt, final)
+        assert all(r[nt]["iterations"] == 800 for r in per)
+    tab = pose_opt.tables(per, NOISE, dict(niter=800), dict(mode="graph"))
+    json.dumps(tab)
+    assert set(tab["mean_solved"]["gaussian"]) == set(pose_opt.THRESHOLDS)
+    assert set(tab["mean_errors"]) == set(NOISE)

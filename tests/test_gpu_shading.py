@@ -178,7 +178,7 @@ def test_native_shading_matches_float32_composition(kind, device):
     composed with it, ulp-level d bary differences are amplified by the 1 / face-area factors)."""
     from pertrenderer_amd.renderer.rasterizer import Fragments
     old = torch.are_deterministic_algorithms_enabled()
-    torch.use_deterministic_algorithms(True)
+    torch.use_deterministic_algorithms(True, warn_only=True)  # the reference's grid_sample backward has none
     try:
         mesh, frag, lights, cams, mats, verts, loc, extra = _scene(device, kind)
         b = frag.bary_coords.detach().clone().requires_grad_(True)
@@ -194,7 +194,22 @@ def test_native_shading_matches_float32_composition(kind, device):
         G = G * (frag.pix_to_face >= 0)[..., None]
         leaves = [b, vd, loc, extra]
         names = ("bary", "verts", "light", "texture" if kind == "uv" else "vertex colours")
-        for name, x, y in zip(names, _grads(out, G, leaves), _grads(ref, G, leaves)):
+        got, exp = _grads(out, G, leaves), _grads(ref, G, leaves)
+        if kind == "uv":
+            # bilinear sampling is not differentiable on texel grid lines: a slot whose map
+            # coordinate lies within 1e-4 texel of one takes a one-sided derivative there, and
+            # which side depends on the last ulp of its coordinate (torch's grid_sample
+            # contracts to FMAs); those slots' d bary are left out, every other value is compared
+            tex = m.textures
+            uv = _interp64(fr.pix_to_face, b.detach().double(), tex.verts_uvs_list()[0].double(),
+                           tex.faces_uvs_list()[0])
+            Hm, Wm = tex.maps_padded().shape[1:3]
+            ix, iy = uv[..., 0] * (Wm - 1), uv[..., 1] * (Hm - 1)
+            edge = lambda c: (c - c.round()).abs() < 1e-4
+            keep = ~(edge(ix) | edge(iy))
+            assert float(keep.float().mean()) > 0.9
+            got[0], exp[0] = got[0] * keep[..., None], exp[0] * keep[..., None]
+        for name, x, y in zip(names, got, exp):
             assert_close(x, y, name=name)
     finally:
         torch.use_deterministic_algorithms(old)

@@ -83,17 +83,33 @@ def _worker(rank, world, port, q):
         P_ref = 0.5 * (xr ** 2 + xr ** 3)
         g_ref = torch.cos(P_ref) * c * 0.5 * (2 * xr + 3 * xr ** 2)
         ok4 = torch.allclose(P.detach(), P_ref, atol=1e-6) and torch.allclose(x.grad, g_ref, atol=1e-6)
-        # 5) reduce_scalar_grads on a never-zeroed CPU 0-d leaf (the reference's sigma): each call
-        #    completes only this backward's partial, so the leaf accumulates like one process
-        from pertrenderer_amd.parallel import reduce_scalar_grads
+        # 5) reduce_scalar_grads on a CPU 0-d leaf (the reference's sigma): each call completes
+        #    only what the backwards since the last call delivered, so the leaf ends as in one
+        #    process whether it accumulates (eval.py:382-385), is replaced with zeros
+        #    (eval.py:386) or reset to None (optimizer.zero_grad) between iterations
+        from pertrenderer_amd.parallel import reduce_scalar_grads, track_scalar_grads
         sg = torch.tensor(2.0, requires_grad=True)
+        track_scalar_grads([sg])
         vals = []
         for _ in range(3):
             (sg * float(rank + 1)).backward()
             reduce_scalar_grads([sg])
             vals.append(float(sg.grad))
-        ok5 = sg.grad.device.type == "cpu" and np.allclose(vals, [3.0, 6.0, 9.0])
-        ok4 = ok4 and ok5
+        sg.grad = torch.zeros_like(sg)  # eval.py:386
+        (sg * float(rank + 1)).backward()
+        reduce_scalar_grads([sg])
+        vals.append(float(sg.grad))
+        sg.grad.zero_()
+        (sg * float(rank + 1)).backward()
+        (sg * float(rank + 1)).backward()  # two backwards, one reduction
+        reduce_scalar_grads([sg])
+        vals.append(float(sg.grad))
+        sg.grad = None
+        (sg * float(rank + 1)).backward()
+        reduce_scalar_grads([sg])
+        vals.append(float(sg.grad))
+        ok5 = sg.grad.device.type == "cpu" and np.allclose(vals, [3.0, 6.0, 9.0, 3.0, 6.0, 3.0]), vals
+        ok4 = ok4 and ok5[0]
         q.put((rank, bool(ok1), bool(ok2 and ok3 and ok4)))
     finally:
         dist.destroy_process_group()

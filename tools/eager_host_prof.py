@@ -40,6 +40,34 @@ def main():
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(25)
     st.sort_stats("cumulative").print_stats(40)
+    st.sort_stats("cumulative").print_stats("pertrenderer_amd|bench", 60)
+    # host time per stage with the GPU drained before each stage (no waiting inside a stage)
+    import collections
+    acc = collections.defaultdict(float)
+    from pertrenderer_amd.renderer.transforms import Rotate, so3_exponential_map
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        R = so3_exponential_map(wl.log_rot)
+        mesh = wl.base.update_padded(Rotate(R).transform_points(wl.base.verts_padded()))
+        t1 = time.perf_counter(); acc["pose"] += t1 - t
+        frag = wl.renderer.rasterizer(mesh, cameras=wl.cameras)
+        t2 = time.perf_counter(); acc["rasterizer"] += t2 - t1
+        img = wl.renderer.shader(frag, mesh, cameras=wl.cameras)
+        t3 = time.perf_counter(); acc["shader"] += t3 - t2
+        loss = ((img[..., :3] - wl.target) ** 2).mean()
+        t4 = time.perf_counter(); acc["loss"] += t4 - t3
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        loss.backward()
+        t5 = time.perf_counter(); acc["backward (incl. its waits)"] += t5 - t4
+        torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        wl.opt.step()
+        wl.zero_grad()
+        t6 = time.perf_counter(); acc["adam + zero_grad"] += t6 - t5
+    for k, v in acc.items():
+        print(f"{k:30s} {v / steps * 1e6:8.1f} us host")
 
 
 if __name__ == "__main__":
