@@ -151,22 +151,26 @@ def kernel_bytes(name, P, K, S, F):
     }.get(name)
 
 
-def dense_roofline(device, P_side=256, K=50, S=8, iters=20):
-    """Blend kernels on dense synthetic fragments (every slot valid) — the bandwidth microbench."""
-    g = torch.Generator().manual_seed(0)
-    N, H, W = 1, P_side, P_side
-    p2f = torch.randint(0, 5000, (N, H, W, K), generator=g).to(device)
-    dists = ((torch.rand((N, H, W, K), generator=g) - 0.5) * 6e-3).to(device).requires_grad_(True)
-    zbuf = (5.0 + 2.0 * torch.rand((N, H, W, K), generator=g)).sort(-1).values.to(device).requires_grad_(True)
-    colors = torch.rand((N, H, W, K, 3), generator=g).to(device).requires_grad_(True)
+def dense_roofline(device, P_side=256, K=50, S=8, iters=20, N=1, Sr=None):
+    """Blend kernels on dense synthetic fragments (every slot valid) at a configuration's shape
+    (N images of P_side^2, K, Sr / Sa samples) — the bandwidth microbench of SURVEY §8(d); the
+    real meshes' fragments are mostly padding (2/3 of the slots at cfg 2, 93 % at cfg 4), which
+    the kernels never read, so only dense fragments give a meaningful fraction of HBM peak."""
+    g = torch.Generator(device).manual_seed(0)
+    H = W = P_side
+    Sr = S if Sr is None else Sr
+    p2f = torch.randint(0, 5000, (N, H, W, K), generator=g, device=device)
+    dists = ((torch.rand((N, H, W, K), generator=g, device=device) - 0.5) * 6e-3).requires_grad_(True)
+    zbuf = (5.0 + 2.0 * torch.rand((N, H, W, K), generator=g, device=device)).sort(-1).values.requires_grad_(True)
+    colors = torch.rand((N, H, W, K, 3), generator=g, device=device).requires_grad_(True)
     sig, gam, alp = (torch.tensor(v, device=device, requires_grad=True) for v in (1e-3, 1e-2, 1.0))
-    gimg = torch.randn((N, H, W, 4), device=device)
+    gimg = torch.randn((N, H, W, 4), device=device, generator=g)
     with KernelTimer(lead_cycles=LEAD_CYCLES) as kt:
         for it in range(iters + 3):
             if it == 3:
                 torch.cuda.synchronize()
                 kt.reset()
-            img = pa.perturbed_blend(colors, p2f, dists, zbuf, sig, gam, alp, S, S, background=(0, 0, 0))
+            img = pa.perturbed_blend(colors, p2f, dists, zbuf, sig, gam, alp, Sr, S, background=(0, 0, 0))
             img.backward(gimg)
         torch.cuda.synchronize()
     out = {}
@@ -174,7 +178,8 @@ def dense_roofline(device, P_side=256, K=50, S=8, iters=20):
         b = kernel_bytes(name, N * H * W, K, S, 0)
         out[name] = {"achieved": round(b / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms": round(ms, 4),
-                     "bytes": b, "launches": n}
+                     "bytes": b, "launches": n,
+                     "shape": f"{N}x{P_side}^2, K={K}, Sr={Sr}, Sa={S}, every slot valid"}
     return out
 
 
@@ -496,9 +501,15 @@ def main():
                       "between the spin and the start event so the clocks are up when the launch starts"}
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if headline and os.path.exists(pmc):  # PMC passes are taken on the headline workload
+        # rocprofv3 cannot collect counters inside this process's timed run (the counter passes need
+        # their own runs, tools/gpu.sh pmc), so the line carries the committed measurement of the
+        # same workload and code, labelled with its source
         tr = json.load(open(pmc)).get(dom)
         if tr:
             roof["traffic"] = tr.get("bytes_per_launch")
+            roof["traffic_source"] = ("profiles/pmc_traffic.json: (2 FETCH_SIZE + WRITE_SIZE) KiB of this call's "
+                                      "kernels, separate rocprofv3 --pmc passes of tools/kprof.py on this workload "
+                                      f"({json.load(open(pmc)).get('_run', 'see profiles/')})")
             if tr.get("valu_issue_us"):  # the bound that applies: VALU issue
                 roof["valu_issue_us"] = tr["valu_issue_us"]
                 roof["valu_frac"] = round(tr["valu_issue_us"] / (1e3 * d["ms"]), 4)
@@ -548,8 +559,9 @@ def main():
                   "peak_from": "tools/philox_bench.hip on one MI355X: 511 G Philox blocks/s x 4 normals"}
     if note:
         out["note"] = note
-    if rank == 0 and not args.no_dense and headline:
-        out["roofline_dense"] = dense_roofline(device)
+    if rank == 0 and world == 1 and not args.no_dense and args.config != "eval":
+        # the blend kernels' fraction of HBM peak on dense fragments at this configuration's shape
+        out["roofline_dense"] = dense_roofline(device, Hs, K, S, N=B, Sr=Sr)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
         threads, total, model = host_cpus()
         v, dt = cpu_baseline(args.cpu_frames, threads)

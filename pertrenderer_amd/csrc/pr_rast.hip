@@ -1002,7 +1002,10 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     const int ncols = min(TW, W - col0), nrows = min(TH, H - row0);
     const int per_row = ncols * K, total = nrows * per_row;
     const float inv_row = 1.f / (float)per_row, inv_k = 1.f / (float)K;
-    constexpr int U = 4;
+#ifndef PR_RAST_OUTU  // slots per lane in flight in the output pass (sweep knob)
+#define PR_RAST_OUTU 4
+#endif
+    constexpr int U = PR_RAST_OUTU;
     for (int base = 0; base < total; base += 64 * U) {
       float2 e[U];
       int sz[U], kk[U], cc[U], rr[U];
@@ -1049,13 +1052,15 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
   int n_app_tot = n_app, n_ins_tot = n_ins;
   for (int o = 32; o > 0; o >>= 1) { n_app_tot += __shfl_xor(n_app_tot, o); n_ins_tot += __shfl_xor(n_ins_tot, o); }
   if (lane == 0) {
-    unsigned hw;
+    unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     const unsigned t = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     if (t < kProfTiles) {
       long long* rec = g_rast_prof + (size_t)t * 16;
       rec[0] = tile_x; rec[1] = tile_y; rec[2] = blockIdx.z; rec[3] = nlist;
-      rec[4] = rt0; rec[5] = (long long)__builtin_amdgcn_s_memrealtime(); rec[6] = hw;
+      rec[4] = rt0; rec[5] = (long long)__builtin_amdgcn_s_memrealtime();
+      rec[6] = (long long)hw | ((long long)(xcc & 0xf) << 32);
       for (int i = 0; i < 6; ++i) rec[7 + i] = stamp[i];
       rec[13] = SL;
       rec[14] = n_app_tot;

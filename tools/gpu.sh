@@ -1,0 +1,100 @@
+# One driver for the GPU-box runs (through gpurun):  bash tools/gpu.sh <command> [args]
+#
+#   tests [TAG]                     GPU test suite + smoke()
+#   quick [TAG]                     smoke, GPU tests, one graph bench line
+#   bench TAG [bench.py args]       one bench line -> gpurun_out/bench_TAG.json (+ kernel summary)
+#   sweep TAG CONFIG SPEC...        bench kernel times per variant; SPEC = "name|ENV=V ...|libname"
+#                                   (libname: a variant built with build_native --out, default the product)
+#   rprof TAG [ENV=V ...]...        rast_fwd per-tile timeline (-DPR_RAST_PROFILE variant), one per env set
+#   pmc TAG [kprof.py args]         PMC counter passes, each its own rocprofv3 run (kernel trace only)
+#   prof TAG [bench.py args]        rocprofv3 --kernel-trace --stats of one bench command
+#   final TAG                       round-end measurement: tests, smoke, bench lines (graph + CPU
+#                                   baseline, eager, eager under CUDA_LAUNCH_BLOCKING=1, eval, cfg3,
+#                                   cfg4), rocprof stats, PMC passes and their summary
+#
+# Every GPU step runs under its own timeout and the chain stops at the first failure.
+set -u
+R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out"; mkdir -p "$OUT"; cd "$R"
+CMD="${1:-quick}"; shift || true
+
+summ() {  # summary of a bench json
+  python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], d['value'], d['ms_per_step'], d['config']['execution'], {k:(v['ms'],v.get('launches')) for k,v in d['kernels'].items()}, 'roofline', d['roofline']['kernel'], d['roofline']['frac'], 'dense', {k:v['frac'] for k,v in d.get('roofline_dense',{}).items()}, 'cpu', d.get('cpu_baseline',{}).get('value'))" "$1" "$2"
+}
+
+tests() {
+  local tag="${1:-t}"
+  timeout -k 10 1100 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/tests_$tag.log" 2>&1
+  local rc=$?; grep -E "^(FAILED|ERROR)|passed|failed" "$OUT/tests_$tag.log" | tail -15; [ $rc -ne 0 ] && return $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$tag.log" 2>&1 || { tail -5 "$OUT/smoke_$tag.log"; return 1; }
+  tail -n 1 "$OUT/smoke_$tag.log"
+}
+
+bench() {
+  local tag="$1"; shift
+  timeout -k 10 600 python bench.py "$@" > "$OUT/bench_$tag.json" 2> "$OUT/bench_$tag.err" || { tail -5 "$OUT/bench_$tag.err"; return 1; }
+  summ "$OUT/bench_$tag.json" "$tag"
+}
+
+sweep() {
+  local tag="$1" cfg="$2"; shift 2
+  for spec in "$@"; do
+    IFS='|' read -r name envs lib <<< "$spec"
+    local libpath=""; [ -n "$lib" ] && libpath="PR_NATIVE_LIB=$R/pertrenderer_amd/$lib.so"
+    env $envs $libpath timeout -k 10 200 python bench.py --config "$cfg" --no-cpu-baseline --no-dense --steps 30 --warmup 5 \
+      > "$OUT/sw_${tag}_$name.json" 2>> "$OUT/sw_$tag.err" || { echo "FAIL $name"; tail -3 "$OUT/sw_$tag.err"; return 1; }
+    summ "$OUT/sw_${tag}_$name.json" "$name"
+  done
+}
+
+rprof() {
+  local tag="$1"; shift
+  [ $# -eq 0 ] && set -- "PR_X=0"
+  for envs in "$@"; do
+    local f="$OUT/rprof_${tag}_${envs// /_}"
+    env $envs PR_NATIVE_LIB=$R/pertrenderer_amd/libpertrender_prof.so timeout -k 10 120 python tools/rast_prof.py "$f.npy" > "$f.log" 2>&1 || { tail -5 "$f.log"; return 1; }
+    python tools/rast_timeline.py "$f.npy"
+  done
+}
+
+pmc() {
+  local tag="$1"; shift
+  (cd /tmp && export TMPDIR=/tmp
+   local i=0
+   for C in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" \
+            "FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+     i=$((i+1))
+     timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$OUT/${tag}_p$i" -o p -- \
+       python "$R/tools/kprof.py" "$@" > "$OUT/${tag}_p$i.log" 2>&1 || { echo "pmc pass $i failed"; tail -5 "$OUT/${tag}_p$i.log"; exit 1; }
+   done) || return 1
+  python tools/pmc_summary.py "$OUT"/${tag}_p* --traffic-out "$OUT/pmc_traffic_$tag.json" > "$OUT/pmc_summary_$tag.txt" 2>&1
+  tail -20 "$OUT/pmc_summary_$tag.txt"
+}
+
+prof() {
+  local tag="$1"; shift
+  (cd /tmp && export TMPDIR=/tmp
+   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$tag" -o prof -- \
+     python "$R/bench.py" "$@" > "$OUT/bench_prof_$tag.json" 2> "$OUT/prof_$tag.err") || { tail -5 "$OUT/prof_$tag.err"; return 1; }
+  find "$OUT/prof_$tag" -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'head -12 {}'
+}
+
+case "$CMD" in
+  tests) tests "${1:-t}" ;;
+  quick) tests "${1:-q}" && bench "${1:-q}" --no-cpu-baseline ;;
+  bench) bench "$@" ;;
+  sweep) sweep "$@" ;;
+  rprof) rprof "$@" ;;
+  pmc) pmc "$@" ;;
+  prof) prof "$@" ;;
+  final)
+    T="${1:-fin}"
+    tests "$T" || exit 1
+    bench "$T" || exit 1
+    bench "eager_$T" --mode eager --no-cpu-baseline --no-dense || exit 1
+    CUDA_LAUNCH_BLOCKING=1 bench "eager_blocking_$T" --mode eager --no-cpu-baseline --no-dense || exit 1
+    for c in eval cfg3 cfg4; do bench "${c}_$T" --config $c --no-cpu-baseline || exit 1; done
+    prof "$T" --no-cpu-baseline --no-dense || exit 1
+    pmc "pmc_$T" || exit 1
+    ;;
+  *) echo "unknown command $CMD"; exit 2 ;;
+esac
