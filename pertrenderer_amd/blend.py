@@ -13,6 +13,8 @@ logits in d gamma (smoothagg.py:54).  sigma / gamma / alpha may be CPU 0-d leave
 as 0-d tensors that autograd moves to the CPU) or device tensors (passed by pointer:
 no host synchronisation, so the step can be captured in a HIP graph).
 """
+import os
+
 import torch
 
 from . import _native as nat
@@ -144,6 +146,115 @@ def _scalar_grads(gs, needs, refs):
     return [gs[i].to(dtype=ref.dtype) if w else None for i, (w, ref) in enumerate(zip(want, refs))]
 
 
+# ------------------------------------------------ smoothing-scalar gradient link
+# The reference's smoothing scalars are CPU 0-d leaves (smoothrast.py:111-123, smoothagg.py:145-163),
+# so every backward must bring their gradients to the host: one synchronisation.  Taken inside the
+# blend's backward it stalls the host until the GPU has drained, before the rasterizer's backward
+# is even launched.  A _ScalarLink node carries them instead: the blend's backward hands it the
+# (3,) device buffer plus an event recorded after the kernels that write it, and the link's
+# backward waits for that event only (a side-stream copy into pinned memory).  MeshRenderer
+# creates the link before the rasterizer (prelink), so autograd, which runs the highest sequence
+# number first, reaches it after the rasterizer's backward is launched; the host then waits only
+# for the blend's kernels, not for the whole queue.
+_LINK = os.environ.get("PR_SCALAR_LINK", "1") != "0"  # 0: the blend's backward copies them itself
+_STATE = {}
+
+
+class _ScalarLink(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, device, sigma, gamma, alpha):
+        ctx.meta = [(t.dtype, t.shape) if torch.is_tensor(t) and t.requires_grad else None
+                    for t in (sigma, gamma, alpha)]
+        return torch.empty(3, dtype=F32, device=device)  # a conduit: the kernels read host floats
+
+    @staticmethod
+    def backward(ctx, g):
+        host = _host_copy(g, getattr(g, "_pr_ready", None))
+        return (None,) + tuple(host[i].to(m[0]).reshape(m[1]) if m is not None else None
+                               for i, m in enumerate(ctx.meta))
+
+
+def _host_copy(g, ready):
+    """g (3,) on the device -> a CPU tensor, waiting only for the event `ready` (when given)."""
+    if ready is None or not g.is_cuda:
+        return g.detach().to("cpu")
+    dev = g.device
+    side = _STATE.get(("side", dev))
+    if side is None:
+        side = _STATE[("side", dev)] = torch.cuda.Stream(dev)
+        _STATE[("pinned", dev)] = torch.empty(3, dtype=F32, pin_memory=True)
+    buf = _STATE[("pinned", dev)]
+    side.wait_event(ready)
+    with torch.cuda.stream(side):
+        buf.copy_(g.detach(), non_blocking=True)
+    g.record_stream(side)
+    side.synchronize()
+    return buf.clone()
+
+
+def _linkable(vals, device):
+    if not (_LINK and torch.is_grad_enabled() and device.type == "cuda"):
+        return False
+    tens = [v for v in vals if torch.is_tensor(v)]
+    if not any(t.requires_grad for t in tens) or any(t.device.type != "cpu" or t.numel() != 1 for t in tens):
+        return False
+    return not torch.cuda.is_current_stream_capturing()
+
+
+def _key(vals, device):
+    return (str(device),) + tuple((id(v), v._version) if torch.is_tensor(v) else v for v in vals)
+
+
+def prelink(vals, device):
+    """Create the link of the smoothing scalars `vals` now (MeshRenderer: before the rasterizer);
+    the next native blend of the same scalars on `device` uses it.  Returns a token for drop."""
+    if not _linkable(vals, device):
+        return None
+    key = _key(vals, device)
+    _STATE["pre"] = (key, _ScalarLink.apply(device, *vals))
+    return key
+
+
+def drop_prelink(token):
+    pre = _STATE.get("pre")
+    if token is not None and pre is not None and pre[0] == token:
+        del _STATE["pre"]
+
+
+def prelink_shader(shader, meshes):
+    """prelink for a shader holding perturbed smoothing operators (RandomSimpleShader /
+    RandomPhongShader); None when it holds none."""
+    sr, sa = getattr(shader, "smoothrast", None), getattr(shader, "smoothagg", None)
+    if sr is None or sa is None or not hasattr(sr, "sigma") or not hasattr(sa, "gamma"):
+        return None
+    device = getattr(meshes, "device", None)
+    return prelink((sr.sigma, sa.gamma, sa.alpha), torch.device(device)) if device is not None else None
+
+
+def _link_scalars(vals, device):
+    """(values, link): with a link, the scalars go to the kernel as host floats and their gradients
+    through the link; otherwise the tensors themselves (the blend copies their gradients)."""
+    if not _linkable(vals, device):
+        return vals, None
+    key, pre = _key(vals, device), _STATE.get("pre")
+    if pre is not None and pre[0] == key:
+        del _STATE["pre"]
+        link = pre[1]
+    else:
+        link = _ScalarLink.apply(device, *vals)
+    return tuple(float(v.detach()) if torch.is_tensor(v) else float(v) for v in vals), link
+
+
+def _link_grad(gsc, need):
+    """The device gradient buffer for the link, marked with the event after its kernels."""
+    if not need:
+        return None
+    ev = torch.cuda.Event()
+    ev.record()
+    gsc._pr_ready = ev
+    return gsc
+
+
 def _counts_for(pix_to_face):
     """The native rasterizer's valid-prefix counts of these fragments (int32 (N,H,W) on the same
     device), or None: the kernels then read pix_to_face at every slot."""
@@ -180,7 +291,7 @@ def _no_uniform_grad(vflags):
 
 class _FusedBlendFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, dists, zbuf, colors, sigma, gamma, alpha, p2f, znear, zfar, cfg):
+    def forward(ctx, dists, zbuf, colors, sigma, gamma, alpha, link, p2f, znear, zfar, cfg):
         nat.require_device(dists, zbuf, colors, p2f)
         lib = nat.load()
         N, H, W, K = p2f.shape
@@ -236,7 +347,7 @@ class _FusedBlendFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         s_g, g_g, a_g = _scalar_grads(gsc, need[3:6], ctx.refs)
         return (gd if need[0] else None, gz if need[1] else None, gc if need[2] else None,
-                s_g, g_g, a_g, None, None, None, None)
+                s_g, g_g, a_g, _link_grad(gsc, need[6]), None, None, None, None)
 
 
 class _FusedVertexBlendFn(torch.autograd.Function):
@@ -245,7 +356,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
     to bary (-> rasterizer backward) and the vertex colours instead of a texel tensor."""
 
     @staticmethod
-    def forward(ctx, dists, zbuf, bary, vert_colors, sigma, gamma, alpha, p2f, faces, znear, zfar, cfg):
+    def forward(ctx, dists, zbuf, bary, vert_colors, sigma, gamma, alpha, link, p2f, faces, znear, zfar, cfg):
         nat.require_device(dists, zbuf, bary, vert_colors, p2f, faces)
         lib = nat.load()
         N, H, W, K = p2f.shape
@@ -303,7 +414,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         _timed("blend_bwd", lambda: nat.call("pr_blend_bwd", "pr_blend_bwd", g, a))
         s_g, g_g, a_g = _scalar_grads(gsc, need[4:7], ctx.refs)
         return (gd if need[0] else None, gz if need[1] else None, gb if need[2] else None, gv,
-                s_g, g_g, a_g, None, None, None, None, None)
+                s_g, g_g, a_g, _link_grad(gsc, need[7]), None, None, None, None, None)
 
 
 def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, sigma, gamma, alpha,
@@ -328,7 +439,8 @@ def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, s
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
-    return _FusedVertexBlendFn.apply(dists, zbuf, bary, vert_colors, sigma, gamma, alpha, pix_to_face, faces,
+    (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
+    return _FusedVertexBlendFn.apply(dists, zbuf, bary, vert_colors, sigma, gamma, alpha, link, pix_to_face, faces,
                                      znear, zfar, cfg)
 
 
@@ -355,7 +467,8 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
-    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, pix_to_face, znear, zfar, cfg)
+    (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
+    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, link, pix_to_face, znear, zfar, cfg)
 
 
 def soft_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, eps=1e-10, background=(1.0, 1.0, 1.0),
@@ -372,7 +485,8 @@ def soft_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, eps=1e-10,
         raise ValueError("dists / zbuf must match pix_to_face's shape")
     cfg = dict(Sr=1, Sa=1, eps=float(eps), bg=_background(background), noise=Noise.philox(),
                vflags=nat.PR_BLEND_SOFT, counts=_counts_for(pix_to_face))
-    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, pix_to_face, znear, zfar, cfg)
+    (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
+    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, link, pix_to_face, znear, zfar, cfg)
 
 
 # ==================================================== standalone heaviside

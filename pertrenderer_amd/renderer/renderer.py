@@ -78,5 +78,13 @@ class MeshRenderer(torch.nn.Module):
         return self
 
     def forward(self, meshes_world, **kwargs):
-        fragments = self.rasterizer(meshes_world, **kwargs)
-        return self.shader(fragments, meshes_world, **kwargs)
+        from .. import blend
+        # the perturbed shaders' smoothing-scalar gradient link, made before the rasterizer's nodes
+        # so that the backward's one host synchronisation comes after the rasterizer's backward is
+        # launched (blend.prelink)
+        token = blend.prelink_shader(self.shader, meshes_world)
+        try:
+            fragments = self.rasterizer(meshes_world, **kwargs)
+            return self.shader(fragments, meshes_world, **kwargs)
+        finally:
+            blend.drop_prelink(token)
