@@ -1468,6 +1468,35 @@ extern "C" int pr_blend_prof_dump(void* dst, size_t bytes) {
 }
 #endif
 
+// Diagnostic (not part of the ABI header): resident workgroups per CU of the Philox vertex /
+// texel-colour blend kernels at a shape, as the HIP occupancy calculator sees them; out[0..3] =
+// fwd single-pass, fwd multi-pass, bwd single-pass, bwd multi-pass; out[4..7] = their LDS bytes.
+extern "C" int pr_diag_blend_occupancy(int K, int Sa, long long P, int cm, int* out) {
+  const int KP1 = K + 1;
+  const Shape sf = pick_shape(KP1, Sa, P, false), sb = pick_shape(KP1, Sa, P, true);
+  const size_t lf = fwd_lds(sf.PB, sf.cap), lb = bwd_lds(sb.PB, sb.cap, Sa);
+  int r = 0;
+  auto occ = [&](const void* f, size_t lds) {
+    int n = -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, kThreads, lds) != hipSuccess) r = -1;
+    return n;
+  };
+  if (cm == 2) {
+    out[0] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 2, false>, lf);
+    out[1] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 2, true>, lf);
+    out[2] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 2, false>, lb);
+    out[3] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 2, true>, lb);
+  } else {
+    out[0] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 1, false>, lf);
+    out[1] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 1, true>, lf);
+    out[2] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 1, false>, lb);
+    out[3] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 1, true>, lb);
+  }
+  out[4] = out[5] = (int)lf;
+  out[6] = out[7] = (int)lb;
+  return r;
+}
+
 extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
   if (!args) return set_error(PR_ERR_ARG, "blend_fwd: null args");
   const PRBlendFwdArgs& a = *args;

@@ -19,12 +19,18 @@ from pertrenderer_amd import _native as nat  # noqa: E402
 import argparse  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", choices=sorted(bench.CONFIGS), default="cfg2")
-cfg = bench.CONFIGS[ap.parse_args().config]
+ap.add_argument("--dense", action="store_true", help="the dense-fragment microbench (bench.dense_roofline's blend)")
+args = ap.parse_args()
+cfg = bench.CONFIGS[args.config]
 # blocks past the first 65536 are not recorded (a cfg4 frame has 524288: images 0-1 only)
-wl = bench.Workload(torch.device("cuda:0"), cfg["image_size"], cfg["K"], cfg["samples"], batch=cfg["batch"])
-for _ in range(3):
-    wl.forward().backward()
-    torch.cuda.synchronize()
+if args.dense:
+    bench.dense_roofline(torch.device("cuda:0"), cfg["image_size"], cfg["K"], cfg["samples"], iters=2,
+                         Sr=cfg.get("rast_samples"))
+else:
+    wl = bench.Workload(torch.device("cuda:0"), cfg["image_size"], cfg["K"], cfg["samples"], batch=cfg["batch"])
+    for _ in range(3):
+        wl.forward().backward()
+        torch.cuda.synchronize()
 lib = nat.load()
 NB = 1 << 16
 REC = 12
