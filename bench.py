@@ -543,7 +543,11 @@ def main():
                                f"{samples_txt} Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, "
                                "fwd + L2 loss + bwd + Adam step on the pose (lr 5e-2)",
                    "image_size": Hs, "faces_per_pixel": K, "nb_samples": S, "rast_samples": Sr, "batch": B,
-                   "distinct_frames_per_step": distinct, "execution": mode, "parallelism": par},
+                   "distinct_frames_per_step": distinct, "execution": mode, "parallelism": par,
+                   # eval.py:4 sets CUDA_LAUNCH_BLOCKING=1; the HIP runtime honours HIP_LAUNCH_BLOCKING only
+                   # (tools/launch_blocking_check.py), so eval.py itself runs launches asynchronously here
+                   "launch_blocking": {k: os.environ[k] for k in ("HIP_LAUNCH_BLOCKING", "CUDA_LAUNCH_BLOCKING")
+                                       if k in os.environ}},
         "ms_forward": round(ms_fwd, 4), "ms_backward": round(ms_bwd, 4), "fwd_bwd_split_from": split_from,
         "fwd_frames_per_s": round(distinct * 1e3 / ms_fwd, 2), "kernels": kern, "roofline": roof,
     }

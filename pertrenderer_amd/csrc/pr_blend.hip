@@ -940,6 +940,9 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
       PX[pl * 12 + 3] = (float)jb;   // unperturbed argmax of the K+1 logits
     }
     if constexpr (CM == 2) {
+#ifdef PR_BLEND_PROF_SPLIT_B2  // diagnostic: B2's pixel part to slot 7, its colour gathers to slot 2
+      PR_BSTAMP(7);
+#endif
       // dW = g_rgb . colour of the slot entries B5 reads (a win, or j0): the colour is
       // interpolated from the vertex colours here, once per such entry
       if (act) {

@@ -415,8 +415,15 @@ template <int SL> struct RastCfg {
   static constexpr int CH = SL >= 4 ? PR_RAST_CH4 : 64;
   static_assert(CAP <= 8 * 64, "suffix-min pass holds CAP / 64 <= 8 entries per lane");
 };
-#ifndef PR_RAST_QPAD  // queue row padding in entries (sweep knob)
-#define PR_RAST_QPAD 0
+// Queue row padding in entries.  The output pass reads a pixel's consecutive slots from one
+// lane to the next: at the unpadded 16-entry (128 B) row stride those reads pile onto two of
+// the 64 banks (~30-way conflicts; they were essentially all of rast_fwd's 1.6 M LDS bank
+// conflicts per launch at cfg 2), one entry of padding spreads them.  The 8-slice layout (deep
+// queues, K > 128) stays unpadded: LDS per wave matters more there (4-13 % slower padded at cfg 4).
+#ifndef PR_RAST_QPAD  // sweeps: a fixed padding for every slice count
+template <int SL> constexpr int rast_qpad() { return SL == 4 ? 1 : 0; }
+#else
+template <int SL> constexpr int rast_qpad() { return PR_RAST_QPAD; }
 #endif
 #ifndef PR_RAST_MERGE  // 0: candidates landing inside a queue are inserted slice by slice (r1 path)
 #define PR_RAST_MERGE 1
@@ -504,7 +511,7 @@ PR_DEV bool ekey_less(float2 x, float2 y) { return key_less(x.x, __float_as_int(
 template <int SL>
 size_t rast_fwd_lds_sl(int K) {
   using C = RastCfg<SL>;
-  return C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL + PR_RAST_QPAD) * 8 + (size_t)C::CAP * 12 + 64 * 4 + C::CH * 8 + 16;
+  return C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL + rast_qpad<SL>()) * 8 + (size_t)C::CAP * 12 + 64 * 4 + C::CH * 8 + 16;
 }
 
 size_t rast_fwd_lds(int K, int SL) {
@@ -591,7 +598,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
                                                       const uint2* __restrict__ fbox, int ring, BinGrid bins) {
   constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
   constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
-  constexpr int QS = TP + PR_RAST_QPAD;  // queue row stride (entries): padding spreads a pixel's rows over banks
+  constexpr int QS = TP + rast_qpad<SL>();  // queue row stride (entries): padding spreads a pixel's rows over banks
   extern __shared__ float smem[];
   const int K = a.K;
   const int lane = threadIdx.x, pix = lane / SL, slice = lane % SL;

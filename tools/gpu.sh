@@ -9,7 +9,7 @@
 #   pmc TAG [kprof.py args]         PMC counter passes, each its own rocprofv3 run (kernel trace only)
 #   prof TAG [bench.py args]        rocprofv3 --kernel-trace --stats of one bench command
 #   final TAG                       round-end measurement: tests, smoke, bench lines (graph + CPU
-#                                   baseline, eager, eager under CUDA_LAUNCH_BLOCKING=1, eval, cfg3,
+#                                   baseline, eager, eager under HIP_LAUNCH_BLOCKING=1, eval, cfg3,
 #                                   cfg4), rocprof stats, PMC passes and their summary
 #
 # Every GPU step runs under its own timeout and the chain stops at the first failure.
@@ -91,7 +91,12 @@ case "$CMD" in
     tests "$T" || exit 1
     bench "$T" || exit 1
     bench "eager_$T" --mode eager --no-cpu-baseline --no-dense || exit 1
-    CUDA_LAUNCH_BLOCKING=1 bench "eager_blocking_$T" --mode eager --no-cpu-baseline --no-dense || exit 1
+    # eval.py's CUDA_LAUNCH_BLOCKING=1 (eval.py:4) is not honoured by the HIP runtime (the plain eager row
+    # is what eval.py gets); HIP_LAUNCH_BLOCKING=1 is the host-synchronous launch mode it asks for
+    HIP_LAUNCH_BLOCKING=1 bench "eager_blocking_$T" --mode eager --no-cpu-baseline --no-dense || exit 1
+    timeout -k 10 60 python tools/launch_blocking_check.py > "$OUT/launch_blocking_$T.txt" 2>&1 &&
+      CUDA_LAUNCH_BLOCKING=1 timeout -k 10 60 python tools/launch_blocking_check.py >> "$OUT/launch_blocking_$T.txt" 2>&1 &&
+      HIP_LAUNCH_BLOCKING=1 timeout -k 10 60 python tools/launch_blocking_check.py >> "$OUT/launch_blocking_$T.txt" 2>&1 || exit 1
     for c in eval cfg3 cfg4; do bench "${c}_$T" --config $c --no-cpu-baseline || exit 1; done
     prof "$T" --no-cpu-baseline --no-dense || exit 1
     pmc "pmc_$T" || exit 1
