@@ -72,6 +72,7 @@ struct Geo {
   int lpp, lsh;                  // lanes per pixel in the pixel phases (256 / PB, 8..64) and log2
   int bpi;                       // blocks per image for the centre-out block order (0: linear)
   int tail;                      // backward: joint masked-tail draw allowed (PR_BLEND_TAIL=0: off)
+  int empty;                     // empty-block shortcut allowed (PR_BLEND_EMPTY=0: off)
   int cap;                       // LDS entry records per workgroup (>= K + 1)
 };
 
@@ -203,6 +204,16 @@ PR_DEV void block_entries(const int32_t* pcnt, int64_t pix0, int npix, int K, bo
     PS[np + 1] = npix;
     PS[PB + 1] = np + 1;
   }
+}
+
+// The block's threads store v over the n floats at dst (float4 stores when dst is 16-B aligned).
+PR_DEV void block_fill(float* dst, int64_t n, float v) {
+  const int tid = threadIdx.x;
+  int64_t head = ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) ? 0 : n;  // unaligned: scalar
+  const int64_t n4 = (n - head) >> 2;
+  const float4 v4 = make_float4(v, v, v, v);
+  for (int64_t i = tid; i < n4; i += kThreads) reinterpret_cast<float4*>(dst)[i] = v4;
+  for (int64_t i = 4 * n4 + tid; i < n; i += kThreads) dst[i] = v;
 }
 
 // Wave-wide append of the lanes with `want` to an LDS queue: one LDS atomic per wave,
@@ -440,6 +451,25 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, pcnt != nullptr, CAP, PB, CL, CP, EA, PS);
   __syncthreads();
   const float gal = sc.gamma / sc.alpha;
+  // ---- empty block (no pixel has a valid slot: only background entries): every sample's
+  //      argmax is the background, W_bg = Sa / Sa = 1, alpha = 1 - (empty product) = 0; the
+  //      same values the phases below would produce, without them
+  if (pcnt && g.empty && uni(EA[bnpix]) == bnpix) {
+    for (int i = tid; i < bnpix * p.Sa; i += kThreads) a.winners[bpix0 * p.Sa + i] = (uint8_t)K;
+    if constexpr (CM != 0) {
+      if (tid < bnpix) {
+        const float wb = (float)p.Sa / (float)p.Sa;
+        reinterpret_cast<float4*>(a.image)[bpix0 + tid] =
+            make_float4(0.f + wb * p.background[0], 0.f + wb * p.background[1], 0.f + wb * p.background[2], 1.f - 1.f);
+      }
+    } else {
+      for (int i = tid; i < bnpix * KP1; i += kThreads) {
+        const int k = i - (i / KP1) * KP1;
+        a.weights[bpix0 * KP1 + i] = k == K ? (float)p.Sa / (float)p.Sa : 0.f / (float)p.Sa;
+      }
+    }
+    return;
+  }
 
   const int npass = MULTI ? uni(PS[PB + 1]) : 1;
   for (int pass = 0; pass < npass; ++pass) {
@@ -746,6 +776,19 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
   __syncthreads();
   const float gal = sc.gamma / sc.alpha;
   float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
+  // ---- empty block (compacted entries, no pixel with a valid slot): the background wins every
+  //      sample and is also the unperturbed argmax, so with the baseline every a_s = 0: no d z,
+  //      no scalar partials; masked slots get zero d zbuf / d dists / d colour (the values B8m
+  //      writes).  Without the baseline (GaussianAgg_wovr) a_s = dW_bg and the full path runs.
+  if (RAST && tail && g.empty && !(p.flags & PR_BLEND_AGG_WOVR) && uni(EA[bnpix]) == bnpix) {
+    const int64_t s0 = bpix0 * K, n = (int64_t)bnpix * K;
+    block_fill(a.grad_zbuf + s0, n, 0.f);
+    block_fill(a.grad_dists + s0, n, 0.f);
+    if constexpr (CM == 1) block_fill(a.grad_colors + 3 * s0, 3 * n, 0.f);
+    if constexpr (CM == 2) block_fill(a.grad_bary + 3 * s0, 3 * n, 0.f);
+    if (tid < 4) partials[blk * 4 + tid] = 0.f;
+    return;
+  }
 
   const int npass = MULTI ? uni(PS[PB + 1]) : 1;
   for (int pass = 0; pass < npass; ++pass) {
@@ -1450,6 +1493,8 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   g.bpi = (order >> (bwd ? 1 : 0) & 1) && g.HW % PB == 0 ? g.HW / PB : 0;
   static const int tail = getenv("PR_BLEND_TAIL") ? atoi(getenv("PR_BLEND_TAIL")) : 1;
   g.tail = tail;
+  const char* empty = getenv("PR_BLEND_EMPTY");  // read per call: tests compare both paths in one process
+  g.empty = empty ? atoi(empty) : 1;
   return g;
 }
 
