@@ -10,7 +10,8 @@
 #   prof TAG [bench.py args]        rocprofv3 --kernel-trace --stats of one bench command
 #   final TAG                       round-end measurement: tests, smoke, bench lines (graph + CPU
 #                                   baseline, eager, eager under HIP_LAUNCH_BLOCKING=1, eval, cfg3,
-#                                   cfg4), rocprof stats, PMC passes and their summary
+#                                   cfg4, eager eval), cfg5 (pose_opt 100 x 800), rocprof stats, PMC
+#                                   passes and their summary
 #
 # Every GPU step runs under its own timeout and the chain stops at the first failure.
 set -u
@@ -98,6 +99,11 @@ case "$CMD" in
       CUDA_LAUNCH_BLOCKING=1 timeout -k 10 60 python tools/launch_blocking_check.py >> "$OUT/launch_blocking_$T.txt" 2>&1 &&
       HIP_LAUNCH_BLOCKING=1 timeout -k 10 60 python tools/launch_blocking_check.py >> "$OUT/launch_blocking_$T.txt" 2>&1 || exit 1
     for c in eval cfg3 cfg4; do bench "${c}_$T" --config $c --no-cpu-baseline || exit 1; done
+    bench "eager_eval_$T" --config eval --mode eager --no-cpu-baseline --no-dense || exit 1
+    # BASELINE cfg5: eval.py's pose benchmark, 100 problems x 800 iterations x {softras, gaussian}
+    timeout -k 10 600 python -m pertrenderer_amd.pose_opt -np 100 -ni 800 --mode graph --out "$OUT/cfg5_$T" \
+      > "$OUT/cfg5_$T.log" 2>&1 || { tail -5 "$OUT/cfg5_$T.log"; exit 1; }
+    tail -3 "$OUT/cfg5_$T.log"
     prof "$T" --no-cpu-baseline --no-dense || exit 1
     pmc "pmc_$T" || exit 1
     ;;
