@@ -737,6 +737,10 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
 }
 
 // ================================================================= backward
+#ifndef PR_BLEND_B2R  // B2's per-lane entry chunk held in registers (0: always walk LDS)
+#define PR_BLEND_B2R 8
+#endif
+constexpr int kB2R = PR_BLEND_B2R > 0 ? PR_BLEND_B2R : 1;
 // Same entry layout and passes as the forward.  Entries are compacted (a pixel's valid
 // slots + background) when the masked tail is drawn jointly (B6); otherwise every slot
 // keeps its entry, since injected / Cauchy noise needs each masked slot's own d z.
@@ -923,14 +927,35 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
     const bool act = pl < npix;
     const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, ckp = (c + g.lpp) >> g.lsh;  // ceil((c+1)/lpp)
     const int j0c = l * ckp, j1c = min(c + 1, j0c + ckp), k1c = min(c, j1c);
+    // chunks of at most kB2R entries (every pixel of the launch: K + 1 <= kB2R * lpp) are read
+    // into registers once; the loops below then touch LDS only for their results (same
+    // arithmetic, same order)
+    const bool regs = !MULTI && g.KP1 <= kB2R * g.lpp;  // (the multi-pass template keeps its VGPR cap)
+    float rpr[kB2R], rzz[kB2R];
+    if (regs) {
+#pragma unroll
+      for (int u = 0; u < kB2R; ++u) {
+        const int k = j0c + u;
+        rpr[u] = act && k < k1c ? PR[e0 + k] : 0.f;
+        rzz[u] = act && k < k1c ? ZZ[e0 + k] : 0.f;
+      }
+    }
     float zm = kNegInf, tp = 1.f;
     int km = 1 << 30;
-    if (act)
+    if (regs) {
+#pragma unroll
+      for (int u = 0; u < kB2R; ++u) {
+        if (!(act && j0c + u < k1c)) break;
+        if (rzz[u] > zm) { zm = rzz[u]; km = j0c + u; }
+        tp *= (1.f - rpr[u]);
+      }
+    } else if (act) {
       for (int k = j0c; k < k1c; ++k) {
         const float zi = ZZ[e0 + k];
         if (zi > zm) { zm = zi; km = k; }
         tp *= (1.f - PR[e0 + k]);
       }
+    }
     for (int m = 1; m < g.lpp; m <<= 1) {
       const float oz = __shfl_xor(zm, m);
       const int ok = __shfl_xor(km, m);
@@ -953,7 +978,20 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
       const float iu = __shfl_up(inc, 1, g.lpp), sd = __shfl_down(sinc, 1, g.lpp);
       float pre = l > 0 ? iu : 1.f, suf = l + 1 < g.lpp ? sd : 1.f;
       if (act && l == 0) PX[pl * 12 + 5] = tp * suf;  // prod (1 - prob): a masked slot's exclusive product
-      if (act) {
+      if (regs) {
+        float ex[kB2R];
+#pragma unroll
+        for (int u = kB2R - 1; u >= 0; --u) {
+          ex[u] = suf;
+          if (act && j0c + u < k1c) suf *= (1.f - rpr[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kB2R; ++u) {
+          if (!(act && j0c + u < k1c)) break;
+          EX[e0 + j0c + u] = pre * ex[u];
+          pre *= (1.f - rpr[u]);
+        }
+      } else if (act) {
         for (int k = k1c - 1; k >= j0c; --k) {
           EX[e0 + k] = suf;
           suf *= (1.f - PR[e0 + k]);
@@ -966,12 +1004,22 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
     }
     float zb = kNegInf;
     int jb = 1 << 30;
-    if (act)
+    if (regs) {
+#pragma unroll
+      for (int u = 0; u < kB2R; ++u) {
+        const int e = j0c + u;
+        if (!(act && e < j1c)) break;
+        const int j = e < c ? e : K;
+        const float z = j < K ? gal * logf(rpr[u]) + rzz[u] - zmax : p.eps - zmax;
+        if (z > zb || jb == (1 << 30)) { zb = z; jb = j; }
+      }
+    } else if (act) {
       for (int e = j0c; e < j1c; ++e) {
         const int j = e < c ? e : K;
         const float z = j < K ? gal * logf(PR[e0 + e]) + ZZ[e0 + e] - zmax : p.eps - zmax;
         if (z > zb || jb == (1 << 30)) { zb = z; jb = j; }
       }
+    }
     for (int m = 1; m < g.lpp; m <<= 1) {
       const float oz = __shfl_xor(zb, m);
       const int oj = __shfl_xor(jb, m);
