@@ -14,6 +14,7 @@ as 0-d tensors that autograd moves to the CPU) or device tensors (passed by poin
 no host synchronisation, so the step can be captured in a HIP graph).
 """
 import os
+import threading
 
 import torch
 
@@ -157,7 +158,14 @@ def _scalar_grads(gs, needs, refs):
 # number first, reaches it after the rasterizer's backward is launched; the host then waits only
 # for the blend's kernels, not for the whole queue.
 _LINK = os.environ.get("PR_SCALAR_LINK", "1") != "0"  # 0: the blend's backward copies them itself
-_STATE = {}
+_TLS = threading.local()  # per thread: the pending prelink, and per device a side stream + pinned buffer
+
+
+def _state():
+    st = getattr(_TLS, "state", None)
+    if st is None:
+        st = _TLS.state = {}
+    return st
 
 
 class _ScalarLink(torch.autograd.Function):
@@ -179,11 +187,12 @@ def _host_copy(g, ready):
     if ready is None or not g.is_cuda:
         return g.detach().to("cpu")
     dev = g.device
-    side = _STATE.get(("side", dev))
+    st = _state()
+    side = st.get(("side", dev))
     if side is None:
-        side = _STATE[("side", dev)] = torch.cuda.Stream(dev)
-        _STATE[("pinned", dev)] = torch.empty(3, dtype=F32, pin_memory=True)
-    buf = _STATE[("pinned", dev)]
+        side = st[("side", dev)] = torch.cuda.Stream(dev)
+        st[("pinned", dev)] = torch.empty(3, dtype=F32, pin_memory=True)
+    buf = st[("pinned", dev)]
     side.wait_event(ready)
     with torch.cuda.stream(side):
         buf.copy_(g.detach(), non_blocking=True)
@@ -211,14 +220,15 @@ def prelink(vals, device):
     if not _linkable(vals, device):
         return None
     key = _key(vals, device)
-    _STATE["pre"] = (key, _ScalarLink.apply(device, *vals))
+    _state()["pre"] = (key, _ScalarLink.apply(device, *vals))
     return key
 
 
 def drop_prelink(token):
-    pre = _STATE.get("pre")
+    st = _state()
+    pre = st.get("pre")
     if token is not None and pre is not None and pre[0] == token:
-        del _STATE["pre"]
+        del st["pre"]
 
 
 def prelink_shader(shader, meshes):
@@ -236,9 +246,10 @@ def _link_scalars(vals, device):
     through the link; otherwise the tensors themselves (the blend copies their gradients)."""
     if not _linkable(vals, device):
         return vals, None
-    key, pre = _key(vals, device), _STATE.get("pre")
+    st = _state()
+    key, pre = _key(vals, device), st.get("pre")
     if pre is not None and pre[0] == key:
-        del _STATE["pre"]
+        del st["pre"]
         link = pre[1]
     else:
         link = _ScalarLink.apply(device, *vals)

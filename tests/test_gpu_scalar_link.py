@@ -76,7 +76,7 @@ def test_link_autograd_grad_and_prelink_consumed(device):
     torch.use_deterministic_algorithms(True)
     try:
         wl, loss = _frame(device, True)
-        assert blend._STATE.get("pre") is None  # MeshRenderer's prelink was consumed or dropped
+        assert blend._state().get("pre") is None  # MeshRenderer's prelink was consumed or dropped
         gs = torch.autograd.grad(loss, [wl.rast.sigma, wl.agg.gamma, wl.agg.alpha, wl.log_rot])
         ref = _grads(device, True, False)
     finally:
