@@ -428,6 +428,9 @@ template <int SL> constexpr int rast_qpad() { return PR_RAST_QPAD; }
 #ifndef PR_RAST_MERGE  // 0: candidates landing inside a queue are inserted slice by slice (r1 path)
 #define PR_RAST_MERGE 1
 #endif
+#ifndef PR_RAST_FRAGC  // 0: the output pass evaluates faces lane by lane over all slots (r2 path)
+#define PR_RAST_FRAGC 1
+#endif
 #ifndef PR_RAST_CULLU  // sweeps: 8 measured equal, 4 slower (+10 us)
 #define PR_RAST_CULLU 16
 #endif
@@ -1013,6 +1016,11 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
 #define PR_RAST_OUTU 4
 #endif
     constexpr int U = PR_RAST_OUTU;
+    // compacted fragment pass (tiles of <= 16 pixels): the slot walk writes p2f / zbuf and the
+    // padded slots' -1s only; the valid slots' barycentrics / distances are then computed one
+    // valid slot per lane (a pixel's valid slots are its queue prefix), so no face evaluation
+    // runs for a lane group that holds padding -- on a heavy tile half or more of its slots
+    constexpr bool kCompact = FRAG && TP <= 16 && PR_RAST_FRAGC;
     for (int base = 0; base < total; base += 64 * U) {
       float2 e[U];
       int sz[U], kk[U], cc[U], rr[U];
@@ -1035,7 +1043,14 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
         const int fid = __float_as_int(e[u].y);
         a.pix_to_face[o[u]] = valid ? (int64_t)fid : (int64_t)-1;
         a.zbuf[o[u]] = valid ? e[u].x : -1.f;
-        if constexpr (FRAG) {
+        if constexpr (kCompact) {
+          if (!valid) {
+            a.dists[o[u]] = -1.f;
+            a.bary[o[u] * 3 + 0] = -1.f;
+            a.bary[o[u] * 3 + 1] = -1.f;
+            a.bary[o[u] * 3 + 2] = -1.f;
+          }
+        } else if constexpr (FRAG) {
           float bc[3] = {-1.f, -1.f, -1.f}, dist = -1.f;
           if (valid) {
             const V2 pp{ndc(W - 1 - (col0 + cc[u]), W, H), ndc(H - 1 - (row0 + rr[u]), H, W)};
@@ -1049,6 +1064,56 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
           a.bary[o[u] * 3 + 0] = bc[0];
           a.bary[o[u] * 3 + 1] = bc[1];
           a.bary[o[u] * 3 + 2] = bc[2];
+        }
+      }
+    }
+    if constexpr (kCompact) {
+      // valid slot v belongs to the pixel t with ex[t] <= v < ex[t] + qsz[t] (ex: exclusive
+      // prefix of the queue sizes over the tile's pixels, wave-uniform), at queue position v - ex[t]
+      const int mysz = lane < TP ? qsz[lane] : 0;
+      int incl = mysz;
+#pragma unroll
+      for (int o = 1; o < TP; o <<= 1) {
+        const int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+      }
+      const int excl = incl - mysz;
+      int ex[TP];
+#pragma unroll
+      for (int t = 0; t < TP; ++t) ex[t] = __builtin_amdgcn_readlane(excl, t);
+      const int nvalid = __builtin_amdgcn_readlane(incl, TP - 1);
+      for (int vb = 0; vb < nvalid; vb += 64 * U) {
+        float2 e[U];
+        int tl[U], kk[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int v = min(vb + u * 64 + lane, nvalid - 1);
+          int t = 0, e0 = 0;
+#pragma unroll
+          for (int s = 1; s < TP; ++s) {
+            const bool ge = v >= ex[s];
+            t = ge ? s : t;
+            e0 = ge ? ex[s] : e0;
+          }
+          tl[u] = t;
+          kk[u] = v - e0;
+          e[u] = q[kk[u] * QS + t];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (vb + u * 64 + lane >= nvalid) break;
+          const int fid = __float_as_int(e[u].y);
+          const int rr = tl[u] / TW, cc = tl[u] % TW;
+          const int64_t o = (((int64_t)n * H + row0 + rr) * W + col0 + cc) * K + kk[u];
+          const V2 pp{ndc(W - 1 - (col0 + cc), W, H), ndc(H - 1 - (row0 + rr), H, W)};
+          const FaceRec r = faces[fid];
+          float bc[3], pz, d;
+          bool inside;
+          face_eval<PERSP, CLIP>(r, pp, bc, pz, inside, d);
+          a.dists[o] = inside ? -d : d;
+          a.bary[o * 3 + 0] = bc[0];
+          a.bary[o * 3 + 1] = bc[1];
+          a.bary[o * 3 + 2] = bc[2];
         }
       }
     }
