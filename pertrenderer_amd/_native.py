@@ -197,17 +197,27 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
+def dense(t, dtype):
+    """`t` detached as a contiguous `dtype` tensor: `t.detach().to(dtype).contiguous()`, without
+    the two no-op dispatcher calls when it already is one (the eager step makes ~30 of these)."""
+    if t.dtype is dtype and t.is_contiguous():
+        return t.detach()
+    return t.detach().to(dtype).contiguous()
+
+
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def stream_of(t):
-    """The current torch stream of `t`'s device, as the hipStream_t handle."""
+    """The current torch stream of `t`'s device, as the hipStream_t handle (a plain int: ctypes
+    passes it for the c_void_p argument)."""
     if _raw_stream is not None:
-        return C.c_void_p(_raw_stream(t.device.index if t.device.index is not None else torch.cuda.current_device()))
-    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+        return _raw_stream(t.device.index if t.device.index is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream(t.device).cuda_stream
 
 
 _get_device = getattr(torch._C, "_cuda_getDevice", None) or torch.cuda.current_device
+_FNS = {}
 
 
 def call(name, what, t, *args):
@@ -216,14 +226,17 @@ def call(name, what, t, *args):
     sharding over devices, multidevice.py) the call runs under a device guard, so every launch,
     memset and error query of the library addresses `t`'s device.  Raises NativeError on a
     non-zero status."""
-    fn = getattr(load(), name)
+    fn = _FNS.get(name)
+    if fn is None:
+        fn = _FNS[name] = getattr(load(), name)
     idx = t.device.index
     if idx is not None and idx != _get_device():
         with torch.cuda.device(idx):
             code = fn(*args, stream_of(t))
     else:
         code = fn(*args, stream_of(t))
-    check(code, what)
+    if code != 0:
+        check(code, what)
 
 
 def deterministic():

@@ -40,6 +40,10 @@ def _planes(z, N, device):
             t = _PLANE_CACHE[key] = torch.full((N,), float(z), dtype=F32, device=device)
         return t
     if torch.is_tensor(z):
+        if z.dtype is F32 and z.device == device and z.numel() == N:  # the cameras' (N,) planes: a view
+            r = z.detach().reshape(N)
+            if r.is_contiguous():
+                return r
         z = z.detach().to(device=device, dtype=F32).reshape(-1)
         if z.numel() == 1:
             z = z.expand(N)
@@ -59,7 +63,7 @@ def _background(bg):
 
 
 def _contig(t, dtype=F32):
-    return t.detach().to(dtype).contiguous()
+    return nat.dense(t, dtype)
 
 
 def _scalars(vals, device):
@@ -266,11 +270,17 @@ def _link_grad(gsc, need):
     return gsc
 
 
+_valid_counts = None
+
+
 def _counts_for(pix_to_face):
     """The native rasterizer's valid-prefix counts of these fragments (int32 (N,H,W) on the same
     device), or None: the kernels then read pix_to_face at every slot."""
-    from .renderer.rasterizer import valid_counts
-    c = valid_counts(pix_to_face)
+    global _valid_counts
+    if _valid_counts is None:
+        from .renderer.rasterizer import valid_counts as _vc
+        _valid_counts = _vc
+    c = _valid_counts(pix_to_face)
     if c is None or c.device != pix_to_face.device or tuple(c.shape) != tuple(pix_to_face.shape[:3]):
         return None
     return c.contiguous()
@@ -307,7 +317,7 @@ class _FusedBlendFn(torch.autograd.Function):
         lib = nat.load()
         N, H, W, K = p2f.shape
         dev = p2f.device
-        p2f_c = p2f.detach().to(torch.int64).contiguous()
+        p2f_c = nat.dense(p2f, torch.int64)
         d_c, z_c, c_c = _contig(dists), _contig(zbuf), _contig(colors)
         zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
         noise = cfg["noise"].to(dev)
@@ -343,7 +353,7 @@ class _FusedBlendFn(torch.autograd.Function):
         dev = p2f_c.device
         p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf,
                     nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | cfg["vflags"])
-        g = gimg.detach().to(F32).contiguous()
+        g = nat.dense(gimg, F32)
         gd, gz, gc = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(c_c)
         gsc = torch.empty(3, dtype=F32, device=dev)
         a = nat.PRBlendBwdArgs()
@@ -372,8 +382,8 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         lib = nat.load()
         N, H, W, K = p2f.shape
         dev = p2f.device
-        p2f_c = p2f.detach().to(torch.int64).contiguous()
-        f_c = faces.detach().to(torch.int64).contiguous()
+        p2f_c = nat.dense(p2f, torch.int64)
+        f_c = nat.dense(faces, torch.int64)
         d_c, z_c, b_c, v_c = _contig(dists), _contig(zbuf), _contig(bary), _contig(vert_colors)
         zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
         noise = cfg["noise"].to(dev)
@@ -408,7 +418,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         dev = p2f_c.device
         p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf, ctx.flags)
         need = ctx.needs_input_grad
-        g = gimg.detach().to(F32).contiguous()
+        g = nat.dense(gimg, F32)
         gd, gz, gb = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(b_c)
         gv = torch.zeros_like(v_c) if need[3] else None
         gsc = torch.empty(3, dtype=F32, device=dev)
@@ -535,7 +545,7 @@ class _HeavisideFn(torch.autograd.Function):
         sdev = ctx.sdev
         lib = nat.load()
         a = _heaviside_args(tuple(d_c.shape), ctx.Sr, ctx.noise, ctx.sv, sdev, d_c, ctx.flags)
-        g = gP.detach().to(F32).contiguous()
+        g = nat.dense(gP, F32)
         gd = torch.empty_like(d_c)
         gs = torch.empty(1, dtype=F32, device=d_c.device)
         a.grad_prob, a.grad_dists, a.grad_sigma = nat.ptr(g), nat.ptr(gd), nat.ptr(gs)
@@ -569,7 +579,7 @@ class _AggregateFn(torch.autograd.Function):
         N, H, W, K = zbuf.shape
         dev = zbuf.device
         z_c, p_c = _contig(zbuf), _contig(prob)
-        m_c = mask.detach().to(torch.uint8).contiguous()
+        m_c = nat.dense(mask, torch.uint8)
         zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
         noise = cfg["noise"].to(dev)
         sc, sc_dev = _scalars((1.0, gamma, alpha), dev)
@@ -598,7 +608,7 @@ class _AggregateFn(torch.autograd.Function):
         dev = z_c.device
         p = _params((N, H, W, K), 1, cfg["Sa"], sc, sc_dev, cfg["eps"], (0.0, 0.0, 0.0), noise, zn, zf,
                     cfg["vflags"])
-        g = gW.detach().to(F32).contiguous()
+        g = nat.dense(gW, F32)
         gz, gp = torch.empty_like(z_c), torch.empty_like(p_c)
         gsc = torch.empty(3, dtype=F32, device=dev)
         a = nat.PRBlendBwdArgs()

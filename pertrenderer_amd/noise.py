@@ -68,7 +68,9 @@ class Noise:
         return Noise(nat.PR_NOISE_INJECTED, 0, 0, noise_r, noise_a, 0, 0)
 
     def to(self, device):
-        mv = (lambda t: None if t is None else t.to(device=device, dtype=torch.float32).contiguous())
+        if self.noise_r is None and self.noise_a is None:  # Philox: nothing on the host to move
+            return self
+        mv =(lambda t: None if t is None else t.to(device=device, dtype=torch.float32).contiguous())
         return Noise(self.mode, self.seed_r, self.seed_a, mv(self.noise_r), mv(self.noise_a),
                      self.offset_r, self.offset_a, self.seeds)
 

@@ -16,10 +16,10 @@ class _InterpFn(torch.autograd.Function):
         lib = nat.load()
         shape = tuple(p2f.shape)
         D = attr.shape[-1]
-        p2f_c = p2f.detach().to(torch.int64).contiguous()
-        b_c = bary.detach().to(F32).contiguous()
-        fa = attr.detach().to(F32).contiguous()
-        fc = None if faces is None else faces.detach().to(torch.int64).contiguous()
+        p2f_c = nat.dense(p2f, torch.int64)
+        b_c = nat.dense(bary, F32)
+        fa = nat.dense(attr, F32)
+        fc = None if faces is None else nat.dense(faces, torch.int64)
         out = torch.empty(shape + (D,), dtype=F32, device=b_c.device)
         a = nat.PRInterpArgs()
         a.pix_to_face, a.bary, a.face_attr = nat.ptr(p2f_c), nat.ptr(b_c), nat.ptr(fa)
@@ -37,7 +37,7 @@ class _InterpFn(torch.autograd.Function):
         need_b, need_f = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         if not (need_b or need_f):
             return None, None, None, None
-        go = g.detach().to(F32).contiguous()
+        go = nat.dense(g, F32)
         gb = torch.empty_like(b_c) if need_b else None
         gf = torch.empty_like(fa) if need_f else None
         a = nat.PRInterpArgs()

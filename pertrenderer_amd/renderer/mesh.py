@@ -268,7 +268,7 @@ class _VertNormalsFn(torch.autograd.Function):
         from .. import _native as nat
         lib = nat.load()
         v = verts.detach().contiguous()
-        f = faces.detach().to(torch.int64).contiguous()
+        f = nat.dense(faces, torch.int64)
         n = torch.empty_like(v)
         raw = torch.empty_like(v)
         a = nat.PRNormalsArgs()
@@ -286,7 +286,7 @@ class _VertNormalsFn(torch.autograd.Function):
         from .. import _native as nat
         v, f, raw = ctx.saved_tensors
         lib = nat.load()
-        gc = g.detach().to(torch.float32).contiguous()
+        gc = nat.dense(g, torch.float32)
         graw, gv = torch.empty_like(v), torch.empty_like(v)
         a = nat.PRNormalsArgs()
         a.verts, a.faces, a.V, a.F = nat.ptr(v), nat.ptr(f), v.shape[0], f.shape[0]

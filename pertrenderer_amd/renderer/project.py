@@ -27,8 +27,8 @@ class _ProjectFn(torch.autograd.Function):
     def forward(ctx, verts, faces, first, nfaces, w2v, proj, csr_start=None, csr_corners=None):
         nat.require_device(verts, faces, w2v, proj)
         lib = nat.load()
-        v = verts.detach().to(F32).contiguous()
-        f = faces.detach().to(torch.int64).contiguous()
+        v = nat.dense(verts, F32)
+        f = nat.dense(faces, torch.int64)
         a = nat.PRProjectArgs()
         a.verts, a.faces, a.mesh_first_face, a.mesh_num_faces = nat.ptr(v), nat.ptr(f), nat.ptr(first), nat.ptr(nfaces)
         N = first.shape[0]
@@ -48,7 +48,7 @@ class _ProjectFn(torch.autograd.Function):
         if not ctx.needs_input_grad[0]:
             return (None,) * 8
         lib = nat.load()
-        go = g.detach().to(F32).contiguous()
+        go = nat.dense(g, F32)
         gv = torch.empty_like(v)
         a = nat.PRProjectArgs()
         a.verts, a.faces, a.mesh_first_face, a.mesh_num_faces = nat.ptr(v), nat.ptr(f), nat.ptr(first), nat.ptr(nfaces)

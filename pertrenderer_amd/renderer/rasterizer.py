@@ -101,7 +101,7 @@ class _RasterizeFn(torch.autograd.Function):
     def forward(ctx, face_verts, first, nfaces, H, W, K, blur, persp, clip, cull, bins=(0, 0)):
         nat.require_device(face_verts, first, nfaces)
         lib = nat.load()
-        fv = face_verts.detach().to(F32).contiguous()
+        fv = nat.dense(face_verts, F32)
         N = first.shape[0]
         dev = fv.device
         a = nat.PRRastArgs()
@@ -144,7 +144,7 @@ class _RasterizeFn(torch.autograd.Function):
         keep = []
         for name, g in (("grad_zbuf", gzbuf), ("grad_bary", gbary), ("grad_dists", gdists)):
             if g is not None:
-                g = g.detach().to(F32).contiguous()
+                g = nat.dense(g, F32)
                 keep.append(g)
                 setattr(a, name, nat.ptr(g))
         gfv = torch.empty_like(fv)
@@ -172,8 +172,8 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         from .project import _per_mesh
         nat.require_device(verts, faces, first, nfaces, w2v, proj)
         lib = nat.load()
-        v = verts.detach().to(F32).contiguous()
-        f = faces.detach().to(torch.int64).contiguous()
+        v = nat.dense(verts, F32)
+        f = nat.dense(faces, torch.int64)
         N, F, dev = first.shape[0], f.shape[0], v.device
         m1, m2 = _per_mesh(w2v, N, "world_to_view"), _per_mesh(proj, N, "projection")
         fv = torch.empty((F, 3, 3), dtype=F32, device=dev)
@@ -232,7 +232,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         keep = []
         for name, g in (("grad_zbuf", gzbuf), ("grad_bary", gbary), ("grad_dists", gdists)):
             if g is not None:
-                g = g.detach().to(F32).contiguous()
+                g = nat.dense(g, F32)
                 keep.append(g)
                 setattr(a, name, nat.ptr(g))
         a.grad_face_verts = nat.ptr(gfv)

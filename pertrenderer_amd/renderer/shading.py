@@ -82,9 +82,9 @@ class _ShadeFn(torch.autograd.Function):
         nat.require_device(bary, verts, normals, tex, light, camera)
         lib = nat.load()
         N, H, W, K = cfg["p2f"].shape
-        keep = dict(bary=bary.detach().to(F32).contiguous(), verts=verts.detach().to(F32).contiguous(),
-                    normals=normals.detach().to(F32).contiguous(), tex=tex.detach().to(F32).contiguous(),
-                    light=light.detach().to(F32).contiguous(), camera=camera.detach().to(F32).contiguous())
+        keep = dict(bary=nat.dense(bary, F32), verts=nat.dense(verts, F32),
+                    normals=nat.dense(normals, F32), tex=nat.dense(tex, F32),
+                    light=nat.dense(light, F32), camera=nat.dense(camera, F32))
         colors = torch.empty((N, H, W, K, 3), dtype=F32, device=bary.device)
         a = _args(cfg, keep)
         a.colors = nat.ptr(colors)
@@ -100,7 +100,7 @@ class _ShadeFn(torch.autograd.Function):
         cfg = ctx.cfg
         lib = nat.load()
         need = ctx.needs_input_grad
-        g = gcol.detach().to(F32).contiguous()
+        g = nat.dense(gcol, F32)
         a = _args(cfg, keep)
         a.grad_colors = nat.ptr(g)
         out = [torch.empty_like(t) if need[i] else None
@@ -174,7 +174,7 @@ def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face
     verts = meshes.verts_packed()
     faces = meshes.faces_packed().to(torch.int64).contiguous()
     rows = lambda x: _rows(x, N, dev).contiguous()
-    cfg = dict(p2f=p2f.detach().to(torch.int64).contiguous(), counts=counts, faces=faces, mode=mode,
+    cfg = dict(p2f=nat.dense(p2f, torch.int64), counts=counts, faces=faces, mode=mode,
                face_uvs=face_uvs, directional=_is_directional(lights),
                ambient=rows(materials.ambient_color * lights.ambient_color),
                diffuse_color=rows(lights.diffuse_color), specular_color=rows(lights.specular_color),

@@ -18,7 +18,7 @@ class _SO3ExpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, log_rot, eps):
         lib = nat.load()
-        w = log_rot.detach().to(F32).contiguous()
+        w = nat.dense(log_rot, F32)
         R = torch.empty((w.shape[0], 3, 3), dtype=F32, device=w.device)
         a = nat.PRSO3Args()
         a.N, a.eps, a.log_rot, a.R = w.shape[0], float(eps), nat.ptr(w), nat.ptr(R)
@@ -31,7 +31,7 @@ class _SO3ExpFn(torch.autograd.Function):
     def backward(ctx, gR):
         (w,) = ctx.saved_tensors
         lib = nat.load()
-        g = gR.detach().to(F32).contiguous()
+        g = nat.dense(gR, F32)
         gw = torch.empty_like(w)
         a = nat.PRSO3Args()
         a.N, a.eps, a.log_rot, a.grad_R, a.grad_log_rot = w.shape[0], float(ctx.eps), nat.ptr(w), nat.ptr(g), nat.ptr(gw)
@@ -43,8 +43,8 @@ class _RotateFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, points, R):
         lib = nat.load()
-        p = points.detach().to(F32).contiguous()
-        r = R.detach().to(F32).contiguous()
+        p = nat.dense(points, F32)
+        r = nat.dense(R, F32)
         out = torch.empty_like(p)
         a = nat.PRRotateArgs()
         a.N, a.P, a.R_batched = p.shape[0], p.shape[1], int(r.shape[0] > 1)
@@ -57,7 +57,7 @@ class _RotateFn(torch.autograd.Function):
     def backward(ctx, gout):
         p, r = ctx.saved_tensors
         lib = nat.load()
-        g = gout.detach().to(F32).contiguous()
+        g = nat.dense(gout, F32)
         need_p, need_r = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         gp = torch.empty_like(p) if need_p else None
         gr = torch.empty_like(r) if need_r else None
