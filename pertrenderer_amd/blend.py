@@ -337,6 +337,7 @@ class _FusedBlendFn(torch.autograd.Function):
         a.pix_count = nat.ptr(cfg["counts"])
         _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
         ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, cache)
+        ctx.p = p  # the backward's parameter block is the forward's
         ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
         ctx.refs = (sigma, gamma, alpha)
@@ -351,8 +352,7 @@ class _FusedBlendFn(torch.autograd.Function):
         lib = nat.load()
         N, H, W, K = p2f_c.shape
         dev = p2f_c.device
-        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf,
-                    nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | cfg["vflags"])
+        p = ctx.p
         g = nat.dense(gimg, F32)
         gd, gz, gc = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(c_c)
         gsc = torch.empty(3, dtype=F32, device=dev)
@@ -402,6 +402,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         a.pix_count = nat.ptr(cfg["counts"])
         _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
         ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache)
+        ctx.p = p  # the backward's parameter block is the forward's
         ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc, ctx.flags = cfg, noise, sc, flags
         ctx.refs = (sigma, gamma, alpha)
@@ -416,7 +417,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         lib = nat.load()
         N, H, W, K = p2f_c.shape
         dev = p2f_c.device
-        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf, ctx.flags)
+        p = ctx.p
         need = ctx.needs_input_grad
         g = nat.dense(gimg, F32)
         gd, gz, gb = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(b_c)
