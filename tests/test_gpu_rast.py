@@ -80,6 +80,10 @@ def _run_native(fv, first, nf, H, W, K, blur, persp, clip, cull, dev, bins=(0, 0
     dict(H=32, W=32, K=20, blur=5e-3, persp=False, clip=True, cull=False),
     dict(H=24, W=40, K=5, blur=2e-3, persp=True, clip=True, cull=True),
     dict(H=16, W=16, K=70, blur=5e-2, persp=False, clip=True, cull=False),
+    # K = 1; and K > 128 (8 face slices on 4x2 tiles), on sizes that leave partial border tiles:
+    # the compacted fragment pass's edge cases (empty pixels between full ones, partial tiles)
+    dict(H=29, W=35, K=1, blur=5e-3, persp=False, clip=True, cull=False),
+    dict(H=21, W=27, K=140, blur=8e-2, persp=False, clip=True, cull=False),
 ])
 @pytest.mark.parametrize("bins", [(0, 0), (8, 10000), (16, 6)])
 def test_rasterizer_forward_matches_oracle_bitwise(cfg, bins, device):
