@@ -46,6 +46,7 @@ from pertrenderer_amd.renderer import (FoVPerspectiveCameras, MeshRasterizer, Me
 from pertrenderer_amd.renderer.transforms import Rotate, so3_exponential_map  # noqa: E402
 from pertrenderer_amd.parallel import average_gradients, sample_shard  # noqa: E402
 from pertrenderer_amd.timing import KernelTimer  # noqa: E402
+from pertrenderer_amd.build_native import source_sha  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -369,7 +370,16 @@ def instrumented_pass(wl, steps):
         torch.cuda.synchronize()
     for p, g in zip(wl.params(), grads):
         p.grad = g
-    return kt.summary("min"), kt.summary("median")
+    return kt.summary("min"), kt.summary("median"), kt.kernel_summary("mean"), kt.kernel_summary("min")
+
+
+def committed_record(name, sha):
+    """profiles/<name> when it was measured on these native sources (its "source_sha"), else None."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    rec = json.load(open(path))
+    return rec if rec.get("source_sha") == sha else None
 
 
 def eager_split(wl, steps):
@@ -484,35 +494,51 @@ def main():
     else:
         ms_fwd, ms_bwd = eager_split(wl, n_split)
         split_from = "HIP events around the eager forward / loss.backward()"
-    ksum, kmed = instrumented_pass(wl, n_split)
+    ksum, kmed, kk, kkmin = instrumented_pass(wl, n_split)
     kern = {}
     for name, (n, ms) in ksum.items():
         bts = kernel_bytes(name, P, wl.K, S_local, wl.F)
         kern[name] = {"launches": n, "ms": round(ms, 4), "ms_median": round(kmed[name][1], 4), "bytes": bts,
                       "GBps": round(bts / (ms * 1e-3) / 1e9, 1)}
-    dom = max(kern, key=lambda k: kern[k]["ms"] * kern[k]["launches"])
+        if name in kk:  # the call's dominant kernel alone (the library's own event pair around it)
+            kname, _, kms = kk[name]
+            kern[name].update({"kernel": kname, "kernel_ms": round(kms, 4), "kernel_ms_min": round(kkmin[name][2], 4)})
+    # roofline: the longest kernel (as rocprofv3 names it) by its live per-launch duration
+    timed = [k for k in kern if "kernel_ms" in kern[k]] or list(kern)
+    dom = max(timed, key=lambda k: kern[k].get("kernel_ms", kern[k]["ms"]) * kern[k]["launches"])
     d = kern[dom]
-    roof = {"kernel": dom, "bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(d["GBps"] / HBM_PEAK_GBS, 4), "traffic": None,
-            "bytes_per_launch": d["bytes"], "ms_per_launch": d["ms"],
-            "timing": "minimum over launches of HIP events around each launch on its stream (each "
-                      "behind a device-side lead spin, so host time is excluded), eager replica of the timed "
-                      "step right after the timed region (same kernels and arguments), a 64 MB elementwise pass "
-                      "between the spin and the start event so the clocks are up when the launch starts"}
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if headline and os.path.exists(pmc):  # PMC passes are taken on the headline workload
+    k_ms = d.get("kernel_ms", d["ms"])
+    achieved = d["bytes"] / (k_ms * 1e-3) / 1e9
+    sha = source_sha()
+    roof = {"kernel": d.get("kernel", dom), "call": dom, "bound": "hbm", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_per_launch": d["bytes"], "ms_per_launch": round(k_ms, 4), "source_sha": sha,
+            "timing": "mean over the launches of an eager replica of the timed step (same kernels and arguments, "
+                      "right after the timed region) of a HIP event pair the library records on the launch stream "
+                      "immediately around this kernel (pr_ktimer_arm); each launch behind a device-side lead spin "
+                      "(host time excluded) and a 64 MB elementwise pass (clocks up)",
+            "bytes_from": "algorithmic bytes of the call (SURVEY.md §8(d), bench.kernel_bytes), all attributed to "
+                          "its dominant kernel"}
+    prof = committed_record("rocprof_kernels.json", sha) if headline else None
+    if prof and roof["kernel"] in prof.get("kernels", {}):
+        avg_us = prof["kernels"][roof["kernel"]]["avg_us"]
+        roof["rocprof"] = {"avg_us": avg_us, "achieved": round(d["bytes"] / (avg_us * 1e-6) / 1e9, 1),
+                           "frac": round(d["bytes"] / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                           "source": f"profiles/rocprof_kernels.json ({prof.get('run', '')}), measured on these "
+                                     f"native sources (source_sha {sha})"}
+    pmc = committed_record("pmc_traffic.json", sha) if headline else None
+    if pmc and pmc.get(dom):  # PMC passes are taken on the headline workload
         # rocprofv3 cannot collect counters inside this process's timed run (the counter passes need
         # their own runs, tools/gpu.sh pmc), so the line carries the committed measurement of the
-        # same workload and code, labelled with its source
-        tr = json.load(open(pmc)).get(dom)
-        if tr:
-            roof["traffic"] = tr.get("bytes_per_launch")
-            roof["traffic_source"] = ("profiles/pmc_traffic.json: (2 FETCH_SIZE + WRITE_SIZE) KiB of this call's "
-                                      "kernels, separate rocprofv3 --pmc passes of tools/kprof.py on this workload "
-                                      f"({json.load(open(pmc)).get('_run', 'see profiles/')})")
-            if tr.get("valu_issue_us"):  # the bound that applies: VALU issue
-                roof["valu_issue_us"] = tr["valu_issue_us"]
-                roof["valu_frac"] = round(tr["valu_issue_us"] / (1e3 * d["ms"]), 4)
+        # same workload and the same native sources (source_sha), labelled with its source
+        tr = pmc[dom]
+        roof["traffic"] = tr.get("bytes_per_launch")
+        roof["traffic_source"] = ("profiles/pmc_traffic.json: (2 FETCH_SIZE + WRITE_SIZE) KiB of this call's "
+                                  f"kernels {tr.get('kernels')}, separate rocprofv3 --pmc passes of tools/kprof.py on "
+                                  f"this workload, same source_sha ({pmc.get('_run', 'see profiles/')})")
+        if tr.get("valu_issue_us"):  # the bound that applies: VALU issue
+            roof["valu_issue_us"] = tr["valu_issue_us"]
+            roof["valu_frac"] = round(tr["valu_issue_us"] / (1e3 * k_ms), 4)
 
     B, Hs, K = cfg["batch"], cfg["image_size"], cfg["K"]
     distinct = B * (world if shard == "frames" else 1)  # distinct frames per step

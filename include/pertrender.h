@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 14
+#define PR_ABI_VERSION 15
 
 /* error codes */
 #define PR_OK 0
@@ -369,6 +369,15 @@ int pr_rotate_bwd(const PRRotateArgs* args, void* stream);
 
 int pr_abi_version(void);
 const char* pr_last_error(void);
+
+/* Live per-kernel timing (measurement only; no reference counterpart).  pr_ktimer_arm(slot) makes
+ * the next hot-path call of this thread record a pair of HIP events on its launch stream right
+ * before and right after its dominant kernel (blend_fwd_kernel, blend_bwd_kernel, rast_fwd_kernel,
+ * rast_bwd_kernel); pr_ktimer_read(slot, ...) returns that kernel's duration in ms and its name
+ * after the stream has drained.  0 <= slot < 256 (-1 disarms); events are created on the current device.
+ * Not armed: no events are recorded (graph capture never sees them). */
+int pr_ktimer_arm(int32_t slot);
+int pr_ktimer_read(int32_t slot, float* ms, char* name, int32_t name_cap);
 
 int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream);
 size_t pr_blend_bwd_workspace_size(const PRBlendBwdArgs* args);

@@ -6,7 +6,11 @@ perturbed Heaviside over signed edge distances and the Monte-Carlo perturbed-
 argmax colour aggregation, forward and backward — runs in hand-written HIP for
 gfx950 (libpertrender.so, C ABI in include/pertrender.h).
 """
-from . import _native
+from .launch_mode import honour_cuda_launch_blocking as _honour
+
+_honour()  # first thing: eval.py's CUDA_LAUNCH_BLOCKING=1 as HIP_LAUNCH_BLOCKING=1 (launch_mode.py)
+
+from . import _native  # noqa: E402
 from .blend import perturbed_aggregate, perturbed_blend, perturbed_blend_vertex, perturbed_heaviside, soft_blend
 from .multidevice import activate_from_env as _activate_sample_devices
 from .multidevice import sample_devices, set_sample_devices

@@ -129,6 +129,8 @@ class PRNormalsArgs(C.Structure):
 EXPORTS = {
     "pr_abi_version": (C.c_int, []),
     "pr_last_error": (C.c_char_p, []),
+    "pr_ktimer_arm": (C.c_int, [C.c_int32]),
+    "pr_ktimer_read": (C.c_int, [C.c_int32, C.POINTER(C.c_float), C.c_char_p, C.c_int32]),
     "pr_blend_fwd": (C.c_int, [C.POINTER(PRBlendFwdArgs), _vp]),
     "pr_blend_bwd_workspace_size": (C.c_size_t, [C.POINTER(PRBlendBwdArgs)]),
     "pr_blend_bwd": (C.c_int, [C.POINTER(PRBlendBwdArgs), _vp]),
@@ -156,7 +158,7 @@ EXPORTS = {
     "pr_vert_normals_fwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
     "pr_vert_normals_bwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
 }
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _lib = None
 

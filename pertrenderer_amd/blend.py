@@ -13,6 +13,7 @@ logits in d gamma (smoothagg.py:54).  sigma / gamma / alpha may be CPU 0-d leave
 as 0-d tensors that autograd moves to the CPU) or device tensors (passed by pointer:
 no host synchronisation, so the step can be captured in a HIP graph).
 """
+import collections
 import os
 import threading
 
@@ -27,7 +28,8 @@ F32 = torch.float32
 _ABS = 1 << 63  # absolute-key marker (see PRBlendParams.seeds)
 
 
-_PLANE_CACHE = {}
+_PLANE_CACHE = collections.OrderedDict()
+_PLANE_CACHE_MAX = 16  # LRU: a caller scheduling float planes per step does not grow it without bound
 
 
 def _planes(z, N, device):
@@ -38,6 +40,10 @@ def _planes(z, N, device):
         t = _PLANE_CACHE.get(key)
         if t is None:
             t = _PLANE_CACHE[key] = torch.full((N,), float(z), dtype=F32, device=device)
+            while len(_PLANE_CACHE) > _PLANE_CACHE_MAX:
+                _PLANE_CACHE.popitem(last=False)
+        else:
+            _PLANE_CACHE.move_to_end(key)
         return t
     if torch.is_tensor(z):
         if z.dtype is F32 and z.device == device and z.numel() == N:  # the cameras' (N,) planes: a view
@@ -314,7 +320,6 @@ class _FusedBlendFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, dists, zbuf, colors, sigma, gamma, alpha, link, p2f, znear, zfar, cfg):
         nat.require_device(dists, zbuf, colors, p2f)
-        lib = nat.load()
         N, H, W, K = p2f.shape
         dev = p2f.device
         p2f_c = nat.dense(p2f, torch.int64)
@@ -329,7 +334,7 @@ class _FusedBlendFn(torch.autograd.Function):
         # per-slot (prob, rast score) kept for the backward instead of regenerating rast noise
         soft = bool(cfg["vflags"] & nat.PR_BLEND_SOFT)
         cache = (torch.empty((N, H, W, K, 2), dtype=F32, device=dev)
-                 if RAST_CACHE and not soft and any(ctx.needs_input_grad[:6]) else None)
+                 if RAST_CACHE and not soft and any(ctx.needs_input_grad[:7]) else None)
         a = nat.PRBlendFwdArgs()
         a.p = p
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
@@ -344,6 +349,7 @@ class _FusedBlendFn(torch.autograd.Function):
         return image
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gimg):
         _no_uniform_grad(ctx.cfg.get("vflags", 0))
         p2f_c, d_c, z_c, c_c, zn, zf, winners, cache = ctx.saved_tensors
@@ -379,7 +385,6 @@ class _FusedVertexBlendFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, dists, zbuf, bary, vert_colors, sigma, gamma, alpha, link, p2f, faces, znear, zfar, cfg):
         nat.require_device(dists, zbuf, bary, vert_colors, p2f, faces)
-        lib = nat.load()
         N, H, W, K = p2f.shape
         dev = p2f.device
         p2f_c = nat.dense(p2f, torch.int64)
@@ -393,7 +398,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
         need = ctx.needs_input_grad
-        cache = torch.empty((N, H, W, K, 2), dtype=F32, device=dev) if RAST_CACHE and any(need[:7]) else None
+        cache = torch.empty((N, H, W, K, 2), dtype=F32, device=dev) if RAST_CACHE and any(need[:8]) else None
         a = nat.PRBlendFwdArgs()
         a.p = p
         a.pix_to_face, a.dists, a.zbuf = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c)
@@ -409,6 +414,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         return image
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gimg):
         _no_uniform_grad(ctx.cfg.get("vflags", 0))
         p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache = ctx.saved_tensors
@@ -527,7 +533,6 @@ class _HeavisideFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, dists, sigma, Sr, noise, flags):
         nat.require_device(dists)
-        lib = nat.load()
         d_c = _contig(dists)
         noise = noise.to(d_c.device)
         (sv,), sdev = _scalars((sigma,), d_c.device)
@@ -541,6 +546,7 @@ class _HeavisideFn(torch.autograd.Function):
         return prob
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gP):
         d_c, = ctx.saved_tensors
         sdev = ctx.sdev
@@ -576,7 +582,6 @@ class _AggregateFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, zbuf, prob, gamma, alpha, mask, znear, zfar, cfg):
         nat.require_device(zbuf, prob, mask)
-        lib = nat.load()
         N, H, W, K = zbuf.shape
         dev = zbuf.device
         z_c, p_c = _contig(zbuf), _contig(prob)
@@ -599,6 +604,7 @@ class _AggregateFn(torch.autograd.Function):
         return weights
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gW):
         _no_uniform_grad(ctx.cfg["vflags"])
         z_c, p_c, m_c, zn, zf, winners = ctx.saved_tensors

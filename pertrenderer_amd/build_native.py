@@ -30,6 +30,18 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
+def source_sha():
+    """sha256 (16 hex digits) of the native sources and headers: ties a committed rocprofv3 / PMC
+    record under profiles/ (its "source_sha") to the code a run loads."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        h.update(os.path.basename(f).encode())
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _stale():
     if not os.path.exists(LIB):
         return True

@@ -1489,24 +1489,28 @@ template <int NOISE, bool MULTI>
 void launch_fwd(const PRBlendFwdArgs& a, Geo geo, int NC, hipStream_t st, size_t lds, int nblk) {
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
+  ktimer_mark(0, "blend_fwd_kernel", st);
   if (rast && cm == 2) blend_fwd_kernel<NOISE, true, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
   else if (rast && cm == 1) blend_fwd_kernel<NOISE, true, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
   else if (rast) blend_fwd_kernel<NOISE, true, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
   else if (cm == 1) blend_fwd_kernel<NOISE, false, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
   else if (cm == 2) blend_fwd_kernel<NOISE, false, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
   else blend_fwd_kernel<NOISE, false, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  ktimer_mark(1, "blend_fwd_kernel", st);
 }
 
 template <int NOISE, bool MULTI>
 void launch_bwd(const PRBlendBwdArgs& a, Geo geo, hipStream_t st, size_t lds, int nblk, float* part) {
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
+  ktimer_mark(0, "blend_bwd_kernel", st);
   if (rast && cm == 2) blend_bwd_kernel<NOISE, true, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
   else if (rast && cm == 1) blend_bwd_kernel<NOISE, true, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
   else if (rast) blend_bwd_kernel<NOISE, true, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
   else if (cm == 1) blend_bwd_kernel<NOISE, false, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
   else if (cm == 2) blend_bwd_kernel<NOISE, false, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
   else blend_bwd_kernel<NOISE, false, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  ktimer_mark(1, "blend_bwd_kernel", st);
 }
 
 Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {

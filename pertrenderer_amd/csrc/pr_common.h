@@ -101,6 +101,8 @@ PR_DEV T ld(const T* p) { return *p; }
 namespace pr {
 int set_error(int code, const std::string& msg);
 int check_launch(const char* what);
+// live per-kernel timing (pr_ktimer_arm): which = 0 before the dominant kernel's launch, 1 after
+void ktimer_mark(int which, const char* kernel, hipStream_t st);
 
 // PR_BLEND_SOFT: the deterministic SoftRast + SoftAgg blend (pr_softblend.hip)
 size_t soft_blend_workspace(const PRBlendParams& p);

@@ -1154,8 +1154,10 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb,
   static const int prio_t = getenv("PR_RAST_PRIO_T") ? atoi(getenv("PR_RAST_PRIO_T")) & 255 : 40;
   const bool sq = grid.x % 2 == 0 && (grid.y == grid.x || grid.y == 2 * grid.x);
   const int ring = (ring_env && sq ? 1 : 0) | (prio_env ? 2 : 0) | (prio_t << 8);
+  ktimer_mark(0, "rast_fwd_kernel", st);
   if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring, bins);
   else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring, bins);
+  ktimer_mark(1, "rast_fwd_kernel", st);
 }
 
 template <bool PERSP, bool CLIP>
@@ -1975,10 +1977,12 @@ extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {
     if (exact) rast_bwd_kernel<R, true><<<grid, kBwdThreads, 0, st>>>(a, order);  \
     else rast_bwd_kernel<R, false><<<grid, kBwdThreads, 0, st>>>(a, order);       \
   } while (0)
+  ktimer_mark(0, "rast_bwd_kernel", st);
   if (rows == 8) PR_RAST_BWD_LAUNCH(8);
   else if (rows == 4) PR_RAST_BWD_LAUNCH(4);
   else if (rows == 1) PR_RAST_BWD_LAUNCH(1);
   else PR_RAST_BWD_LAUNCH(2);
+  ktimer_mark(1, "rast_bwd_kernel", st);
 #undef PR_RAST_BWD_LAUNCH
   return check_launch("rast_bwd");
 }

@@ -26,6 +26,7 @@ This is the north star's sample partition without torchrun; the torchrun paths
 (``parallel.py``, bench.py) remain the measured multi-GPU configuration.
 """
 import os
+import warnings
 
 import torch
 import torch.cuda.comm as _comm
@@ -70,7 +71,12 @@ def devices_from_env(value=None):
         n = min(int(value), torch.cuda.device_count())
         return [f"cuda:{i}" for i in range(n)] if n > 1 else None
     items = [v.strip() for v in value.split(",") if v.strip()]
-    return [v if v.startswith("cuda") else f"cuda:{int(v)}" for v in items]
+    devs = [v if v.startswith("cuda") else f"cuda:{int(v)}" for v in items]
+    n = torch.cuda.device_count()  # 0 on a host without GPUs: nothing to check against there
+    bad = [d for d in devs if n > 0 and torch.device(d).index is not None and torch.device(d).index >= n]
+    if bad:
+        raise ValueError(f"PR_SAMPLE_DEVICES names {bad}, but this process sees {n} GPU(s)")
+    return devs
 
 
 def activate_from_env():
@@ -78,6 +84,11 @@ def activate_from_env():
     one process, eval.py:112-116) shards its Monte-Carlo samples over the node's GPUs with no
     change to its source -- `PR_SAMPLE_DEVICES=all python experiments/eval.py ...`."""
     devs = devices_from_env()
+    if devs is not None and int(os.environ.get("WORLD_SIZE", "1") or 1) > 1:
+        # a torchrun rank owns its LOCAL_RANK device: sharding its samples over every GPU from cuda:0
+        # would collide with the other ranks (bench.py / parallel.py shard across processes instead)
+        warnings.warn("PR_SAMPLE_DEVICES is ignored in a multi-process job (WORLD_SIZE > 1)", RuntimeWarning)
+        return None
     if devs is not None:
         set_sample_devices(devs)
     return devs

@@ -13,7 +13,6 @@ class _InterpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, bary, attr, p2f, faces):
         nat.require_device(bary, attr, p2f)
-        lib = nat.load()
         shape = tuple(p2f.shape)
         D = attr.shape[-1]
         p2f_c = nat.dense(p2f, torch.int64)
@@ -31,9 +30,9 @@ class _InterpFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, g):
         b_c, fa, p2f_c, fc = ctx.saved_tensors
-        lib = nat.load()
         need_b, need_f = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         if not (need_b or need_f):
             return None, None, None, None

@@ -266,7 +266,6 @@ class _VertNormalsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, verts, faces, csr_start=None, csr_corners=None):
         from .. import _native as nat
-        lib = nat.load()
         v = verts.detach().contiguous()
         f = nat.dense(faces, torch.int64)
         n = torch.empty_like(v)
@@ -285,7 +284,6 @@ class _VertNormalsFn(torch.autograd.Function):
     def backward(ctx, g):
         from .. import _native as nat
         v, f, raw = ctx.saved_tensors
-        lib = nat.load()
         gc = nat.dense(g, torch.float32)
         graw, gv = torch.empty_like(v), torch.empty_like(v)
         a = nat.PRNormalsArgs()

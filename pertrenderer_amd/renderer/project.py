@@ -26,7 +26,6 @@ class _ProjectFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, verts, faces, first, nfaces, w2v, proj, csr_start=None, csr_corners=None):
         nat.require_device(verts, faces, w2v, proj)
-        lib = nat.load()
         v = nat.dense(verts, F32)
         f = nat.dense(faces, torch.int64)
         a = nat.PRProjectArgs()
@@ -43,11 +42,11 @@ class _ProjectFn(torch.autograd.Function):
         return fv
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, g):
         v, f, first, nfaces, m1, m2 = ctx.saved_tensors
         if not ctx.needs_input_grad[0]:
             return (None,) * 8
-        lib = nat.load()
         go = nat.dense(g, F32)
         gv = torch.empty_like(v)
         a = nat.PRProjectArgs()

@@ -132,6 +132,7 @@ class _RasterizeFn(torch.autograd.Function):
         return p2f, zbuf, bary, dists, counts
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gp2f, gzbuf, gbary, gdists, gcounts):
         fv, first, nfaces, p2f, counts = ctx.saved_tensors
         H, W, K, blur, persp, clip, cull = ctx.cfg
@@ -215,6 +216,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         return p2f, zbuf, bary, dists, counts
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gp2f, gzbuf, gbary, gdists, gcounts):
         v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv = ctx.saved_tensors
         if gfv is None:

@@ -80,7 +80,6 @@ class _ShadeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, bary, verts, normals, tex, light, camera, cfg):
         nat.require_device(bary, verts, normals, tex, light, camera)
-        lib = nat.load()
         N, H, W, K = cfg["p2f"].shape
         keep = dict(bary=nat.dense(bary, F32), verts=nat.dense(verts, F32),
                     normals=nat.dense(normals, F32), tex=nat.dense(tex, F32),
@@ -94,6 +93,7 @@ class _ShadeFn(torch.autograd.Function):
         return colors
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gcol):
         bary, verts, normals, tex, light, camera = ctx.saved_tensors
         keep = dict(bary=bary, verts=verts, normals=normals, tex=tex, light=light, camera=camera)

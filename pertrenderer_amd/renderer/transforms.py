@@ -17,7 +17,6 @@ F32 = torch.float32
 class _SO3ExpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, log_rot, eps):
-        lib = nat.load()
         w = nat.dense(log_rot, F32)
         R = torch.empty((w.shape[0], 3, 3), dtype=F32, device=w.device)
         a = nat.PRSO3Args()
@@ -28,9 +27,9 @@ class _SO3ExpFn(torch.autograd.Function):
         return R
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gR):
         (w,) = ctx.saved_tensors
-        lib = nat.load()
         g = nat.dense(gR, F32)
         gw = torch.empty_like(w)
         a = nat.PRSO3Args()
@@ -42,7 +41,6 @@ class _SO3ExpFn(torch.autograd.Function):
 class _RotateFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, points, R):
-        lib = nat.load()
         p = nat.dense(points, F32)
         r = nat.dense(R, F32)
         out = torch.empty_like(p)
@@ -54,9 +52,9 @@ class _RotateFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gout):
         p, r = ctx.saved_tensors
-        lib = nat.load()
         g = nat.dense(gout, F32)
         need_p, need_r = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         gp = torch.empty_like(p) if need_p else None

@@ -29,6 +29,8 @@ class KernelTimer:
     def __init__(self, external=False, lead_cycles=0, warm_bytes=0):
         self._open = {}
         self.events = collections.defaultdict(list)
+        self.kslots = collections.defaultdict(list)  # call name -> [native timer slot per launch]
+        self._nslot = 0
         self.external = external
         self.lead_cycles = lead_cycles
         # after the (single-wave) spin the chip is idle and its clocks drop; a short full-chip
@@ -54,14 +56,41 @@ class KernelTimer:
         ev = torch.cuda.Event(enable_timing=True, external=self.external)
         ev.record(torch.cuda.current_stream())
         self._open[name] = ev
+        if not self.external and self._nslot < 256:
+            from . import _native as nat
+            if nat.load().pr_ktimer_arm(self._nslot) == 0:
+                self.kslots[name].append(self._nslot)
+                self._nslot += 1
 
     def stop(self, name):
         ev = torch.cuda.Event(enable_timing=True, external=self.external)
         ev.record(torch.cuda.current_stream())
         self.events[name].append((self._open.pop(name), ev))
+        if not self.external:
+            from . import _native as nat
+            nat.load().pr_ktimer_arm(-1)  # a call that launched no timed kernel leaves nothing armed
 
     def reset(self):
         self.events.clear()
+        self.kslots.clear()
+        self._nslot = 0
+
+    def kernel_summary(self, stat="mean"):
+        """{call name: (kernel name, launches, ms)} of the dominant kernel of each native call,
+        from the library's own event pair around that kernel -- after torch.cuda.synchronize()."""
+        from . import _native as nat
+        lib = nat.load()
+        out = {}
+        for name, slots in self.kslots.items():
+            ms, kname = [], None
+            for s in slots:
+                v, buf = ctypes.c_float(), ctypes.create_string_buffer(64)
+                if lib.pr_ktimer_read(s, ctypes.byref(v), buf, 64) == 0:
+                    ms.append(v.value)
+                    kname = buf.value.decode()
+            if ms:
+                out[name] = (kname, len(ms), _stat(sorted(ms), stat))
+        return out
 
     def summary(self, stat="mean"):
         """{name: (launches, ms)} with ms the mean, median or minimum over launches — call after
@@ -69,14 +98,16 @@ class KernelTimer:
         out = {}
         for name, pairs in self.events.items():
             ms = sorted(a.elapsed_time(b) for a, b in pairs)
-            if not ms:
-                continue
-            if stat == "median":
-                m = len(ms) // 2
-                v = ms[m] if len(ms) % 2 else 0.5 * (ms[m - 1] + ms[m])
-            elif stat == "min":
-                v = ms[0]
-            else:
-                v = sum(ms) / len(ms)
-            out[name] = (len(ms), v)
+            if ms:
+                out[name] = (len(ms), _stat(ms, stat))
         return out
+
+
+def _stat(ms, stat):
+    """mean / median / min of a sorted list."""
+    if stat == "median":
+        m = len(ms) // 2
+        return ms[m] if len(ms) % 2 else 0.5 * (ms[m - 1] + ms[m])
+    if stat == "min":
+        return ms[0]
+    return sum(ms) / len(ms)

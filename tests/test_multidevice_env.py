@@ -58,3 +58,13 @@ def test_native_call_guards_the_device(monkeypatch):
     entered.clear()
     nat.call("pr_fake", "fake", on(0), "args")
     assert calls[-1] == ([], ("args", "stream")) and entered == []  # current device: no guard
+
+
+def test_activation_skipped_in_multi_process_jobs():
+    """A torchrun rank owns its LOCAL_RANK device: PR_SAMPLE_DEVICES is ignored there (with a warning)."""
+    code = "import pertrenderer_amd as pa; print(pa.sample_devices())"
+    env = dict(os.environ, PR_SAMPLE_DEVICES="0,1", WORLD_SIZE="2")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == "None" and "ignored" in out.stderr

@@ -76,7 +76,8 @@ prof() {
   (cd /tmp && export TMPDIR=/tmp
    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$tag" -o prof -- \
      python "$R/bench.py" "$@" > "$OUT/bench_prof_$tag.json" 2> "$OUT/prof_$tag.err") || { tail -5 "$OUT/prof_$tag.err"; return 1; }
-  find "$OUT/prof_$tag" -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'head -12 {}'
+  local f; f=$(find "$OUT/prof_$tag" -name "*kernel_stats.csv" | sort | sed -n 1p)
+  python tools/rocprof_summary.py "$f" "$OUT/rocprof_kernels_$tag.json" "rocprofv3 --kernel-trace --stats -- python bench.py $*"
 }
 
 case "$CMD" in
@@ -104,7 +105,7 @@ case "$CMD" in
     timeout -k 10 600 python -m pertrenderer_amd.pose_opt -np 100 -ni 800 --mode graph --out "$OUT/cfg5_$T" \
       > "$OUT/cfg5_$T.log" 2>&1 || { tail -5 "$OUT/cfg5_$T.log"; exit 1; }
     tail -3 "$OUT/cfg5_$T.log"
-    prof "$T" --no-cpu-baseline --no-dense || exit 1
+    prof "$T" --steps 200 --warmup 20 --no-cpu-baseline --no-dense || exit 1
     pmc "pmc_$T" || exit 1
     ;;
   *) echo "unknown command $CMD"; exit 2 ;;

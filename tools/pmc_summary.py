@@ -76,5 +76,10 @@ if __name__ == "__main__":
         if any(s in k for s in ("blend", "rast", "interp", "project", "heaviside")):
             print(k, json.dumps({c: round(v) for c, v in sorted(res[k].items())}))
     if out:
-        json.dump(traffic(res), open(out, "w"), indent=1)
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from pertrenderer_amd.build_native import source_sha
+        tr = traffic(res)
+        tr["source_sha"] = source_sha()  # bench.py uses the record only for the same native sources
+        tr["_run"] = os.environ.get("PR_PROFILE_RUN", "tools/gpu.sh pmc")
+        json.dump(tr, open(out, "w"), indent=1)
         print("wrote", out)
