@@ -57,6 +57,8 @@ extern "C" {
                             /* N(0,1) by Box-Muller, Cauchy by tan(pi (u - 1/2))             */
 #define PR_NOISE_INJECTED 1 /* caller-provided N(0,1) tensors (reference-parity mode) */
 
+#define PR_BLEND_SYNC_BYTES 1024 /* PRBlendFwdArgs.sync */
+
 /* pr_blend flags */
 #define PR_BLEND_RAST 1  /* probabilities from dists via the perturbed Heaviside (else `prob` input) */
 #define PR_BLEND_COLOR 2 /* colour mix + alpha -> image (else weights (N,H,W,K+1) out) */
@@ -118,6 +120,15 @@ typedef struct PRBlendFwdArgs {
   /* nullable (N,H,W) valid-prefix counts of pix_to_face (pr_rast_fwd's pix_count): mask = k < */
   /* count, and no fragment tensor is read at masked slots                                   */
   const int32_t* pix_count;
+  /* nullable (needs pix_count), out: >= pr_blend_plan_size(&p) bytes (0: no plan for this call;
+   * plans are opt-in, PR_BLEND_SEG=1).  Given, the call first cuts the pixel blocks of the forward
+   * and of the backward into entry-balanced segments (a block's valid slots + background entries
+   * split into parts of about the same count) and both kernels run one workgroup per segment;
+   * keep it for pr_blend_bwd */
+  int32_t* plan;
+  /* nullable, >= PR_BLEND_SYNC_BYTES: arrival counters the forward zeroes; handed to pr_blend_bwd of
+   * the same call, its last workgroup reduces d sigma / d gamma / d alpha (no finalize kernel) */
+  int32_t* sync;
 } PRBlendFwdArgs;
 
 typedef struct PRBlendBwdArgs {
@@ -145,6 +156,8 @@ typedef struct PRBlendBwdArgs {
   float* grad_bary;           /* VERTEX out (N,H,W,K,3) (replaces grad_colors) */
   float* grad_vert_colors;    /* VERTEX out (V,3), nullable, accumulated (caller zeroes) */
   const int32_t* pix_count;   /* nullable: as in PRBlendFwdArgs (the same tensor as the forward's) */
+  int32_t* plan;              /* nullable: the forward's plan of the same call (same params, pix_count) */
+  int32_t* sync;              /* nullable: the forward's sync buffer of the same call */
 } PRBlendBwdArgs;
 
 typedef struct PRHeavisideArgs {
@@ -380,6 +393,7 @@ int pr_ktimer_arm(int32_t slot);
 int pr_ktimer_read(int32_t slot, float* ms, char* name, int32_t name_cap);
 
 int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream);
+size_t pr_blend_plan_size(const PRBlendParams* p); /* bytes of PRBlendFwdArgs.plan */
 size_t pr_blend_bwd_workspace_size(const PRBlendBwdArgs* args);
 int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream);
 

@@ -25,6 +25,7 @@ PR_BLEND_RAST_WOVR = 32
 PR_BLEND_AGG_WOVR = 64
 PR_BLEND_SOFT = 128
 PR_GRAD_PREZEROED = 1
+PR_BLEND_SYNC_BYTES = 1024
 PR_DETERMINISTIC = 2
 
 _vp = C.c_void_p
@@ -45,7 +46,7 @@ class PRBlendFwdArgs(C.Structure):
     _fields_ = [("p", PRBlendParams), ("pix_to_face", _vp), ("mask", _vp), ("dists", _vp),
                 ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("image", _vp), ("weights", _vp),
                 ("winners", _vp), ("rast_cache", _vp), ("bary", _vp), ("faces", _vp), ("vert_colors", _vp),
-                ("pix_count", _vp)]
+                ("pix_count", _vp), ("plan", _vp), ("sync", _vp)]
 
 
 class PRBlendBwdArgs(C.Structure):
@@ -55,7 +56,7 @@ class PRBlendBwdArgs(C.Structure):
                 ("grad_zbuf", _vp), ("grad_colors", _vp), ("grad_scalars", _vp),
                 ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("rast_cache", _vp), ("bary", _vp),
                 ("faces", _vp), ("vert_colors", _vp), ("grad_bary", _vp), ("grad_vert_colors", _vp),
-                ("pix_count", _vp)]
+                ("pix_count", _vp), ("plan", _vp), ("sync", _vp)]
 
 
 class PRHeavisideArgs(C.Structure):
@@ -130,6 +131,7 @@ EXPORTS = {
     "pr_abi_version": (C.c_int, []),
     "pr_last_error": (C.c_char_p, []),
     "pr_ktimer_arm": (C.c_int, [C.c_int32]),
+    "pr_blend_plan_size": (C.c_size_t, [C.POINTER(PRBlendParams)]),
     "pr_ktimer_read": (C.c_int, [C.c_int32, C.POINTER(C.c_float), C.c_char_p, C.c_int32]),
     "pr_blend_fwd": (C.c_int, [C.POINTER(PRBlendFwdArgs), _vp]),
     "pr_blend_bwd_workspace_size": (C.c_size_t, [C.POINTER(PRBlendBwdArgs)]),

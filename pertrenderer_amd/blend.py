@@ -292,6 +292,24 @@ def _counts_for(pix_to_face):
     return c.contiguous()
 
 
+def _plan(lib, p, counts, dev):
+    """The entry-balanced segment plan buffer of a fused blend call (None when the library does not
+    plan this call: no valid-prefix counts, or a frame above its plan size)."""
+    if counts is None:
+        return None
+    n = lib.pr_blend_plan_size(nat.C.byref(p))
+    return torch.empty((n + 3) // 4, dtype=torch.int32, device=dev) if n else None
+
+
+# The backward's fused scalar reduction (PRBlendFwdArgs.sync: its last workgroup forms d sigma /
+# d gamma / d alpha instead of a finalize kernel); PR_BLEND_SYNC=0 keeps the separate kernel
+_FUSED_FINALIZE = os.environ.get("PR_BLEND_SYNC", "1") != "0"
+
+
+def _sync(dev):
+    return torch.empty(nat.PR_BLEND_SYNC_BYTES // 4, dtype=torch.int32, device=dev) if _FUSED_FINALIZE else None
+
+
 def _timed(name, fn):
     hook = _timing.active()
     if hook is not None:
@@ -335,13 +353,15 @@ class _FusedBlendFn(torch.autograd.Function):
         soft = bool(cfg["vflags"] & nat.PR_BLEND_SOFT)
         cache = (torch.empty((N, H, W, K, 2), dtype=F32, device=dev)
                  if RAST_CACHE and not soft and any(ctx.needs_input_grad[:7]) else None)
+        plan = None if soft else _plan(nat.load(), p, cfg["counts"], dev)
+        sync = None if soft else _sync(dev)
         a = nat.PRBlendFwdArgs()
         a.p = p
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
-        a.pix_count = nat.ptr(cfg["counts"])
+        a.pix_count, a.plan, a.sync = nat.ptr(cfg["counts"]), nat.ptr(plan), nat.ptr(sync)
         _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
-        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, cache)
+        ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, cache, plan, sync)
         ctx.p = p  # the backward's parameter block is the forward's
         ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc = cfg, noise, sc
@@ -352,7 +372,7 @@ class _FusedBlendFn(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, gimg):
         _no_uniform_grad(ctx.cfg.get("vflags", 0))
-        p2f_c, d_c, z_c, c_c, zn, zf, winners, cache = ctx.saved_tensors
+        p2f_c, d_c, z_c, c_c, zn, zf, winners, cache, plan, sync = ctx.saved_tensors
         sc_dev = ctx.sc_dev
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
         lib = nat.load()
@@ -367,7 +387,7 @@ class _FusedBlendFn(torch.autograd.Function):
         a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
         a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
         a.grad_dists, a.grad_zbuf, a.grad_colors, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gc), nat.ptr(gsc)
-        a.pix_count = nat.ptr(cfg["counts"])
+        a.pix_count, a.plan, a.sync = nat.ptr(cfg["counts"]), nat.ptr(plan), nat.ptr(sync)
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         _timed("blend_bwd", lambda: nat.call("pr_blend_bwd", "pr_blend_bwd", g, a))
@@ -404,9 +424,10 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         a.pix_to_face, a.dists, a.zbuf = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c)
         a.bary, a.faces, a.vert_colors = nat.ptr(b_c), nat.ptr(f_c), nat.ptr(v_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
-        a.pix_count = nat.ptr(cfg["counts"])
+        plan, sync = _plan(nat.load(), p, cfg["counts"], dev), _sync(dev)
+        a.pix_count, a.plan, a.sync = nat.ptr(cfg["counts"]), nat.ptr(plan), nat.ptr(sync)
         _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
-        ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache)
+        ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache, plan, sync)
         ctx.p = p  # the backward's parameter block is the forward's
         ctx.sc_dev = sc_dev
         ctx.cfg, ctx.noise, ctx.sc, ctx.flags = cfg, noise, sc, flags
@@ -417,7 +438,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, gimg):
         _no_uniform_grad(ctx.cfg.get("vflags", 0))
-        p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache = ctx.saved_tensors
+        p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache, plan, sync = ctx.saved_tensors
         sc_dev = ctx.sc_dev
         cfg, noise, sc = ctx.cfg, ctx.noise, ctx.sc
         lib = nat.load()
@@ -436,7 +457,7 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
         a.grad_dists, a.grad_zbuf, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gsc)
         a.grad_bary, a.grad_vert_colors = nat.ptr(gb), nat.ptr(gv)
-        a.pix_count = nat.ptr(cfg["counts"])
+        a.pix_count, a.plan, a.sync = nat.ptr(cfg["counts"]), nat.ptr(plan), nat.ptr(sync)
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         _timed("blend_bwd", lambda: nat.call("pr_blend_bwd", "pr_blend_bwd", g, a))

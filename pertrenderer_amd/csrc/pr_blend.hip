@@ -23,7 +23,10 @@
 // for 24-bit uniforms): a rast slot with |dist/sigma| > 5.8 has the same outcome
 // for every sample, and an agg logit more than 2*5.8*gamma below the pixel's
 // largest logit can never win.
+#include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "pr_common.h"
 
@@ -41,11 +44,11 @@ constexpr int kBProfRec = 12;
 __device__ long long g_blend_prof[2 * kBProfBlocks * kBProfRec];
 #define PR_BPROF_DECL long long bst_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bt_ = __builtin_amdgcn_s_memtime(), \
                       brt_ = __builtin_amdgcn_s_memrealtime()
-#define PR_BPROF_DUMP(which)                                                                   \
-  if (threadIdx.x == 0 && blockIdx.x < kBProfBlocks) {                                         \
+#define PR_BPROF_DUMP(which, rec)                                                              \
+  if (threadIdx.x == 0 && (rec) < kBProfBlocks) {                                              \
     unsigned hw_;                                                                              \
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                          \
-    long long* r_ = g_blend_prof + ((size_t)(which) * kBProfBlocks + blockIdx.x) * kBProfRec;  \
+    long long* r_ = g_blend_prof + ((size_t)(which) * kBProfBlocks + (rec)) * kBProfRec;       \
     r_[0] = brt_; r_[1] = (long long)__builtin_amdgcn_s_memrealtime();                          \
     for (int i_ = 0; i_ < 8; ++i_) r_[2 + i_] = bst_[i_];                                       \
     r_[10] = hw_; r_[11] = 1;                                                                  \
@@ -65,6 +68,7 @@ __device__ long long g_blend_prof[2 * kBProfBlocks * kBProfRec];
 #define PR_BLEND_BWD_WPE 1
 #endif
 
+
 struct Geo {
   int64_t P, PK;  // pixels, slots
   int K, KP1, PB, HW;
@@ -74,12 +78,48 @@ struct Geo {
   int tail;                      // backward: joint masked-tail draw allowed (PR_BLEND_TAIL=0: off)
   int empty;                     // empty-block shortcut allowed (PR_BLEND_EMPTY=0: off)
   int cap;                       // LDS entry records per workgroup (>= K + 1)
+  int seg;                       // segment plan: entries per part E (0: static grid, passes of cap)
+  int lsh_max;                   // segment plan: log2 of the most lanes per pixel a part may use
+  int plan_fwd_list, plan_bwd_list;  // segment plan: int offsets of the two segment lists
 };
 
-// pixel block of this workgroup: centre-out within each image when blocks tile images
 // a value every lane holds alike (read from LDS: a vector register) into a scalar register
 PR_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// Segment plan (PRBlendFwdArgs.plan), int32 words: the header (per kernel: segment count and the
+// entries per part E it was cut with), the per-block entry totals of the forward's and the
+// backward's pixel blocks (uint16, scratch), then the two segment lists (block << 6 | part, in
+// dispatch order).  E is raised on dense frames so that the segments never exceed the kernels'
+// grids (the host's bound T + X: every block's parts fit in T + (total entries) / E).
+constexpr int kPlanFwdSegs = 0, kPlanBwdSegs = 1, kPlanFwdE = 2, kPlanBwdE = 3, kPlanHeader = 8;
+
+// Fused scalar reduction (PRBlendFwdArgs.sync): the backward's workgroups arrive on counters
+// sharded by blockIdx % 8 (one word saturates near 90 atomics / us; the last generation of a
+// grid arrives together), the last arrival of each class on a top counter; the last workgroup
+// overall reads every partial (release / acquire fences around the arrivals) and forms d sigma,
+// d gamma, d alpha -- the work of blend_finalize_kernel, one kernel boundary fewer.  It then
+// zeroes the counters (a second backward of the same forward); pr_blend_fwd zeroes them first.
+constexpr int kSyncStride = 16, kSyncTop = 8 * kSyncStride;
+
+PR_DEV void sync_zero(int32_t* sync) {
+  if (threadIdx.x < 9) sync[threadIdx.x == 8 ? kSyncTop : threadIdx.x * kSyncStride] = 0;
+}
+
+PR_DEV bool last_arrival(int32_t* sync, int nblk, int* flag) {
+  __syncthreads();  // this workgroup's partials are written
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const int r = (int)(blockIdx.x % 8), n_r = (nblk - r + 7) / 8;
+    int last = 0;
+    if (atomicAdd(sync + r * kSyncStride, 1) == n_r - 1) last = atomicAdd(sync + kSyncTop, 1) == min(nblk, 8) - 1;
+    if (last) __threadfence();
+    *flag = last;
+  }
+  __syncthreads();
+  return uni(*flag) != 0;
+}
+
+// pixel block of this workgroup: centre-out within each image when blocks tile images
 PR_DEV int64_t pixel_block(const Geo& g) {
   if (g.bpi == 0) return blockIdx.x;
   const int64_t n = blockIdx.x / g.bpi;
@@ -168,8 +208,17 @@ PR_DEV void fill_owner(uint8_t* OWN, const int* ea, int eb, const int* cl, int n
 // the entries (CL + 1: the background entry), and the passes: maximal runs of consecutive
 // pixels whose entries fit CAP records (CAP >= K + 1, so a pixel always fits), as starts
 // PS[0..np) + end PS[np] = npix, with the pass count in PS[PB + 1].
+PR_DEV int seg_parts(int tot, int E) { return tot > E ? (tot + E - 1) / E : 1; }
+
+// A block's entries (valid slots + background) for the segment plan: the per-pixel count the
+// scan below sums.
+PR_DEV int pixel_entries(const int32_t* pcnt, int64_t gp, int K, bool compact) {
+  return (compact ? min(max((int)pcnt[gp], 0), K) : K) + 1;
+}
+
+// E > 0: the passes are the block's entry-balanced segment parts instead (see below).
 PR_DEV void block_entries(const int32_t* pcnt, int64_t pix0, int npix, int K, bool compact, int CAP, int PB,
-                          int* CL, int* CP, int* EA, int* PS) {
+                          int* CL, int* CP, int* EA, int* PS, int E = 0) {
   const int tid = threadIdx.x;
   const int cp = tid < npix ? (pcnt ? min(max((int)pcnt[pix0 + tid], 0), K) : K) : 0;
   const int c = compact ? cp : K;
@@ -188,6 +237,23 @@ PR_DEV void block_entries(const int32_t* pcnt, int64_t pix0, int npix, int K, bo
   if (tid == 0) {
     EA[npix] = tot;
     PS[0] = 0;
+  }
+  if (E > 0) {
+    // entry-balanced parts (segment plan): n = ceil(tot / E) parts, pixel pl in part
+    // floor(mid * n / tot) with mid its entries' midpoint.  The host keeps 2 (K+1) <= E <=
+    // CAP - (K+1): a part spans tot / n >= (K+1) entries, so no part is empty, and holds at most
+    // E + K + 1 <= CAP.  The plan kernel counts n from tot alone (seg_parts).
+    const int n = seg_parts(tot, E);
+    const int part = tid < npix ? min(n - 1, ((2 * ex + v) * n) / (2 * tot)) : n;
+    for (int j = 1; j < n; ++j) {
+      const int start = __popcll(__ballot(part < j));
+      if (tid == 0) PS[j] = start;
+    }
+    if (tid == 0) {
+      PS[n] = npix;
+      PS[PB + 1] = n;
+    }
+    return;
   }
   // greedy passes, uniform over the wave (every value broadcast by shuffles); one pass
   // when everything fits
@@ -424,11 +490,13 @@ PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
 // fragments it really has, not by K.
 // MULTI: the block may need several passes (CAP < PB * (K + 1)); without it the pass loop
 // is a single straight-line pass (no loop-carried registers: 46 instead of 70 VGPRs).
-template <int NOISE, bool RAST, int CM, bool MULTI>
-__global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(PRBlendFwdArgs a, Geo g, int NC) {
+// One pixel block (tile) of the forward: all of its passes (static grid), or only its segment
+// part `part` of the entry-balanced plan (SEG).  rec: the profile record of this call.
+template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
+PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const Sc& sc, const int64_t blk,
+                     const int part, const int64_t rec) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
-  const Sc sc = resolve(p);
   const int K = g.K, KP1 = g.KP1, PB = g.PB, CAP = g.cap;
   float* A = smem;                 // [CAP] prob (the distance while queued), then int win counts
   float* B = A + CAP;              // [CAP] z_inv, then logits z
@@ -445,10 +513,10 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   int* PXI = reinterpret_cast<int*>(PX);
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
-  const int64_t blk = pixel_block(g), bpix0 = blk * PB;
+  const int64_t bpix0 = blk * PB;
   const int bnpix = (int)min((int64_t)PB, g.P - bpix0);
   const int32_t* pcnt = a.pix_count;
-  if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, pcnt != nullptr, CAP, PB, CL, CP, EA, PS);
+  if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, pcnt != nullptr, CAP, PB, CL, CP, EA, PS, SEG ? g.seg : 0);
   __syncthreads();
   const float gal = sc.gamma / sc.alpha;
   // ---- empty block (no pixel has a valid slot: only background entries): every sample's
@@ -468,12 +536,23 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         a.weights[bpix0 * KP1 + i] = k == K ? (float)p.Sa / (float)p.Sa : 0.f / (float)p.Sa;
       }
     }
+    __syncthreads();  // (SEG: the next segment rewrites this block's LDS)
     return;
   }
 
-  const int npass = MULTI ? uni(PS[PB + 1]) : 1;
-  for (int pass = 0; pass < npass; ++pass) {
+  const int npass = SEG ? 1 : (MULTI ? uni(PS[PB + 1]) : 1);
+  for (int it = 0; it < npass; ++it) {
+  const int pass = SEG ? part : it;
   const int ps = uni(PS[pass]), npix = uni(PS[pass + 1]) - ps;
+  // lanes per pixel in the pixel phases and candidate stripes of the argmax: a segment of few
+  // pixels spreads them over more lanes
+  int lsh = g.lsh, NC = NC0;
+  if constexpr (SEG) {
+    while (lsh < g.lsh_max && (2 << lsh) * npix <= kThreads) ++lsh;
+    const int ng = agg_num_groups(p);
+    while (NC < 64 && npix * ng * NC * 2 <= kThreads && (KP1 + NC * 2 - 1) / (NC * 2) >= 4) NC <<= 1;
+  }
+  const int lpp = 1 << lsh;
   const int64_t pix0 = bpix0 + ps;
   const int* cl = CL + ps;
   const int* cpv = CP + ps;
@@ -481,7 +560,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   const int eb = uni(ea[0]);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   if (tid == 0) *QN = 0;
-  fill_owner(OWN, ea, eb, cl, npix, g.lsh, g.lpp);
+  fill_owner(OWN, ea, eb, cl, npix, lsh, lpp);
   __syncthreads();
   PR_BSTAMP(0);
 
@@ -575,9 +654,9 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   //         argmax candidates (ascending j).  A pixel's entries are its cl slot entries,
   //         then the background (entry cl -> j = K); lanes take contiguous chunks
   {
-    const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
+    const int pl = tid >> lsh, l = tid & (lpp - 1);
     const bool act = pl < npix;
-    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, ckp = (c + g.lpp) >> g.lsh;  // ceil((c+1)/lpp)
+    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, ckp = (c + lpp) >> lsh;  // ceil((c+1)/lpp)
     const int j0 = l * ckp, j1 = min(c + 1, j0 + ckp), k1 = min(c, j1);
     float al = 1.f, zm = kNegInf;
     if (act)
@@ -585,7 +664,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         al *= (1.f - A[e0 + k]);
         zm = fmaxf(zm, B[e0 + k]);
       }
-    for (int m = 1; m < g.lpp; m <<= 1) {
+    for (int m = 1; m < lpp; m <<= 1) {
       al *= __shfl_xor(al, m);
       zm = fmaxf(zm, __shfl_xor(zm, m));
     }
@@ -599,7 +678,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         CNT[e0 + e] = 0;
         zl = fmaxf(zl, z);
       }
-    for (int m = 1; m < g.lpp; m <<= 1) zl = fmaxf(zl, __shfl_xor(zl, m));
+    for (int m = 1; m < lpp; m <<= 1) zl = fmaxf(zl, __shfl_xor(zl, m));
     // candidates: finite logits not below zl - skipm (bounded Box-Muller noise only: a
     // logit further below the best can never win); lane chunks are contiguous, so an
     // exclusive scan of the lane counts gives each lane its output offset
@@ -614,12 +693,12 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         nc += (z > kNegInf && z >= zfloor) ? 1 : 0;
       }
     int inc = nc;  // inclusive scan of the lane counts within the pixel's lanes
-    for (int o = 1; o < g.lpp; o <<= 1) {
-      const int y = __shfl_up(inc, o, g.lpp);
+    for (int o = 1; o < lpp; o <<= 1) {
+      const int y = __shfl_up(inc, o, lpp);
       if (l >= o) inc += y;
     }
     int off = inc - nc;
-    const int tot = __shfl(inc, g.lpp - 1, g.lpp);
+    const int tot = __shfl(inc, lpp - 1, lpp);
     if (act)
       for (int e = j0; e < j1; ++e) {
         const float z = B[e0 + e];
@@ -692,11 +771,11 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   const float fSa = (float)p.Sa;
   if constexpr (CM != 0) {
     // the pixel's lanes sweep its slot entries; only slots that won a sample are read
-    const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
+    const int pl = tid >> lsh, l = tid & (lpp - 1);
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
     if (pl < npix) {
       const int e0 = ea[pl] - eb;
-      for (int k = l; k < cl[pl]; k += g.lpp) {
+      for (int k = l; k < cl[pl]; k += lpp) {
         const int cw = CNT[e0 + k];
         if (cw == 0) continue;
         const float w = (float)cw / fSa;
@@ -707,7 +786,7 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
         acc2 += w * c[2];
       }
     }
-    for (int m = 1; m < g.lpp; m <<= 1) {
+    for (int m = 1; m < lpp; m <<= 1) {
       acc0 += __shfl_xor(acc0, m);
       acc1 += __shfl_xor(acc1, m);
       acc2 += __shfl_xor(acc2, m);
@@ -732,8 +811,25 @@ __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(P
   PR_BSTAMP(5);
   }  // passes
 #ifdef PR_BLEND_PROFILE
-  PR_BPROF_DUMP(0);
+  PR_BPROF_DUMP(0, rec);
 #endif
+}
+
+// Static grid: workgroup = pixel block.  SEG: workgroup b runs segment b of the plan (the grid is
+// the plan's bound on the segment count; workgroups past the plan's count exit at once).
+template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
+__global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(PRBlendFwdArgs a, Geo g, int NC) {
+  if (a.sync && blockIdx.x == 0) sync_zero(a.sync);  // for the backward's fused reduction
+  if constexpr (!SEG) {
+    fwd_tile<NOISE, RAST, CM, MULTI, false>(a, g, NC, resolve(a.p), pixel_block(g), -1, blockIdx.x);
+  } else {
+    const int32_t* plan = a.plan;
+    const int si = blockIdx.x;
+    if (si >= uni(plan[kPlanFwdSegs])) return;
+    const uint32_t code = reinterpret_cast<const uint32_t*>(plan + g.plan_fwd_list)[si];
+    g.seg = uni(plan[kPlanFwdE]);
+    fwd_tile<NOISE, RAST, CM, false, true>(a, g, NC, resolve(a.p), (int64_t)(code >> 6), (int)(code & 63), si);
+  }
 }
 
 // ================================================================= backward
@@ -745,11 +841,14 @@ constexpr int kB2R = PR_BLEND_B2R > 0 ? PR_BLEND_B2R : 1;
 // slots + background) when the masked tail is drawn jointly (B6); otherwise every slot
 // keeps its entry, since injected / Cauchy noise needs each masked slot's own d z.
 // (MULTI: at least 6 waves per SIMD, the occupancy its 24 KB of LDS allows anyway)
-template <int NOISE, bool RAST, int CM, bool MULTI>
-__global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
+//
+// One pixel block of the backward: all passes (static grid) or segment part `part` (SEG); its
+// scalar partials go to partials[4 pidx .. 4 pidx + 4).
+template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
+PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float* partials, const int64_t blk,
+                     const int part, const int64_t pidx) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
-  const Sc sc = resolve(p);
   const int K = g.K, KP1 = g.KP1, PB = g.PB, CAP = g.cap;
   const int Sa = p.Sa;
   float* PR = smem;                    // [CAP] prob
@@ -768,7 +867,7 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
   uint8_t* WN = OWN + CAP;             // [PB][Sa] the forward's winners of the pass
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
-  const int64_t blk = pixel_block(g), bpix0 = blk * PB;
+  const int64_t bpix0 = blk * PB;
   const int bnpix = (int)min((int64_t)PB, g.P - bpix0);
   const int32_t* pcnt = a.pix_count;
   const int ng = agg_num_groups(p), g0 = agg_first_group(p);
@@ -776,7 +875,7 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
   // B6 draws the masked tail jointly (tail_pair) in Philox Gaussian mode when the valid
   // prefix is known; injected noise (parity) and Cauchy noise keep one row per slot
   const bool tail = NOISE == PR_NOISE_PHILOX && !agg_cauchy && pcnt != nullptr && g.tail;
-  if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, tail, CAP, PB, CL, CP, EA, PS);
+  if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, tail, CAP, PB, CL, CP, EA, PS, SEG ? g.seg : 0);
   __syncthreads();
   const float gal = sc.gamma / sc.alpha;
   float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
@@ -790,20 +889,26 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
     block_fill(a.grad_dists + s0, n, 0.f);
     if constexpr (CM == 1) block_fill(a.grad_colors + 3 * s0, 3 * n, 0.f);
     if constexpr (CM == 2) block_fill(a.grad_bary + 3 * s0, 3 * n, 0.f);
-    if (tid < 4) partials[blk * 4 + tid] = 0.f;
+    if (tid < 4) partials[pidx * 4 + tid] = 0.f;
+    __syncthreads();  // (SEG: the next segment rewrites this block's LDS)
     return;
   }
 
-  const int npass = MULTI ? uni(PS[PB + 1]) : 1;
-  for (int pass = 0; pass < npass; ++pass) {
+  const int npass = SEG ? 1 : (MULTI ? uni(PS[PB + 1]) : 1);
+  for (int it = 0; it < npass; ++it) {
+  const int pass = SEG ? part : it;
   const int ps = uni(PS[pass]), npix = uni(PS[pass + 1]) - ps;
+  int lsh = g.lsh;  // lanes per pixel: a segment of few pixels may spread them over more lanes
+  if constexpr (SEG)
+    while (lsh < g.lsh_max && (2 << lsh) * npix <= kThreads) ++lsh;
+  const int lpp = 1 << lsh;
   const int64_t pix0 = bpix0 + ps;
   const int* cl = CL + ps;
   const int* cpv = CP + ps;
   const int* ea = EA + ps;
   const int eb = uni(ea[0]), nent = uni(ea[npix]) - eb;
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
-  fill_owner(OWN, ea, eb, cl, npix, g.lsh, g.lpp, CN);
+  fill_owner(OWN, ea, eb, cl, npix, lsh, lpp, CN);
   __syncthreads();
   PR_BSTAMP(0);
 
@@ -923,14 +1028,14 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
   //          then the background as entry cl -> j = K): z_max + first argmax, exclusive
   //          products for the alpha gradient, logits, unperturbed argmax j0
   {
-    const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
+    const int pl = tid >> lsh, l = tid & (lpp - 1);
     const bool act = pl < npix;
-    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, ckp = (c + g.lpp) >> g.lsh;  // ceil((c+1)/lpp)
+    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, ckp = (c + lpp) >> lsh;  // ceil((c+1)/lpp)
     const int j0c = l * ckp, j1c = min(c + 1, j0c + ckp), k1c = min(c, j1c);
     // chunks of at most kB2R entries (every pixel of the launch: K + 1 <= kB2R * lpp) are read
     // into registers once; the loops below then touch LDS only for their results (same
     // arithmetic, same order)
-    const bool regs = !MULTI && g.KP1 <= kB2R * g.lpp;  // (the multi-pass template keeps its VGPR cap)
+    const bool regs = !MULTI && g.KP1 <= kB2R * lpp;  // (the multi-pass template keeps its VGPR cap)
     float rpr[kB2R], rzz[kB2R];
     if (regs) {
 #pragma unroll
@@ -956,7 +1061,7 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
         tp *= (1.f - PR[e0 + k]);
       }
     }
-    for (int m = 1; m < g.lpp; m <<= 1) {
+    for (int m = 1; m < lpp; m <<= 1) {
       const float oz = __shfl_xor(zm, m);
       const int ok = __shfl_xor(km, m);
       if (oz > zm || (oz == zm && ok < km)) { zm = oz; km = ok; }
@@ -970,13 +1075,13 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
       // exclusive products across the lane chunks (log-step scans up and down the
       // pixel's lanes), then within the chunk
       float inc = tp, sinc = tp;
-      for (int o = 1; o < g.lpp; o <<= 1) {
-        const float y = __shfl_up(inc, o, g.lpp), z = __shfl_down(sinc, o, g.lpp);
+      for (int o = 1; o < lpp; o <<= 1) {
+        const float y = __shfl_up(inc, o, lpp), z = __shfl_down(sinc, o, lpp);
         if (l >= o) inc *= y;
-        if (l + o < g.lpp) sinc *= z;
+        if (l + o < lpp) sinc *= z;
       }
-      const float iu = __shfl_up(inc, 1, g.lpp), sd = __shfl_down(sinc, 1, g.lpp);
-      float pre = l > 0 ? iu : 1.f, suf = l + 1 < g.lpp ? sd : 1.f;
+      const float iu = __shfl_up(inc, 1, lpp), sd = __shfl_down(sinc, 1, lpp);
+      float pre = l > 0 ? iu : 1.f, suf = l + 1 < lpp ? sd : 1.f;
       if (act && l == 0) PX[pl * 12 + 5] = tp * suf;  // prod (1 - prob): a masked slot's exclusive product
       if (regs) {
         float ex[kB2R];
@@ -1020,7 +1125,7 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
         if (z > zb || jb == (1 << 30)) { zb = z; jb = j; }
       }
     }
-    for (int m = 1; m < g.lpp; m <<= 1) {
+    for (int m = 1; m < lpp; m <<= 1) {
       const float oz = __shfl_xor(zb, m);
       const int oj = __shfl_xor(jb, m);
       if (oj != (1 << 30) && (jb == (1 << 30) || oz > zb || (oz == zb && oj < jb))) { zb = oz; jb = oj; }
@@ -1038,7 +1143,7 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
       // interpolated from the vertex colours here, once per such entry
       if (act) {
         const float* gi = PX + pl * 12 + 8;
-        for (int e = l; e < c; e += g.lpp) {
+        for (int e = l; e < c; e += lpp) {
           if (CN[e0 + e] == 0 && e != jb) continue;
           float cc[3];
           slot_color<CM>(a, (pix0 + pl) * K + e, cc);
@@ -1138,18 +1243,18 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
   // ---- B7: d z_max = -sum_k dz_k - dz_K, passed only if max z_inv >= eps; with the tail
   //          draw the masked slots' sum is sum_s AS[s] / Sa
   {
-    const int pl = tid >> g.lsh, l = tid & (g.lpp - 1);
+    const int pl = tid >> lsh, l = tid & (lpp - 1);
     const bool act = pl < npix;
-    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, cks = (c + g.lpp - 1) >> g.lsh;
+    const int c = act ? cl[pl] : 0, e0 = act ? ea[pl] - eb : 0, cks = (c + lpp - 1) >> lsh;
     const int j0c = l * cks, k1c = min(c, j0c + cks);
-    const int nt = act && tail ? Sa : 0, ckt = (nt + g.lpp - 1) >> g.lsh;
+    const int nt = act && tail ? Sa : 0, ckt = (nt + lpp - 1) >> lsh;
     const int t0 = l * ckt, t1 = min(nt, t0 + ckt);
     float s = 0.f, st = 0.f;
     if (act) {
       for (int k = j0c; k < k1c; ++k) s += ZZ[e0 + k];
       for (int t = t0; t < t1; ++t) st += AS[pl * Sa + t];
     }
-    for (int m = 1; m < g.lpp; m <<= 1) {
+    for (int m = 1; m < lpp; m <<= 1) {
       s += __shfl_xor(s, m);
       st += __shfl_xor(st, m);
     }
@@ -1282,24 +1387,23 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
   }
   __syncthreads();
   if (tid < 4) {
-    partials[blk * 4 + tid] = (RED[tid] + RED[4 + tid]) + (RED[8 + tid] + RED[12 + tid]);
+    partials[pidx * 4 + tid] = (RED[tid] + RED[4 + tid]) + (RED[8 + tid] + RED[12 + tid]);
   }
 #ifdef PR_BLEND_PROFILE
   PR_BSTAMP(7);
-  PR_BPROF_DUMP(1);
+  PR_BPROF_DUMP(1, pidx);
 #endif
+  __syncthreads();  // (SEG: the next segment rewrites RED)
 }
 
-// d sigma, d gamma, d alpha from the per-block partials (one workgroup, fixed order)
-__global__ void __launch_bounds__(kThreads) blend_finalize_kernel(const float* partials, int nblk,
-                                                                  PRBlendParams p, int has_rast,
-                                                                  float* out) {
-  __shared__ float red[kThreads * 4];
+// d sigma, d gamma, d alpha from the per-block partials, by one workgroup in a fixed order
+// (deterministic): blocks b, b + 256, ... per thread (four blocks' loads in flight per step: the
+// latency chain of one load per step cost ~6 us), then the waves' xor-shuffle sums, then the
+// four waves in order.  red: 16 floats of LDS.
+PR_DEV void finalize_scalars(const float* partials, int nblk, const PRBlendParams& p, int has_rast, float* out,
+                             float* red) {
   const int tid = threadIdx.x;
-  const Sc sc = resolve(p);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  // blocks b, b+256, ... in order; four blocks' loads in flight per step (the latency chain
-  // of one load per step made this kernel ~6 us)
   int b = tid;
   for (; b + 3 * kThreads < nblk; b += 4 * kThreads) {
     float v[4][4];
@@ -1317,22 +1421,154 @@ __global__ void __launch_bounds__(kThreads) blend_finalize_kernel(const float* p
     for (int c = 0; c < 4; ++c) acc[c] += partials[(int64_t)b * 4 + c];
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) red[tid * 4 + c] = acc[c];
-  __syncthreads();
-  for (int s = kThreads / 2; s > 0; s >>= 1) {
-    if (tid < s) {
+  for (int m = 32; m >= 1; m >>= 1)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) red[tid * 4 + c] += red[(tid + s) * 4 + c];
-    }
-    __syncthreads();
-  }
+    for (int c = 0; c < 4; ++c) acc[c] += __shfl_xor(acc[c], m);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[(tid >> 6) * 4 + c] = acc[c];
+  __syncthreads();
   if (tid == 0) {
-    const float dsig = red[0], Q = red[1], As = red[2], dgal = red[3];
+    const Sc sc = resolve(p);
+    float r[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[c] = (red[c] + red[4 + c]) + (red[8 + c] + red[12 + c]);
+    const float dsig = r[0], Q = r[1], As = r[2], dgal = r[3];
     // smoothagg.py:54-56,72 : mean_s sum a_s (|eps_s|^2 - 1) / gamma
     const float dg1 = ((Q - As) / sc.gamma) / (float)p.Sa;
     out[0] = has_rast ? dsig : 0.f;
     out[1] = dg1 + dgal / sc.alpha;                       // prod_corrected x = gamma/alpha
     out[2] = -dgal * ((sc.gamma / sc.alpha) / sc.alpha);
+  }
+}
+
+template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
+__global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
+  int nblk = (int)gridDim.x;
+  if constexpr (!SEG) {
+    const int64_t blk = pixel_block(g);
+    bwd_tile<NOISE, RAST, CM, MULTI, false>(a, g, resolve(a.p), partials, blk, -1, blk);
+  } else {
+    const int32_t* plan = a.plan;
+    const int si = blockIdx.x;
+    nblk = uni(plan[kPlanBwdSegs]);
+    if (si < nblk) {  // (workgroups past the plan's count still arrive below)
+      const uint32_t code = reinterpret_cast<const uint32_t*>(plan + g.plan_bwd_list)[si];
+      g.seg = uni(plan[kPlanBwdE]);
+      bwd_tile<NOISE, RAST, CM, false, true>(a, g, resolve(a.p), partials, (int64_t)(code >> 6), (int)(code & 63), si);
+    }
+  }
+  if (a.sync) {
+    __shared__ float red[16];
+    __shared__ int flag;
+    if (last_arrival(a.sync, (int)gridDim.x, &flag)) {
+      finalize_scalars(partials, nblk, a.p, RAST ? 1 : 0, a.grad_scalars, red);
+      sync_zero(a.sync);
+    }
+  }
+}
+
+// (plan: the backward ran the plan's segments; their count is read here)
+__global__ void __launch_bounds__(kThreads) blend_finalize_kernel(const float* partials, int nblk,
+                                                                  PRBlendParams p, int has_rast,
+                                                                  float* out, int32_t* plan) {
+  __shared__ float red[16];
+  if (plan) nblk = uni(plan[kPlanBwdSegs]);
+  finalize_scalars(partials, nblk, p, has_rast, out, red);
+}
+
+// ====================================================== segment plan
+// (1) blend_plan_count_kernel, one thread per pixel: every pixel's entries from the valid-prefix
+//     counts, summed over the forward's and the backward's pixel blocks (PB <= 32 adjacent lanes)
+//     -> each block's entry total.  (2) blend_plan_list_kernel, one workgroup: per kernel, the
+//     frame's total entries fix E (at least the host's target; raised so the segments fit the
+//     grid bound T + X), every block's part count seg_parts(tot, E) -- the count block_entries
+//     splits it into -- an exclusive scan of the part counts in dispatch order (the forward's
+//     blocks centre-out on single frames, as its static grid) and the segment list.
+constexpr int kPlanThreads = 1024;
+constexpr int64_t kPlanMaxPixels = int64_t(1) << 18;
+constexpr int kPlanMaxBlocks = (int)(kPlanMaxPixels / 16) + (int)(kPlanMaxPixels / 32);
+
+struct PlanGeo {
+  int P, K;
+  int PB[2], E[2], lo[2], hi[2], X[2], bpi[2], T[2], list[2], compact[2];  // [0] forward, [1] backward
+  int tots;  // int offset of the uint16 block totals ([T0] forward, then [T1] backward)
+};
+
+PR_DEV int block_of_rank(int r, int bpi) {
+  if (bpi == 0) return r;
+  const int n = r / bpi;
+  return n * bpi + centre_out(r - n * bpi, bpi);
+}
+
+__global__ void __launch_bounds__(kThreads) blend_plan_count_kernel(const int32_t* pcnt, PlanGeo q, int32_t* plan) {
+  const int gp = blockIdx.x * kThreads + threadIdx.x;
+  const int c = gp < q.P ? pcnt[gp] : 0;
+  uint16_t* tots = reinterpret_cast<uint16_t*>(plan + q.tots);
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    int e = gp < q.P ? (q.compact[w] ? min(max(c, 0), q.K) : q.K) + 1 : 0;
+    for (int m = 1; m < q.PB[w]; m <<= 1) e += __shfl_xor(e, m);
+    if (gp < q.P && (gp & (q.PB[w] - 1)) == 0) tots[(w ? q.T[0] : 0) + gp / q.PB[w]] = (uint16_t)e;
+  }
+}
+
+__global__ void __launch_bounds__(kPlanThreads) blend_plan_list_kernel(PlanGeo q, int32_t* plan) {
+  __shared__ uint16_t tl[kPlanMaxBlocks];
+  __shared__ int wsum[kPlanThreads / 64];
+  __shared__ int esh;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint16_t* tots = reinterpret_cast<const uint16_t*>(plan + q.tots);
+  const int TT = q.T[0] + q.T[1];
+  for (int i = tid; i < TT; i += kPlanThreads) tl[i] = tots[i];  // (loads independent: all in flight)
+  __syncthreads();
+  for (int w = 0; w < 2; ++w) {
+    const int T = q.T[w], ch = (T + kPlanThreads - 1) / kPlanThreads;
+    const uint16_t* tw = tl + (w ? q.T[0] : 0);
+    const int r0 = min(T, tid * ch), r1 = min(T, r0 + ch);
+    // the frame's entries -> E
+    int tsum = 0;
+    for (int r = r0; r < r1; ++r) tsum += tw[r];
+    for (int o = 32; o >= 1; o >>= 1) tsum += __shfl_xor(tsum, o);
+    if (lane == 0) wsum[wv] = tsum;
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int i = 0; i < kPlanThreads / 64; ++i) tot += wsum[i];
+      const int need = (tot + q.X[w] - 1) / q.X[w];  // parts <= T + tot / E <= T + X
+      esh = min(max(q.E[w], max(need, q.lo[w])), q.hi[w]);
+    }
+    __syncthreads();
+    const int E = esh;
+    // part counts in dispatch order: chunk sums, block-wide exclusive scan, list
+    int sum = 0;
+    for (int r = r0; r < r1; ++r) sum += seg_parts(tw[block_of_rank(r, q.bpi[w])], E);
+    int x = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    __syncthreads();  // wsum reuse
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int woff = 0, total = 0;
+    for (int i = 0; i < kPlanThreads / 64; ++i) {
+      const int v = wsum[i];
+      woff += i < wv ? v : 0;
+      total += v;
+    }
+    int off = woff + x - sum;
+    uint32_t* list = reinterpret_cast<uint32_t*>(plan + q.list[w]);
+    for (int r = r0; r < r1; ++r) {
+      const int b = block_of_rank(r, q.bpi[w]), n = seg_parts(tw[b], E);
+      for (int j = 0; j < n; ++j) list[off + j] = ((uint32_t)b << 6) | (uint32_t)j;
+      off += n;
+    }
+    if (tid == 0) {
+      plan[w ? kPlanBwdSegs : kPlanFwdSegs] = total;
+      plan[w ? kPlanBwdE : kPlanFwdE] = E;
+    }
+    __syncthreads();  // wsum / esh reuse
   }
 }
 
@@ -1485,31 +1721,36 @@ int color_mode(int flags) {
   return !(flags & PR_BLEND_COLOR) ? 0 : ((flags & PR_BLEND_VERTEX) ? 2 : 1);
 }
 
-template <int NOISE, bool MULTI>
+template <typename Fn, typename... Args>
+void launch_grid(Fn* fn, int nblk, size_t lds, hipStream_t st, Args... args) {
+  hipLaunchKernelGGL(fn, dim3(nblk), dim3(kThreads), lds, st, args...);
+}
+
+template <int NOISE, bool MULTI, bool SEG>
 void launch_fwd(const PRBlendFwdArgs& a, Geo geo, int NC, hipStream_t st, size_t lds, int nblk) {
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
   ktimer_mark(0, "blend_fwd_kernel", st);
-  if (rast && cm == 2) blend_fwd_kernel<NOISE, true, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (rast && cm == 1) blend_fwd_kernel<NOISE, true, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (rast) blend_fwd_kernel<NOISE, true, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (cm == 1) blend_fwd_kernel<NOISE, false, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else if (cm == 2) blend_fwd_kernel<NOISE, false, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
-  else blend_fwd_kernel<NOISE, false, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, NC);
+  if (rast && cm == 2) launch_grid(blend_fwd_kernel<NOISE, true, 2, MULTI, SEG>, nblk, lds, st, a, geo, NC);
+  else if (rast && cm == 1) launch_grid(blend_fwd_kernel<NOISE, true, 1, MULTI, SEG>, nblk, lds, st, a, geo, NC);
+  else if (rast) launch_grid(blend_fwd_kernel<NOISE, true, 0, MULTI, SEG>, nblk, lds, st, a, geo, NC);
+  else if (cm == 1) launch_grid(blend_fwd_kernel<NOISE, false, 1, MULTI, SEG>, nblk, lds, st, a, geo, NC);
+  else if (cm == 2) launch_grid(blend_fwd_kernel<NOISE, false, 2, MULTI, SEG>, nblk, lds, st, a, geo, NC);
+  else launch_grid(blend_fwd_kernel<NOISE, false, 0, MULTI, SEG>, nblk, lds, st, a, geo, NC);
   ktimer_mark(1, "blend_fwd_kernel", st);
 }
 
-template <int NOISE, bool MULTI>
+template <int NOISE, bool MULTI, bool SEG>
 void launch_bwd(const PRBlendBwdArgs& a, Geo geo, hipStream_t st, size_t lds, int nblk, float* part) {
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
   ktimer_mark(0, "blend_bwd_kernel", st);
-  if (rast && cm == 2) blend_bwd_kernel<NOISE, true, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (rast && cm == 1) blend_bwd_kernel<NOISE, true, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (rast) blend_bwd_kernel<NOISE, true, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (cm == 1) blend_bwd_kernel<NOISE, false, 1, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else if (cm == 2) blend_bwd_kernel<NOISE, false, 2, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
-  else blend_bwd_kernel<NOISE, false, 0, MULTI><<<nblk, kThreads, lds, st>>>(a, geo, part);
+  if (rast && cm == 2) launch_grid(blend_bwd_kernel<NOISE, true, 2, MULTI, SEG>, nblk, lds, st, a, geo, part);
+  else if (rast && cm == 1) launch_grid(blend_bwd_kernel<NOISE, true, 1, MULTI, SEG>, nblk, lds, st, a, geo, part);
+  else if (rast) launch_grid(blend_bwd_kernel<NOISE, true, 0, MULTI, SEG>, nblk, lds, st, a, geo, part);
+  else if (cm == 1) launch_grid(blend_bwd_kernel<NOISE, false, 1, MULTI, SEG>, nblk, lds, st, a, geo, part);
+  else if (cm == 2) launch_grid(blend_bwd_kernel<NOISE, false, 2, MULTI, SEG>, nblk, lds, st, a, geo, part);
+  else launch_grid(blend_bwd_kernel<NOISE, false, 0, MULTI, SEG>, nblk, lds, st, a, geo, part);
   ktimer_mark(1, "blend_bwd_kernel", st);
 }
 
@@ -1550,6 +1791,71 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   return g;
 }
 
+// The segment plan's configuration for a call (both kernels: the forward computes the plan, the
+// backward of the same call reads it, so both derive it from the same parameters).  Off without
+// valid-prefix counts, on frames larger than kPlanMaxPixels (one plan workgroup; many-generation
+// grids gain little), and with PR_BLEND_SEG=0.  E: entries per part, PR_BLEND_SEG_FWD / _BWD.
+struct PlanCfg {
+  bool on = false;
+  PlanGeo q{};
+  int lsh_max[2] = {0, 0};
+  size_t bytes = 0;
+};
+
+PlanCfg plan_cfg(const PRBlendParams& p, const int32_t* pcnt) {
+  PlanCfg c;
+  // Off by default (PR_BLEND_SEG=1 opts in; read per call: tests compare both paths in one process).
+  // Measured at cfg 2 (profiles/r4_blend_segments.txt): the backward kernel 74.7 -> 66.8 us at
+  // E = 768, but the two plan kernels cost ~15 us and the forward's parts overflow its resident
+  // workgroups (forward kernel 46 -> 53 us): a net loss of ~20 us per step.
+  const char* env = getenv("PR_BLEND_SEG");
+  const int64_t P = (int64_t)p.N * p.H * p.W;
+  if (!pcnt || P > kPlanMaxPixels || !(env && atoi(env) != 0)) return c;
+  const int KP1 = p.K + 1;
+  // (read per call: tests drive several segment sizes in one process)
+  const int e_env[2] = {getenv("PR_BLEND_SEG_FWD") ? atoi(getenv("PR_BLEND_SEG_FWD")) : 0,
+                        getenv("PR_BLEND_SEG_BWD") ? atoi(getenv("PR_BLEND_SEG_BWD")) : 0};
+  // lanes per pixel a part of few pixels may spread over (PR_BLEND_SEG_LPP / _BWD, sweeps).  Default:
+  // the static grid's, which keeps every per-pixel reduction in the same order
+  const int l_env[2] = {getenv("PR_BLEND_SEG_LPP") ? atoi(getenv("PR_BLEND_SEG_LPP")) : 0,
+                        getenv("PR_BLEND_SEG_LPP_BWD") ? atoi(getenv("PR_BLEND_SEG_LPP_BWD")) : 0};
+  constexpr int kDefaultE[2] = {512, 512};
+  int64_t tblocks = 0, off = kPlanHeader;
+  for (int w = 0; w < 2; ++w) {
+    const Shape sh = pick_shape(KP1, p.Sa, P, w == 1);
+    const Geo g = make_geo(p, sh.PB, w == 1);
+    // 2 (K+1) <= E <= CAP - (K+1): parts are never empty and always fit the LDS records
+    const int lo = 2 * KP1, hi = sh.cap - KP1;
+    if (sh.PB < 4 || lo > hi) return c;
+    c.q.PB[w] = sh.PB;
+    c.q.E[w] = e_env[w] > 0 ? e_env[w] : kDefaultE[w];
+    c.q.lo[w] = lo;
+    c.q.hi[w] = hi;
+    c.q.X[w] = (int)((P * KP1 + hi - 1) / hi);  // a dense frame's parts at E = hi
+    c.q.bpi[w] = g.bpi;
+    c.q.T[w] = (int)((P + sh.PB - 1) / sh.PB);
+    int ls = g.lsh;
+    while (ls < 6 && (2 << ls) <= l_env[w]) ++ls;
+    c.lsh_max[w] = ls;
+    tblocks += c.q.T[w];
+  }
+  if (tblocks > kPlanMaxBlocks) return c;
+  c.q.P = (int)P;
+  c.q.K = p.K;
+  c.q.compact[0] = 1;
+  // the backward compacts its entries when it draws the masked tail jointly (blend_bwd_kernel's tail)
+  c.q.compact[1] = p.noise_mode == PR_NOISE_PHILOX && !(p.flags & PR_BLEND_AGG_CAUCHY) && make_geo(p, c.q.PB[1], true).tail;
+  for (int w = 0; w < 2; ++w) {
+    c.q.list[w] = (int)off;
+    off += c.q.T[w] + c.q.X[w];
+  }
+  c.q.tots = (int)off;
+  off += (tblocks + 1) / 2;
+  c.bytes = (size_t)off * sizeof(int32_t);
+  c.on = true;
+  return c;
+}
+
 int64_t bwd_blocks(const PRBlendParams& p) {
   const int PB = pick_shape(p.K + 1, p.Sa, (int64_t)p.N * p.H * p.W, true).PB;
   const int64_t P = (int64_t)p.N * p.H * p.W;
@@ -1582,15 +1888,15 @@ extern "C" int pr_diag_blend_occupancy(int K, int Sa, long long P, int cm, int* 
     return n;
   };
   if (cm == 2) {
-    out[0] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 2, false>, lf);
-    out[1] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 2, true>, lf);
-    out[2] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 2, false>, lb);
-    out[3] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 2, true>, lb);
+    out[0] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 2, false, false>, lf);
+    out[1] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 2, true, false>, lf);
+    out[2] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 2, false, false>, lb);
+    out[3] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 2, true, false>, lb);
   } else {
-    out[0] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 1, false>, lf);
-    out[1] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 1, true>, lf);
-    out[2] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 1, false>, lb);
-    out[3] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 1, true>, lb);
+    out[0] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 1, false, false>, lf);
+    out[1] = occ((const void*)blend_fwd_kernel<PR_NOISE_PHILOX, true, 1, true, false>, lf);
+    out[2] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 1, false, false>, lb);
+    out[3] = occ((const void*)blend_bwd_kernel<PR_NOISE_PHILOX, true, 1, true, false>, lb);
   }
   out[4] = out[5] = (int)lf;
   out[6] = out[7] = (int)lb;
@@ -1618,24 +1924,42 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
   const int ng = ((a.p.sample_offset_a + a.p.Sa - 1) >> 2) - (a.p.sample_offset_a >> 2) + 1;
   int NC = 1;
   while (NC < 64 && PB * ng * NC * 2 <= kThreads && (KP1 + NC * 2 - 1) / (NC * 2) >= 4) NC <<= 1;
-  const int64_t nblk = (geo.P + PB - 1) / PB;
+  int64_t nblk = (geo.P + PB - 1) / PB;
   const size_t lds = fwd_lds(PB, sh.cap);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool multi = sh.cap < PB * KP1;
-  if (a.p.noise_mode == PR_NOISE_INJECTED) {
-    if (multi) launch_fwd<PR_NOISE_INJECTED, true>(a, geo, NC, st, lds, (int)nblk);
-    else launch_fwd<PR_NOISE_INJECTED, false>(a, geo, NC, st, lds, (int)nblk);
+  const PlanCfg pc = a.plan ? plan_cfg(a.p, a.pix_count) : PlanCfg{};
+  if (pc.on) {  // entry-balanced segments (blend_plan_kernel) taken by resident workgroups
+    blend_plan_count_kernel<<<(pc.q.P + kThreads - 1) / kThreads, kThreads, 0, st>>>(a.pix_count, pc.q, a.plan);
+    blend_plan_list_kernel<<<1, kPlanThreads, 0, st>>>(pc.q, a.plan);
+    if (int e = check_launch("blend_plan")) return e;
+    geo.lsh_max = pc.lsh_max[0];
+    geo.plan_fwd_list = pc.q.list[0];
+    nblk = pc.q.T[0] + pc.q.X[0];  // the plan's bound on the segments
+    if (a.p.noise_mode == PR_NOISE_INJECTED) launch_fwd<PR_NOISE_INJECTED, false, true>(a, geo, NC, st, lds, (int)nblk);
+    else launch_fwd<PR_NOISE_PHILOX, false, true>(a, geo, NC, st, lds, (int)nblk);
+  } else if (a.p.noise_mode == PR_NOISE_INJECTED) {
+    if (multi) launch_fwd<PR_NOISE_INJECTED, true, false>(a, geo, NC, st, lds, (int)nblk);
+    else launch_fwd<PR_NOISE_INJECTED, false, false>(a, geo, NC, st, lds, (int)nblk);
   } else {
-    if (multi) launch_fwd<PR_NOISE_PHILOX, true>(a, geo, NC, st, lds, (int)nblk);
-    else launch_fwd<PR_NOISE_PHILOX, false>(a, geo, NC, st, lds, (int)nblk);
+    if (multi) launch_fwd<PR_NOISE_PHILOX, true, false>(a, geo, NC, st, lds, (int)nblk);
+    else launch_fwd<PR_NOISE_PHILOX, false, false>(a, geo, NC, st, lds, (int)nblk);
   }
   return check_launch("blend_fwd");
+}
+
+extern "C" size_t pr_blend_plan_size(const PRBlendParams* p) {
+  if (!p || (p->flags & PR_BLEND_SOFT)) return 0;
+  static const int32_t probe = 0;  // any non-null counts pointer
+  const PlanCfg pc = plan_cfg(*p, &probe);
+  return pc.on ? pc.bytes : 0;
 }
 
 extern "C" size_t pr_blend_bwd_workspace_size(const PRBlendBwdArgs* args) {
   if (!args) return 0;
   if (args->p.flags & PR_BLEND_SOFT) return soft_blend_workspace(args->p);
-  return (size_t)bwd_blocks(args->p) * 4 * sizeof(float);
+  const PlanCfg pc = args->plan ? plan_cfg(args->p, args->pix_count) : PlanCfg{};
+  return (size_t)(pc.on ? pc.q.T[1] + pc.q.X[1] : bwd_blocks(args->p)) * 4 * sizeof(float);
 }
 
 extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
@@ -1661,20 +1985,29 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
   const int PB = sh.PB;
   Geo geo = make_geo(a.p, PB, true);
   geo.cap = sh.cap;
-  const int64_t nblk = (geo.P + PB - 1) / PB;
+  int64_t nblk = (geo.P + PB - 1) / PB;
   const size_t lds = bwd_lds(PB, sh.cap, a.p.Sa);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* part = reinterpret_cast<float*>(a.workspace);
   const bool multi = sh.cap < PB * KP1;
-  if (a.p.noise_mode == PR_NOISE_INJECTED) {
-    if (multi) launch_bwd<PR_NOISE_INJECTED, true>(a, geo, st, lds, (int)nblk, part);
-    else launch_bwd<PR_NOISE_INJECTED, false>(a, geo, st, lds, (int)nblk, part);
+  const PlanCfg pc = a.plan ? plan_cfg(a.p, a.pix_count) : PlanCfg{};
+  if (pc.on) {  // the forward's plan: entry-balanced segments taken by resident workgroups
+    geo.lsh_max = pc.lsh_max[1];
+    geo.plan_bwd_list = pc.q.list[1];
+    nblk = pc.q.T[1] + pc.q.X[1];  // the plan's bound on the segments
+    if (a.p.noise_mode == PR_NOISE_INJECTED) launch_bwd<PR_NOISE_INJECTED, false, true>(a, geo, st, lds, (int)nblk, part);
+    else launch_bwd<PR_NOISE_PHILOX, false, true>(a, geo, st, lds, (int)nblk, part);
+  } else if (a.p.noise_mode == PR_NOISE_INJECTED) {
+    if (multi) launch_bwd<PR_NOISE_INJECTED, true, false>(a, geo, st, lds, (int)nblk, part);
+    else launch_bwd<PR_NOISE_INJECTED, false, false>(a, geo, st, lds, (int)nblk, part);
   } else {
-    if (multi) launch_bwd<PR_NOISE_PHILOX, true>(a, geo, st, lds, (int)nblk, part);
-    else launch_bwd<PR_NOISE_PHILOX, false>(a, geo, st, lds, (int)nblk, part);
+    if (multi) launch_bwd<PR_NOISE_PHILOX, true, false>(a, geo, st, lds, (int)nblk, part);
+    else launch_bwd<PR_NOISE_PHILOX, false, false>(a, geo, st, lds, (int)nblk, part);
   }
   if (int e = check_launch("blend_bwd")) return e;
-  blend_finalize_kernel<<<1, kThreads, 0, st>>>(part, (int)nblk, a.p, rast ? 1 : 0, a.grad_scalars);
+  if (a.sync) return PR_OK;  // the scalars were reduced by the kernel's last workgroup
+  blend_finalize_kernel<<<1, kThreads, 0, st>>>(part, (int)nblk, a.p, rast ? 1 : 0, a.grad_scalars,
+                                                pc.on ? a.plan : nullptr);
   return check_launch("blend_finalize");
 }
 

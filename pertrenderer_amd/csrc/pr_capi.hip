@@ -32,7 +32,7 @@ void ktimer_mark(int which, const char* kernel, hipStream_t st) {
   if (g_armed < 0) return;
   KTimer& t = g_timers[g_armed];
   if (which == 0) t.kernel = kernel;
-  hipEventRecord(t.ev[which], st);
+  (void)hipEventRecord(t.ev[which], st);
   if (which == 1) g_armed = -1;
 }
 
@@ -47,10 +47,10 @@ extern "C" int pr_ktimer_arm(int32_t slot) {
   if (slot < 0 || slot >= kTimerSlots) return set_error(PR_ERR_ARG, "ktimer: slot out of range");
   KTimer& t = g_timers[slot];
   int dev = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   if (t.device != dev) {
     for (auto& e : t.ev) {
-      if (e) hipEventDestroy(e);
+      if (e) (void)hipEventDestroy(e);
       e = nullptr;
       if (hipEventCreate(&e) != hipSuccess) return set_error(PR_ERR_HIP, "ktimer: hipEventCreate failed");
     }

@@ -1488,7 +1488,10 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int
   __shared__ int hkey[kHash];
   __shared__ int hfl[kHash];                      // tile-local face index of a hash entry
   __shared__ int flist[kBwdFaces];                // face id of each tile-local index
-  __shared__ uint16_t M[kBwdFaces * TP];          // [face][pixel] -> entry index of this round
+  // [pixel / 4][face][pixel % 4] -> entry index of this round: the transpose's owner lanes (one
+  // per face) read 4 pixels' entries as one 8-B word at consecutive addresses (the [face][pixel]
+  // layout put the lanes 32 B apart: 8-way bank conflicts)
+  __shared__ alignas(8) uint16_t M[kBwdFaces * TP];
   __shared__ float gbuf[9 * kBwdEnt];             // [component][entry]; reused for the sums
   __shared__ int2 clist[kBwdEnt];                 // (pixel << 16 | k, face id)
   __shared__ int ccount, nface;
@@ -1589,7 +1592,7 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int
       if (fl < kBwdFaces) {
 #pragma unroll
         for (int cc = 0; cc < 9; ++cc) gbuf[cc * kBwdEnt + j] = g[cc];
-        M[fl * TP + pix] = (uint16_t)j;
+        M[((pix >> 2) * kBwdFaces + fl) * 4 + (pix & 3)] = (uint16_t)j;
       } else {
 #pragma unroll
         for (int cc = 0; cc < 9; ++cc) atomicAdd(&a.grad_face_verts[(int64_t)fi * 9 + cc], g[cc]);
@@ -1598,11 +1601,11 @@ __global__ void __launch_bounds__(kBwdThreads) rast_bwd_kernel(PRRastArgs a, int
     __syncthreads();
     // ---- 3. transpose: owner lanes sum their face's entries (and reset their M row)
     if (tid < min(nface, kBwdFaces)) {
-      uint16_t* row = M + tid * TP;
+      uint64_t* col = reinterpret_cast<uint64_t*>(M) + tid;
       for (int q = 0; q < nrows * kBwdTile; q += 4) {
-        const uint64_t four = *reinterpret_cast<const uint64_t*>(row + q);
+        const uint64_t four = col[(q >> 2) * kBwdFaces];
         if (four == ~0ull) continue;
-        *reinterpret_cast<uint64_t*>(row + q) = ~0ull;
+        col[(q >> 2) * kBwdFaces] = ~0ull;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const uint32_t jj = (uint32_t)(four >> (16 * t)) & 0xffffu;

@@ -10,8 +10,15 @@ start event before the host has submitted the launch, and the interval would inc
 host time (Python, argument packing).  ``lead_cycles`` enqueues a device-side spin
 (``torch.cuda._sleep``) before the start event, long enough for the host to submit the
 launch behind it, so start event -> kernels -> stop event run back to back on the GPU.
+
+Besides the call-level pair, the timer arms the library's own kernel timer
+(``pr_ktimer_arm``): the native call then records a second pair on its launch stream
+right around its dominant kernel (blend_fwd_kernel, blend_bwd_kernel, rast_fwd_kernel,
+rast_bwd_kernel), so ``kernel_summary`` reports that kernel's duration alone, named as
+rocprofv3 names it -- the basis of bench.py's roofline.
 """
 import collections
+import ctypes
 
 import torch
 

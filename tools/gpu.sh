@@ -19,7 +19,7 @@ R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out"; mkdir -p "$OUT"; cd "$R"
 CMD="${1:-quick}"; shift || true
 
 summ() {  # summary of a bench json
-  python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], d['value'], d['ms_per_step'], d['config']['execution'], {k:(v['ms'],v.get('launches')) for k,v in d['kernels'].items()}, 'roofline', d['roofline']['kernel'], d['roofline']['frac'], 'dense', {k:v['frac'] for k,v in d.get('roofline_dense',{}).items()}, 'cpu', d.get('cpu_baseline',{}).get('value'))" "$1" "$2"
+  python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], d['value'], d['ms_per_step'], d['config']['execution'], {k:(v['ms'],v.get('kernel_ms')) for k,v in d['kernels'].items()}, 'roofline', d['roofline']['kernel'], d['roofline']['frac'], 'dense', {k:v['frac'] for k,v in d.get('roofline_dense',{}).items()}, 'cpu', d.get('cpu_baseline',{}).get('value'))" "$1" "$2"
 }
 
 tests() {
