@@ -127,7 +127,9 @@ typedef struct PRBlendFwdArgs {
    * keep it for pr_blend_bwd */
   int32_t* plan;
   /* nullable, >= PR_BLEND_SYNC_BYTES: arrival counters the forward zeroes; handed to pr_blend_bwd of
-   * the same call, its last workgroup reduces d sigma / d gamma / d alpha (no finalize kernel) */
+   * the same call, its last workgroup reduces d sigma / d gamma / d alpha (no finalize kernel).
+   * Measured slower (each workgroup's release fence writes back L2): the package passes NULL
+   * unless PR_BLEND_SYNC=1 */
   int32_t* sync;
 } PRBlendFwdArgs;
 

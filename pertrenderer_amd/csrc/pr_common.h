@@ -136,4 +136,10 @@ int detsum_layout(void* ws, size_t bytes, int64_t n, int64_t M, int C, DetSum& d
 int detsum_sort(const DetSum& d, hipStream_t st);
 int detsum_gather(const DetSum& d, hipStream_t st);
 int detsum_reduce(const DetSum& d, float* out, int64_t chunk, bool accumulate, hipStream_t st);
+// one sequential pass per key; first: out = the batch's sums (0 for keys without entries), else the
+// chains continue from out (keys without entries keep it)
+int detsum_reduce_chain(const DetSum& d, float* out, bool first, hipStream_t st);
+// entries per batch of the deterministic-mode scatters (bounds their workspace: ~90 B per entry);
+// PR_DET_BATCH overrides (tests drive the batched path on small frames; read per call)
+int64_t det_batch();
 }  // namespace pr

@@ -14,6 +14,11 @@
 //      sequential pass: exactly the order of a serial loop over the entries, as the CPU oracle's
 //      (PyTorch3D's CPU) backward accumulates.  Either way the result depends only on the
 //      entries, never on timing.
+//   5. detsum_reduce_chain: a long entry range in batches (bounded workspace): the first batch
+//      sums from 0, every later one continues each key's sequential chain from the previous
+//      batches' total -- bitwise one serial loop over all the entries.
+#include <cstdlib>
+
 #include <hipcub/hipcub.hpp>
 
 #include "pr_common.h"
@@ -82,10 +87,11 @@ PR_DEV void seq_sum(const float* vals, int64_t s, int64_t e, float acc[C]) {
     for (int c = 0; c < C; ++c) acc[c] += vals[j * C + c];
 }
 
-// pass 1: the head of each chunk sums its chunk into its own sorted position
+// pass 1: the head of each chunk sums its chunk into its own sorted position (init: the chain
+// continues from out[k] -- detsum_reduce_chain; one chunk per key then)
 template <int C>
 __global__ void chunk_kernel(const uint32_t* keys, const uint32_t* start, const uint32_t* end, float* vals,
-                             int64_t n, int64_t M, int64_t chunk) {
+                             int64_t n, int64_t M, int64_t chunk, const float* init) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t k = keys[i];
     if (k >= (uint64_t)M) continue;
@@ -93,7 +99,7 @@ __global__ void chunk_kernel(const uint32_t* keys, const uint32_t* start, const 
     if ((i - s) % chunk != 0) continue;
     float acc[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) acc[c] = 0.f;
+    for (int c = 0; c < C; ++c) acc[c] = init ? init[(int64_t)k * C + c] : 0.f;
     seq_sum<C>(vals, i, i + chunk < e ? i + chunk : e, acc);
 #pragma unroll
     for (int c = 0; c < C; ++c) vals[i * C + c] = acc[c];
@@ -101,11 +107,19 @@ __global__ void chunk_kernel(const uint32_t* keys, const uint32_t* start, const 
 }
 
 // pass 2: per key, its chunk sums in order (one chunk: the plain sequential sum of pass 1)
+// (accumulate: 0 out = sum, 1 out += sum, 2 chained -- the single chunk already started from out;
+// keys without entries keep out)
 template <int C>
 __global__ void segment_kernel(const uint32_t* start, const uint32_t* end, const float* vals, float* out, int64_t M,
                                int64_t chunk, int accumulate) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < M; k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = start[k], e = end[k];
+    if (accumulate == 2) {
+      if (s < e)
+#pragma unroll
+        for (int c = 0; c < C; ++c) out[k * C + c] = vals[s * C + c];
+      continue;
+    }
     float acc[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) acc[c] = 0.f;
@@ -181,14 +195,16 @@ int detsum_gather(const DetSum& d, hipStream_t st) {
   return check_launch("detsum_gather");
 }
 
-int detsum_reduce(const DetSum& d, float* out, int64_t chunk, bool accumulate, hipStream_t st) {
+namespace {
+int reduce_impl(const DetSum& d, float* out, int64_t chunk, int mode, hipStream_t st) {
   if (d.M <= 0) return PR_OK;
   if (d.n <= 0) {
-    if (!accumulate && hipMemsetAsync(out, 0, (size_t)d.M * d.C * 4, st) != hipSuccess)
+    if (mode == 0 && hipMemsetAsync(out, 0, (size_t)d.M * d.C * 4, st) != hipSuccess)
       return set_error(PR_ERR_HIP, "deterministic scatter: memset failed");
     return PR_OK;
   }
   if (chunk <= 0) chunk = d.n;
+  const float* init = mode == 2 ? out : nullptr;
   if (hipMemsetAsync(d.start, 0, (size_t)d.M * 4, st) != hipSuccess ||
       hipMemsetAsync(d.end, 0, (size_t)d.M * 4, st) != hipSuccess)
     return set_error(PR_ERR_HIP, "deterministic scatter: memset failed");
@@ -198,10 +214,10 @@ int detsum_reduce(const DetSum& d, float* out, int64_t chunk, bool accumulate, h
 #define PR_DETSUM_C(CC)                                                                                      \
   case CC:                                                                                                   \
     chunk_kernel<CC><<<blocks(d.n), kThreads, 0, st>>>(d.keys_sorted, d.start, d.end, d.vals_sorted, d.n,    \
-                                                       d.M, chunk);                                          \
+                                                       d.M, chunk, init);                                    \
     if (int e = check_launch("detsum_chunk")) return e;                                                      \
     segment_kernel<CC><<<blocks(d.M), kThreads, 0, st>>>(d.start, d.end, d.vals_sorted, out, d.M, chunk,     \
-                                                         accumulate ? 1 : 0);                                \
+                                                         mode);                                              \
     break;
     PR_DETSUM_C(1) PR_DETSUM_C(3) PR_DETSUM_C(6) PR_DETSUM_C(9)
 #undef PR_DETSUM_C
@@ -209,6 +225,21 @@ int detsum_reduce(const DetSum& d, float* out, int64_t chunk, bool accumulate, h
       return set_error(PR_ERR_ARG, "deterministic scatter: C must be 1, 3, 6 or 9");
   }
   return check_launch("detsum_segment");
+}
+}  // namespace
+
+int64_t det_batch() {
+  const char* e = getenv("PR_DET_BATCH");
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? (int64_t)v : (int64_t(1) << 24);
+}
+
+int detsum_reduce(const DetSum& d, float* out, int64_t chunk, bool accumulate, hipStream_t st) {
+  return reduce_impl(d, out, chunk, accumulate ? 1 : 0, st);
+}
+
+int detsum_reduce_chain(const DetSum& d, float* out, bool first, hipStream_t st) {
+  return reduce_impl(d, out, 0, first ? 0 : 2, st);
 }
 
 }  // namespace pr

@@ -1430,21 +1430,22 @@ PR_DEV void slot_grad_any(const PRRastArgs& a, V2 p, const float* v, int64_t o, 
 
 // ---- deterministic mode (PR_DETERMINISTIC): key every slot by its face (padded slots by F),
 // stable-sort, exact slot gradients at their sorted positions, in-order face sums (pr_detsum.hip)
-__global__ void rast_bwd_keys_kernel(PRRastArgs a, uint32_t* keys, int64_t n) {
-  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t pix = o / a.K;
+// (one batch of slots [s0, s0 + n): entry i is slot s0 + i)
+__global__ void rast_bwd_keys_kernel(PRRastArgs a, uint32_t* keys, int64_t s0, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = s0 + i, pix = o / a.K;
     const bool valid = a.pix_count ? (int)(o - pix * a.K) < a.pix_count[pix] : true;
     const int64_t f = valid ? a.pix_to_face[o] : -1;
-    keys[o] = f >= 0 ? (uint32_t)f : (uint32_t)a.F;
+    keys[i] = f >= 0 ? (uint32_t)f : (uint32_t)a.F;
   }
 }
 
 __global__ void rast_bwd_sorted_grad_kernel(PRRastArgs a, const uint32_t* keys, const uint32_t* idx, float* vals,
-                                            int64_t n) {
+                                            int64_t s0, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t f = keys[i];
     if ((int64_t)f >= a.F) continue;
-    const int64_t o = idx[i];
+    const int64_t o = s0 + idx[i];
     const int64_t pix = o / a.K;
     const int col = (int)(pix % a.W), row = (int)((pix / a.W) % a.H);
     const V2 p{ndc(a.W - 1 - col, a.W, a.H), ndc(a.H - 1 - row, a.H, a.W)};
@@ -1933,22 +1934,28 @@ static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2
 
 extern "C" size_t pr_rast_bwd_workspace_size(const PRRastArgs* a) {
   if (!a || !(a->flags & PR_DETERMINISTIC)) return 0;
-  return detsum_workspace((int64_t)a->N * a->H * a->W * a->K, a->F, 9);
+  return detsum_workspace(std::min<int64_t>((int64_t)a->N * a->H * a->W * a->K, det_batch()), a->F, 9);
 }
 
-// PR_DETERMINISTIC: every face's slot gradients (exact arithmetic) summed in slot order
+// PR_DETERMINISTIC: every face's slot gradients (exact arithmetic) summed in slot order, in
+// batches of det_batch() slots whose sums continue each face's chain (bounded workspace: ~1.5 GB
+// at most, whatever the frame; bitwise the single pass)
 static int rast_bwd_deterministic(const PRRastArgs& a, hipStream_t st) {
-  const int64_t n = (int64_t)a.N * a.H * a.W * a.K;
-  DetSum d;
-  if (int e = detsum_layout(a.workspace, a.workspace_bytes, n, a.F, 9, d)) return e;
+  const int64_t total = (int64_t)a.N * a.H * a.W * a.K, batch = det_batch();
   if (a.F == 0) return PR_OK;
-  const int nb = (int)std::min<int64_t>((n + kThreads - 1) / kThreads, 16384);
-  rast_bwd_keys_kernel<<<nb, kThreads, 0, st>>>(a, d.keys, n);
-  if (int e = check_launch("rast_bwd_keys")) return e;
-  if (int e = detsum_sort(d, st)) return e;
-  rast_bwd_sorted_grad_kernel<<<nb, kThreads, 0, st>>>(a, d.keys_sorted, d.idx_sorted, d.vals_sorted, n);
-  if (int e = check_launch("rast_bwd_sorted_grad")) return e;
-  return detsum_reduce(d, a.grad_face_verts, 0, false, st);
+  for (int64_t s0 = 0; s0 < total; s0 += batch) {
+    const int64_t n = std::min(batch, total - s0);
+    DetSum d;
+    if (int e = detsum_layout(a.workspace, a.workspace_bytes, n, a.F, 9, d)) return e;
+    const int nb = (int)std::min<int64_t>((n + kThreads - 1) / kThreads, 16384);
+    rast_bwd_keys_kernel<<<nb, kThreads, 0, st>>>(a, d.keys, s0, n);
+    if (int e = check_launch("rast_bwd_keys")) return e;
+    if (int e = detsum_sort(d, st)) return e;
+    rast_bwd_sorted_grad_kernel<<<nb, kThreads, 0, st>>>(a, d.keys_sorted, d.idx_sorted, d.vals_sorted, s0, n);
+    if (int e = check_launch("rast_bwd_sorted_grad")) return e;
+    if (int e = detsum_reduce_chain(d, a.grad_face_verts, s0 == 0, st)) return e;
+  }
+  return PR_OK;
 }
 
 extern "C" int pr_rast_bwd(const PRRastArgs* args, void* stream) {

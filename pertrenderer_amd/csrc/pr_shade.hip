@@ -199,15 +199,18 @@ struct ShadeDet {
 
 PR_DEV void put3(float* p, V3 g) { p[0] = g.x; p[1] = g.y; p[2] = g.z; }
 
+// (slots [s0, PK): the deterministic mode runs the frame in batches; the fast path s0 = 0)
 template <bool DET>
-__global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int64_t PK, int64_t HW, Tab tab,
-                                                             ShadeDet det) {
+__global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int64_t s0, int64_t PK, int64_t HW,
+                                                             Tab tab, ShadeDet det) {
   extern __shared__ float lds[];
   if (!DET) {
     for (int i = threadIdx.x; i < tab.size; i += kThreads) lds[i] = 0.f;
     __syncthreads();
   }
-  for (int64_t s = (int64_t)blockIdx.x * kThreads + threadIdx.x; s < PK; s += (int64_t)gridDim.x * kThreads) {
+  for (int64_t s = s0 + (int64_t)blockIdx.x * kThreads + threadIdx.x; s < PK; s += (int64_t)gridDim.x * kThreads) {
+    const int64_t ds = s - s0;  // entry row of this batch (PR_DETERMINISTIC)
+    (void)ds;
     const Slot sl = load_slot(a, s, HW);
     const int n = sl.n;
     const V3 gc = v3(a.grad_colors + s * 3);
@@ -221,10 +224,10 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
       }
       if (DET) {
         if (det.v.n)
-          for (int i = 0; i < 3; ++i) det.v.keys[s * 3 + i] = (uint32_t)det.v.M;
-        if (det.b.n) det.b.keys[s] = (uint32_t)det.b.M;
+          for (int i = 0; i < 3; ++i) det.v.keys[ds * 3 + i] = (uint32_t)det.v.M;
+        if (det.b.n) det.b.keys[ds] = (uint32_t)det.b.M;
         if (det.m.n)
-          for (int c = 0; c < 4; ++c) det.m.keys[s * 4 + c] = (uint32_t)det.m.M;
+          for (int c = 0; c < 4; ++c) det.m.keys[ds * 4 + c] = (uint32_t)det.m.M;
       }
       continue;
     }
@@ -263,8 +266,8 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
       gb[i] = dot(g_P, v3(a.verts + vi * 3)) + dot(g_Nn, v3(a.normals + vi * 3));
       if (DET) {
         if (det.v.n) {
-          det.v.keys[s * 3 + i] = (uint32_t)vi;
-          float* e = det.v.vals + (s * 3 + i) * 9;
+          det.v.keys[ds * 3 + i] = (uint32_t)vi;
+          float* e = det.v.vals + (ds * 3 + i) * 9;
           put3(e, b[i] * g_P);
           put3(e + 3, b[i] * g_Nn);
           put3(e + 6, V3{0.f, 0.f, 0.f});
@@ -285,7 +288,7 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
         const int64_t vi = fv[i];
         gb[i] += dot(g_tex, v3(a.vert_colors + vi * 3));
         if (DET) {
-          if (det.v.n) put3(det.v.vals + (s * 3 + i) * 9 + 6, b[i] * g_tex);
+          if (det.v.n) put3(det.v.vals + (ds * 3 + i) * 9 + 6, b[i] * g_tex);
           continue;
         }
         if (a.grad_vert_colors) acc(lds, tab.useV, tab.cOff + (int)vi * 3, a.grad_vert_colors, vi, b[i] * g_tex);
@@ -305,9 +308,9 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
       for (int c = 0; c < 4; ++c) {
         const bool in = cx[c] >= 0 && cx[c] < a.Wm && cy[c] >= 0 && cy[c] < a.Hm;
         if (DET && det.m.n) {
-          det.m.keys[s * 4 + c] = in ? (uint32_t)(((int64_t)n * a.Hm + (a.Hm - 1 - cy[c])) * a.Wm + cx[c])
+          det.m.keys[ds * 4 + c] = in ? (uint32_t)(((int64_t)n * a.Hm + (a.Hm - 1 - cy[c])) * a.Wm + cx[c])
                                      : (uint32_t)det.m.M;
-          if (in) put3(det.m.vals + (s * 4 + c) * 3, w[c] * g_tex);
+          if (in) put3(det.m.vals + (ds * 4 + c) * 3, w[c] * g_tex);
         }
         if (in) {
           const int64_t ti = ((int64_t)(a.Hm - 1 - cy[c]) * a.Wm + cx[c]) * 3;
@@ -328,9 +331,9 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
     if (a.grad_bary) { a.grad_bary[s * 3] = gb[0]; a.grad_bary[s * 3 + 1] = gb[1]; a.grad_bary[s * 3 + 2] = gb[2]; }
     if (DET) {
       if (det.b.n) {
-        det.b.keys[s] = (uint32_t)n;
-        put3(det.b.vals + s * 6, g_dir);
-        put3(det.b.vals + s * 6 + 3, g_vraw);
+        det.b.keys[ds] = (uint32_t)n;
+        put3(det.b.vals + ds * 6, g_dir);
+        put3(det.b.vals + ds * 6 + 3, g_vraw);
       }
       continue;
     }
@@ -382,9 +385,10 @@ struct DetPlan {
 
 size_t al(size_t b) { return (b + 255) / 256 * 256; }
 
+// sized for one batch of det_batch() slots (the frame runs in batches: shade_bwd_deterministic)
 DetPlan det_plan(const PRShadeArgs& a) {
   DetPlan p{};
-  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+  const int64_t PK = std::min<int64_t>((int64_t)a.N * a.H * a.W * a.K, det_batch());
   const bool vtx = a.grad_verts || a.grad_normals || (a.texture == PR_TEX_VERTEX && a.grad_vert_colors);
   p.nv = vtx && a.V > 0 ? PK * 3 : 0;
   p.Mv = a.V;
@@ -414,23 +418,28 @@ int shade_bwd_deterministic(const PRShadeArgs& a, hipStream_t st) {
   const size_t need = p.wv + p.wb + p.wm + p.out9 + p.out6;
   if (!a.workspace || a.workspace_bytes < need) return set_error(PR_ERR_WORKSPACE, "shade_bwd: workspace too small");
   char* w = reinterpret_cast<char*>(a.workspace);
-  ShadeDet det;
-  if (int e = detsum_layout(w, p.wv, p.nv, p.Mv, 9, det.v)) return e;
-  if (int e = detsum_layout(w + p.wv, p.wb, p.nb, p.Mb, 6, det.b)) return e;
-  if (int e = detsum_layout(w + p.wv + p.wb, p.wm, p.nm, p.Mm, 3, det.m)) return e;
   float* out9 = reinterpret_cast<float*>(w + p.wv + p.wb + p.wm);
   float* out6 = reinterpret_cast<float*>(w + p.wv + p.wb + p.wm + p.out9);
-  const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
+  const int64_t total = (int64_t)a.N * a.H * a.W * a.K, batch = det_batch();
   Tab tab{};
-  shade_bwd_kernel<true><<<shade_blocks(PK), kThreads, 0, st>>>(a, PK, (int64_t)a.H * a.W, tab, det);
-  if (int e = check_launch("shade_bwd_det")) return e;
-  const DetSum* ds[3] = {&det.v, &det.b, &det.m};
-  float* outs[3] = {out9, out6, a.grad_maps};
-  for (int i = 0; i < 3; ++i) {
-    if (ds[i]->n == 0) continue;
-    if (int e = detsum_sort(*ds[i], st)) return e;
-    if (int e = detsum_gather(*ds[i], st)) return e;
-    if (int e = detsum_reduce(*ds[i], outs[i], kDetChunk, false, st)) return e;
+  // batches of slots [s0, s0 + nb): each batch's ordered sums are added to the previous batches'
+  // (deterministic: the batch size is fixed; one batch below det_batch() slots)
+  for (int64_t s0 = 0; s0 < total; s0 += batch) {
+    const int64_t nb = std::min(batch, total - s0);
+    ShadeDet det;
+    if (int e = detsum_layout(w, p.wv, p.nv ? nb * 3 : 0, p.Mv, 9, det.v)) return e;
+    if (int e = detsum_layout(w + p.wv, p.wb, p.nb ? nb : 0, p.Mb, 6, det.b)) return e;
+    if (int e = detsum_layout(w + p.wv + p.wb, p.wm, p.nm ? nb * 4 : 0, p.Mm, 3, det.m)) return e;
+    shade_bwd_kernel<true><<<shade_blocks(nb), kThreads, 0, st>>>(a, s0, s0 + nb, (int64_t)a.H * a.W, tab, det);
+    if (int e = check_launch("shade_bwd_det")) return e;
+    const DetSum* ds[3] = {&det.v, &det.b, &det.m};
+    float* outs[3] = {out9, out6, a.grad_maps};
+    for (int i = 0; i < 3; ++i) {
+      if (ds[i]->n == 0) continue;
+      if (int e = detsum_sort(*ds[i], st)) return e;
+      if (int e = detsum_gather(*ds[i], st)) return e;
+      if (int e = detsum_reduce(*ds[i], outs[i], kDetChunk, s0 > 0, st)) return e;
+    }
   }
   if (p.nv) {
     split_kernel<<<shade_blocks(a.V * 9), kThreads, 0, st>>>(out9, a.V, 9, a.grad_verts, a.grad_normals,
@@ -495,7 +504,7 @@ extern "C" int pr_shade_bwd(const PRShadeArgs* args, void* stream) {
   const int64_t PK = (int64_t)a.N * a.H * a.W * a.K;
   // fewer, fatter workgroups when the LDS table is large (its zero + flush is per workgroup)
   const int nb = std::min(shade_blocks(PK), tab.size > 1024 ? 1024 : 16384);
-  shade_bwd_kernel<false><<<nb, kThreads, (size_t)tab.size * sizeof(float), st>>>(a, PK, (int64_t)a.H * a.W, tab,
+  shade_bwd_kernel<false><<<nb, kThreads, (size_t)tab.size * sizeof(float), st>>>(a, 0, PK, (int64_t)a.H * a.W, tab,
                                                                                   ShadeDet{});
   return check_launch("shade_bwd");
 }

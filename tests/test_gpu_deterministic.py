@@ -180,3 +180,51 @@ def test_normals_gather_matches_atomic_scatter(device):
         out.append((n.detach(), torch.autograd.grad((n * g).sum(), v)[0]))
     assert_close(out[0][0], out[1][0], name="normals")
     assert_close(out[0][1], out[1][1], name="d verts")
+
+
+@pytest.fixture
+def small_batches():
+    """PR_DET_BATCH: the deterministic scatters run in batches of this many entries (default 2^24,
+    which bounds their workspace at cfg 4's 629 M slots); small batches drive the batched path on
+    small frames."""
+    old = os.environ.get("PR_DET_BATCH")
+    os.environ["PR_DET_BATCH"] = "1000"
+    yield
+    if old is None:
+        os.environ.pop("PR_DET_BATCH", None)
+    else:
+        os.environ["PR_DET_BATCH"] = old
+
+
+@pytest.mark.parametrize("persp,clip", [(False, True), (True, True)])
+def test_batched_rasterizer_backward_is_oracle_bitwise(persp, clip, device, deterministic, small_batches):
+    """Batches of 1000 slots whose face sums continue each face's chain (detsum_reduce_chain): still
+    bit for bit the oracle's single serial loop."""
+    fv = np.concatenate([_soup(400, 11, spread=0.6, size=0.5), _soup(200, 12, spread=0.6, size=0.5)])
+    first, nf = np.array([0, 400]), np.array([400, 200])
+    got, p2f, gz, gb, gd = _rast_grad(fv, first, nf, 20, 50, 2e-2, persp, clip, 4, device)
+    assert p2f.size > 10 * 1000 and (p2f >= 0).sum() > 1000
+    np.testing.assert_array_equal(got, rast_ref.rast_bwd(fv, p2f, gz, gb, gd, persp, clip))
+
+
+def test_batched_eval_frame_reproducible_and_close(device, deterministic, small_batches):
+    """Shading's deterministic scatters in batches (each batch's ordered sums added to the previous
+    ones): bitwise reproducible, and the unbatched deterministic path's values at the 1e-5 bar."""
+    a = _eval_frame_grads(device, size=48)
+    b = _eval_frame_grads(device, size=48)
+    for name, x, y in zip(("image", "d log_rot", "d verts", "d light", "d maps"), a, b):
+        assert torch.equal(x, y), name
+    os.environ["PR_DET_BATCH"] = str(1 << 24)
+    c = _eval_frame_grads(device, size=48)
+    for name, x, y in zip(("d log_rot", "d verts", "d light", "d maps"), a[1:], c[1:]):
+        assert_close(x, y, name=name)
+
+
+def test_deterministic_workspace_is_bounded():
+    """The workspace of the deterministic rasterizer backward at cfg 4 (16 x 512^2 x K 150: 629 M
+    slots) is one batch's, not the frame's (~55 GB unbatched)."""
+    from pertrenderer_amd import _native as nat
+    a = nat.PRRastArgs()
+    a.N, a.H, a.W, a.K, a.F = 16, 512, 512, 150, 20000
+    a.flags = nat.PR_DETERMINISTIC
+    assert nat.load().pr_rast_bwd_workspace_size(nat.C.byref(a)) < 3 * 2**30

@@ -17,11 +17,15 @@ from pertrenderer_amd.renderer import Rotate, so3_exponential_map
 from pertrenderer_amd.results import compare_pose_results
 
 pytestmark = pytest.mark.gpu
-H, K, SIGMA, GAMMA, SR, SA = 64, 50, 1e-3, 1e-2, 16, 8
+H, K, SIGMA, GAMMA = 64, 50, 1e-3, 1e-2
+# (Sr, Sa): eval.py's plumbing with nb_samples = 8, and BASELINE cfg 1's nb_samples = 4 (GaussianRast
+# keeps its default Sr = 16: eval.py:124-180, smoothrast.py:137)
+SAMPLES = [(16, 8), (16, 4)]
 
 
-@pytest.fixture
-def setup(device):
+@pytest.fixture(params=SAMPLES, ids=lambda s: f"Sr{s[0]}-Sa{s[1]}")
+def setup(device, request):
+    SR, SA = request.param
     old = pa.noise.get_noise_source()
     pa.set_noise_source("torch")
     torch.manual_seed(0)
@@ -30,10 +34,11 @@ def setup(device):
     target, R_true = gpu.target()
     _, (renderer,) = pose_opt.init_renderers(gpu, R_true, sigma=SIGMA, gamma=GAMMA, nb_samples=SA,
                                              noise_type=("gaussian",))
+    assert (renderer.shader.smoothrast.nb_samples, renderer.shader.get_nb_samples()) == (SR, SA)
     log_rot0 = pose_opt.so3_log_map(R_true @ so3_exponential_map(torch.tensor([[0.2, -0.15, 0.1]], device=device)))
     tex = cpu.meshes.textures
     texture = (tex.faces_uvs_list()[0], tex.verts_uvs_list()[0], tex.maps_padded())
-    yield gpu, cpu, renderer, target[0], R_true, log_rot0, texture
+    yield gpu, cpu, renderer, target[0], R_true, log_rot0, texture, (SR, SA)
     pa.set_noise_source(old)
 
 
@@ -44,7 +49,8 @@ def _gpu_loss(gpu, renderer, target, log_rot):
     return ((img[..., :3] - target) ** 2).mean(), img
 
 
-def _cpu_loss(cpu, texture, target, log_rot):
+def _cpu_loss(cpu, texture, target, log_rot, samples):
+    SR, SA = samples
     R = so3_exponential_map(log_rot)
     m = cpu.meshes.update_padded(Rotate(R).transform_points(cpu.meshes.verts_padded()))
     noise_r = torch.randn((SR, 1, H, H, K))  # smoothrast.py:21, then smoothagg.py:21
@@ -59,7 +65,7 @@ def _cpu_loss(cpu, texture, target, log_rot):
 def test_frame_and_pose_gradient_match_cpu_oracle(setup, deterministic):
     """At the 1e-5 bar; torch.use_deterministic_algorithms makes the GPU's scattered sums
     (rasterizer, shading) in-order sums, the default sums them with float atomics."""
-    gpu, cpu, renderer, target, R_true, log_rot0, texture = setup
+    gpu, cpu, renderer, target, R_true, log_rot0, texture, samples = setup
     lg = log_rot0.clone().requires_grad_(True)
     torch.manual_seed(7)
     old = torch.are_deterministic_algorithms_enabled()
@@ -71,10 +77,9 @@ def test_frame_and_pose_gradient_match_cpu_oracle(setup, deterministic):
         torch.use_deterministic_algorithms(old)
     lc = log_rot0.detach().cpu().clone().requires_grad_(True)
     torch.manual_seed(7)
-    lossc, imgc = _cpu_loss(cpu, texture, target.cpu(), lc)
+    lossc, imgc = _cpu_loss(cpu, texture, target.cpu(), lc, samples)
     lossc.backward()
-    a, e = imgg.detach().cpu().double(), imgc.detach().double()
-    assert float((a - e).abs().max()) < 2e-5, float((a - e).abs().max())
+    assert_close(imgg.detach(), imgc.detach(), name="image")
     assert abs(float(lossg) - float(lossc)) <= 1e-5 * abs(float(lossc))
     assert_close(lg.grad, lc.grad, name="d log_rot")
 
@@ -98,13 +103,14 @@ def _run(step_loss, log_rot0, niter, seed):
 
 
 def test_pose_runs_match_cpu_oracle(setup):
-    gpu, cpu, renderer, target, R_true, log_rot0, texture = setup
+    gpu, cpu, renderer, target, R_true, log_rot0, texture, samples = setup
     n = 25
     lg, rg = _run(lambda r: _gpu_loss(gpu, renderer, target, r), log_rot0, n, 11)
-    lc, rc = _run(lambda r: _cpu_loss(cpu, texture, target.cpu(), r), log_rot0.cpu(), n, 11)
-    # the first iterations coincide to fp32 rounding; later ones may part where a Monte-Carlo
-    # count flips on a sample at its threshold, so the run is compared at the table level
-    np.testing.assert_allclose(lg[:5], lc[:5], rtol=1e-4)
+    lc, rc = _run(lambda r: _cpu_loss(cpu, texture, target.cpu(), r, samples), log_rot0.cpu(), n, 11)
+    # the first iterations coincide to fp32 rounding (the 1e-5 bar); later ones may part where a
+    # Monte-Carlo count flips on a sample at its threshold (the pose differs by ~1e-7 after a few
+    # Adam steps), so the whole run is compared at the table level
+    np.testing.assert_allclose(lg[:5], lc[:5], rtol=1e-5)
     errs = {}
     for name, rot in (("gpu", rg), ("cpu", rc)):
         errs[name] = pose_opt.angle_deg(rot.to(R_true.device), R_true)

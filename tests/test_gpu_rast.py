@@ -37,7 +37,7 @@ def test_native_projection_matches_transform_path(device):
     g = torch.randn_like(fv)
     (gv,) = torch.autograd.grad((fv * g).sum(), v)
     (gr,) = torch.autograd.grad((ref * g).sum(), v)
-    torch.testing.assert_close(gv, gr, rtol=1e-4, atol=1e-5)
+    assert_close(gv, gr, name="d verts")  # 1e-5 relative (conftest)
 
 
 def test_vertex_interpolation_matches_face_gather(device):
@@ -168,7 +168,7 @@ def test_interpolation_matches_oracle_and_backward(device):
     oc = ((bc[..., :, None] * fa).sum(-2)) * m[..., None]
     (oc * gout.cpu()).sum().backward()
     assert_close(b.grad, bc.grad, rtol=1e-5, name="grad_bary")
-    assert_close(a.grad, ac.grad, rtol=1e-4, atol_rel=1e-5, name="grad_attr")
+    assert_close(a.grad, ac.grad, name="grad_attr")
 
 
 @pytest.mark.parametrize("size,K,dist_cam", [(64, 50, 2.7), (24, 16, 2.7), (40, 8, 6.7), (16, 150, 2.7)])
