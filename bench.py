@@ -270,7 +270,9 @@ def build_step(wl, world, mode, device, grad_weight):
     (incl. the Philox key advance) and the Adam step are captured HIP graphs (one graph at
     N=1); sigma/gamma/alpha live on the device so no host synchronisation remains."""
     if mode == "eager":
-        wl.opt = torch.optim.Adam([wl.log_rot], lr=5e-2)
+        # the same Adam update as eval.py:320's torch.optim.Adam, as one fused kernel (the default
+        # multi-tensor path spends ~120 us of host time per step on a single (N,3) parameter)
+        wl.opt = torch.optim.Adam([wl.log_rot], lr=5e-2, fused=True)
 
         def step():
             wl.forward().backward()
@@ -570,6 +572,9 @@ def main():
                                "fwd + L2 loss + bwd + Adam step on the pose (lr 5e-2)",
                    "image_size": Hs, "faces_per_pixel": K, "nb_samples": S, "rast_samples": Sr, "batch": B,
                    "distinct_frames_per_step": distinct, "execution": mode, "parallelism": par,
+                   # where the eager autograd nodes run (host_layer.py): "c++" torch::autograd
+                   # Functions over the C ABI, or the Python Functions
+                   "host_layer": pa.host_layer.layer(),
                    # eval.py:4 sets CUDA_LAUNCH_BLOCKING=1; the HIP runtime honours HIP_LAUNCH_BLOCKING only
                    # (tools/launch_blocking_check.py), so eval.py itself runs launches asynchronously here
                    "launch_blocking": {k: os.environ[k] for k in ("HIP_LAUNCH_BLOCKING", "CUDA_LAUNCH_BLOCKING")

@@ -20,6 +20,7 @@ import threading
 import torch
 
 from . import _native as nat
+from . import host_layer
 from . import noise as noise_mod
 from . import timing as _timing
 from .noise import Noise
@@ -192,6 +193,17 @@ class _ScalarLink(torch.autograd.Function):
                                for i, m in enumerate(ctx.meta))
 
 
+def _new_link(device, vals):
+    """The link node: the C++ layer's when it is in use (its backward waits for the event the C++
+    blend backward records), else _ScalarLink."""
+    ext = host_layer.get()
+    if ext is not None:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        t = lambda v: v if torch.is_tensor(v) else None
+        return ext.scalar_link(t(vals[0]), t(vals[1]), t(vals[2]), idx)
+    return _ScalarLink.apply(device, *vals)
+
+
 def _host_copy(g, ready):
     """g (3,) on the device -> a CPU tensor, waiting only for the event `ready` (when given)."""
     if ready is None or not g.is_cuda:
@@ -230,7 +242,7 @@ def prelink(vals, device):
     if not _linkable(vals, device):
         return None
     key = _key(vals, device)
-    _state()["pre"] = (key, _ScalarLink.apply(device, *vals))
+    _state()["pre"] = (key, _new_link(device, vals))
     return key
 
 
@@ -262,7 +274,7 @@ def _link_scalars(vals, device):
         del st["pre"]
         link = pre[1]
     else:
-        link = _ScalarLink.apply(device, *vals)
+        link = _new_link(device, vals)
     return tuple(float(v.detach()) if torch.is_tensor(v) else float(v) for v in vals), link
 
 
@@ -468,6 +480,36 @@ class _FusedVertexBlendFn(torch.autograd.Function):
                 s_g, g_g, a_g, _link_grad(gsc, need[7]), None, None, None, None, None)
 
 
+def _fused(vertex, dists, zbuf, colors, vert_colors, sigma, gamma, alpha, link, p2f, faces, znear, zfar, cfg):
+    """The fused blend node: the C++ layer's (host_layer.py) when it is in use, else the Python
+    Function.  Both pack the same PRBlendParams and launch the same kernels."""
+    ext = host_layer.get()
+    if ext is not None:
+        tensors = [dists, zbuf, colors, p2f] + ([vert_colors, faces] if vertex else [])
+        if all(t.is_cuda for t in tensors):
+            dev = p2f.device
+            N = p2f.shape[0]
+            sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
+            vals = (sigma, gamma, alpha)
+            # device scalars are read by pointer in the backward too: only leaves whose own storage
+            # the pointer addresses (float32 0-d) are kept alive by the node
+            if sc_dev is None or all(d is None or d.data_ptr() == v.data_ptr() for d, v in zip(sc_dev, vals)):
+                zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
+                noise = cfg["noise"].to(dev)
+                flags = nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | cfg["vflags"]
+                flags |= nat.PR_BLEND_VERTEX if vertex else 0
+                p = _params(tuple(p2f.shape), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf,
+                            flags)
+                t = lambda v: v if torch.is_tensor(v) else None
+                return ext.blend(dists, zbuf, colors, vert_colors, t(sigma), t(gamma), t(alpha), link, p2f, faces,
+                                 cfg["counts"], zn, zf, noise.noise_r, noise.noise_a, noise.seeds,
+                                 nat.C.addressof(p), RAST_CACHE, _FUSED_FINALIZE)
+    if vertex:
+        return _FusedVertexBlendFn.apply(dists, zbuf, colors, vert_colors, sigma, gamma, alpha, link, p2f, faces,
+                                         znear, zfar, cfg)
+    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, link, p2f, znear, zfar, cfg)
+
+
 def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, sigma, gamma, alpha,
                            nb_samples_rast, nb_samples_agg, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0,
                            zfar=100.0, noise=None, fixed_noise=False, rast_kind="gaussian", rast_vr=True,
@@ -491,8 +533,7 @@ def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, s
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
     (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
-    return _FusedVertexBlendFn.apply(dists, zbuf, bary, vert_colors, sigma, gamma, alpha, link, pix_to_face, faces,
-                                     znear, zfar, cfg)
+    return _fused(True, dists, zbuf, bary, vert_colors, sigma, gamma, alpha, link, pix_to_face, faces, znear, zfar, cfg)
 
 
 def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_samples_rast,
@@ -519,7 +560,7 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
     (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
-    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, link, pix_to_face, znear, zfar, cfg)
+    return _fused(False, dists, zbuf, colors, None, sigma, gamma, alpha, link, pix_to_face, None, znear, zfar, cfg)
 
 
 def soft_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, eps=1e-10, background=(1.0, 1.0, 1.0),
@@ -537,7 +578,7 @@ def soft_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, eps=1e-10,
     cfg = dict(Sr=1, Sa=1, eps=float(eps), bg=_background(background), noise=Noise.philox(),
                vflags=nat.PR_BLEND_SOFT, counts=_counts_for(pix_to_face))
     (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
-    return _FusedBlendFn.apply(dists, zbuf, colors, sigma, gamma, alpha, link, pix_to_face, znear, zfar, cfg)
+    return _fused(False, dists, zbuf, colors, None, sigma, gamma, alpha, link, pix_to_face, None, znear, zfar, cfg)
 
 
 # ==================================================== standalone heaviside

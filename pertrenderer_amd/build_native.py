@@ -1,9 +1,10 @@
-"""Build libpertrender.so (gfx950) in-tree with hipcc.
+"""Build libpertrender.so (gfx950) in-tree with hipcc, and the C++ autograd layer over it
+(_pr_torch*.so, csrc/pr_torch.cpp: a torch extension of plain host C++).
 
     python -m pertrenderer_amd.build_native [--force]
 
-The shared library lands next to this file so it travels with the repository
-snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+Both shared libraries land next to this file so they travel with the repository snapshot to
+the GPU box (they are git-ignored, not gpurun-ignored).
 """
 import argparse
 import concurrent.futures
@@ -82,6 +83,42 @@ def build(force=False, verbose=True, out=None, defines=()):
     return lib
 
 
+TORCH_EXT_SRC = os.path.join(CSRC, "pr_torch.cpp")
+
+
+def torch_ext_path():
+    import sysconfig
+    return os.path.join(HERE, "_pr_torch" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_torch_ext(force=False, verbose=True):
+    """g++ of csrc/pr_torch.cpp against the installed torch (headers, libtorch, libc10_hip) and the
+    HIP runtime headers: no device code, so no hipcc.  Rebuilt when the source or the ABI header is
+    newer than the module."""
+    import sysconfig
+    import torch
+    from torch.utils import cpp_extension as ce
+    out = torch_ext_path()
+    deps = [TORCH_EXT_SRC, os.path.join(ROOT, "include", "pertrender.h")]
+    if not force and os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+        return out
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = (["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-w", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+            "-DTORCH_EXTENSION_NAME=_pr_torch", "-DTORCH_API_INCLUDE_EXTENSION_H", "-D__HIP_PLATFORM_AMD__=1",
+            "-DUSE_ROCM=1", f"-I{os.path.join(ROOT, 'include')}", f"-I{rocm}/include",
+            f"-I{sysconfig.get_paths()['include']}"]
+           + [f"-I{p}" for p in ce.include_paths()]
+           + [TORCH_EXT_SRC, "-o", out + ".tmp"]
+           + [f"-L{p}" for p in ce.library_paths()] + [f"-L{rocm}/lib"]
+           + ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lamdhip64"])
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
@@ -89,4 +126,6 @@ if __name__ == "__main__":
     ap.add_argument("-D", dest="defines", action="append", default=[], help="preprocessor define")
     args = ap.parse_args()
     print(build(force=args.force, out=args.out, defines=args.defines))
+    if args.out is None and not args.defines:
+        print(build_torch_ext(force=args.force))
     sys.exit(0)

@@ -1,0 +1,689 @@
+// C++ autograd layer over the C ABI (include/pertrender.h) for the eager step.
+//
+// The eager pose-optimisation step (experiments/eval.py:343-376) runs one autograd node per native
+// op: so3_exponential_map, Rotate.transform_points, MeshRasterizer (projection + rasterizer), the
+// fused perturbed blend (random_rasterizer.py:34-56 with smoothrast.py:12-59 + smoothagg.py:10-73)
+// and the smoothing-scalar gradient link.  As Python autograd.Functions each costs ctypes packing
+// plus Function.apply (~10-50 us of host time per call); here the nodes are
+// torch::autograd::Function subclasses whose forward and backward fill the ABI argument structs
+// and launch through the library's own entry points -- the same kernels, arguments and results
+// as the Python Functions (pertrenderer_amd/blend.py, renderer/rasterizer.py, renderer/transforms.py),
+// which stay the path for HIP-graph capture instrumentation (KernelTimer) and for builds without
+// this extension.
+//
+// The library is not linked: Python hands over the addresses of the entry points of the
+// libpertrender.so it loaded (bind()), so both layers drive the one library instance.
+#include <torch/extension.h>
+#include <torch/csrc/autograd/functions/basic_ops.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "pertrender.h"
+
+namespace {
+
+using at::Tensor;
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+using Opt = c10::optional<Tensor>;
+
+Tensor val(const Opt& t) { return t.has_value() ? *t : Tensor(); }
+
+struct Api {
+  decltype(&pr_abi_version) abi_version = nullptr;
+  decltype(&pr_last_error) last_error = nullptr;
+  decltype(&pr_so3_exp_fwd) so3_exp_fwd = nullptr;
+  decltype(&pr_so3_exp_bwd) so3_exp_bwd = nullptr;
+  decltype(&pr_rotate_fwd) rotate_fwd = nullptr;
+  decltype(&pr_rotate_bwd) rotate_bwd = nullptr;
+  decltype(&pr_project_rast_fwd) project_rast_fwd = nullptr;
+  decltype(&pr_project_bwd) project_bwd = nullptr;
+  decltype(&pr_rast_fwd_workspace_size) rast_fwd_workspace_size = nullptr;
+  decltype(&pr_rast_bwd_workspace_size) rast_bwd_workspace_size = nullptr;
+  decltype(&pr_rast_bwd) rast_bwd = nullptr;
+  decltype(&pr_blend_fwd) blend_fwd = nullptr;
+  decltype(&pr_blend_plan_size) blend_plan_size = nullptr;
+  decltype(&pr_blend_bwd_workspace_size) blend_bwd_workspace_size = nullptr;
+  decltype(&pr_blend_bwd) blend_bwd = nullptr;
+};
+Api g_api;
+bool g_bound = false;
+
+template <class F>
+void bind_one(const std::unordered_map<std::string, int64_t>& addrs, const char* name, F& fn) {
+  auto it = addrs.find(name);
+  if (it == addrs.end() || it->second == 0) throw std::runtime_error(std::string("pr_torch: missing entry ") + name);
+  fn = reinterpret_cast<F>(static_cast<intptr_t>(it->second));
+}
+
+void bind(const std::unordered_map<std::string, int64_t>& addrs) {
+  Api a;
+  bind_one(addrs, "pr_abi_version", a.abi_version);
+  bind_one(addrs, "pr_last_error", a.last_error);
+  bind_one(addrs, "pr_so3_exp_fwd", a.so3_exp_fwd);
+  bind_one(addrs, "pr_so3_exp_bwd", a.so3_exp_bwd);
+  bind_one(addrs, "pr_rotate_fwd", a.rotate_fwd);
+  bind_one(addrs, "pr_rotate_bwd", a.rotate_bwd);
+  bind_one(addrs, "pr_project_rast_fwd", a.project_rast_fwd);
+  bind_one(addrs, "pr_project_bwd", a.project_bwd);
+  bind_one(addrs, "pr_rast_fwd_workspace_size", a.rast_fwd_workspace_size);
+  bind_one(addrs, "pr_rast_bwd_workspace_size", a.rast_bwd_workspace_size);
+  bind_one(addrs, "pr_rast_bwd", a.rast_bwd);
+  bind_one(addrs, "pr_blend_fwd", a.blend_fwd);
+  bind_one(addrs, "pr_blend_plan_size", a.blend_plan_size);
+  bind_one(addrs, "pr_blend_bwd_workspace_size", a.blend_bwd_workspace_size);
+  bind_one(addrs, "pr_blend_bwd", a.blend_bwd);
+  if (a.abi_version() != PR_ABI_VERSION)
+    throw std::runtime_error("pr_torch: built for ABI " + std::to_string(PR_ABI_VERSION) + ", library has " +
+                             std::to_string(a.abi_version()));
+  g_api = a;
+  g_bound = true;
+}
+
+const Api& api() {
+  if (!g_bound) throw std::runtime_error("pr_torch: bind() was not called");
+  return g_api;
+}
+
+void check(int code, const char* what) {
+  if (code != 0)
+    throw std::runtime_error(std::string(what) + " failed (" + std::to_string(code) + "): " + api().last_error());
+}
+
+void* stream_of(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+template <class T>
+T* ptr(const Tensor& t) {
+  return t.defined() ? static_cast<T*>(t.data_ptr()) : nullptr;
+}
+
+// nat.dense: `t` as a contiguous tensor of dtype st (the tensor itself when it already is one)
+Tensor dense(const Tensor& t, at::ScalarType st) {
+  if (!t.defined()) return t;
+  if (t.scalar_type() == st && t.is_contiguous()) return t;
+  return t.to(st).contiguous();
+}
+
+// nat.require_device: a host pointer handed to a kernel would fault the GPU
+void on_device(std::initializer_list<const Tensor*> ts) {
+  for (const Tensor* t : ts)
+    if (t->defined() && !t->is_cuda())
+      throw std::invalid_argument("pertrenderer_amd native ops run on ROCm devices only (got a " +
+                                  t->device().str() + " tensor); there is no CPU fallback");
+}
+
+Tensor empty(at::IntArrayRef shape, at::ScalarType st, const Tensor& like) {
+  return at::empty(shape, like.options().dtype(st));
+}
+
+Tensor workspace(size_t bytes, const Tensor& like) {
+  return at::empty({static_cast<int64_t>(bytes > 0 ? bytes : 1)}, like.options().dtype(at::kByte));
+}
+
+Tensor saved(AutogradContext* ctx, const char* key) {
+  auto it = ctx->saved_data.find(key);
+  return it == ctx->saved_data.end() || it->second.isNone() ? Tensor() : it->second.toTensor();
+}
+
+void keep(AutogradContext* ctx, const char* key, const Tensor& t) {
+  ctx->saved_data[key] = t.defined() ? c10::IValue(t) : c10::IValue();
+}
+
+// torch.autograd.function.once_differentiable: with create_graph the returned gradients carry a
+// node that refuses a second differentiation instead of silently being constants
+variable_list once(const variable_list& grads_in, variable_list out) {
+  if (!at::GradMode::is_enabled()) return out;
+  bool any = false;
+  for (const auto& g : grads_in) any = any || (g.defined() && g.requires_grad());
+  if (!any) return out;
+  variable_list fake;
+  fake.reserve(out.size());
+  for (auto& t : out) {
+    if (t.defined()) {
+      auto d = t.detach();
+      d.set_requires_grad(true);
+      fake.push_back(d);
+    } else {
+      fake.push_back(t);
+    }
+  }
+  auto err = std::make_shared<torch::autograd::DelayedError>(
+      "trying to differentiate twice a function that was marked with @once_differentiable",
+      static_cast<int64_t>(fake.size()));
+  return (*err)(std::move(fake));
+}
+
+// ------------------------------------------------------------------ smoothing-scalar link
+// blend.py's _ScalarLink: the reference's smoothing scalars are CPU 0-d leaves, so every backward
+// brings their gradients to the host.  The blend's backward records an event after the kernels
+// that write its (3,) gradient buffer; the link's backward (reached after the rasterizer's backward
+// is launched: it was created before the rasterizer) waits for that event only, on a side stream.
+struct Ready {
+  std::mutex mu;
+  std::unordered_map<const void*, std::pair<int, hipEvent_t>> pending;  // buffer -> (device, event)
+  std::unordered_map<int, std::vector<hipEvent_t>> free;
+  std::unordered_map<int, std::pair<hipStream_t, float*>> side;  // device -> side stream, pinned (4,)
+};
+Ready& ready() {
+  static Ready* r = new Ready();  // never destroyed: HIP may be torn down first at exit
+  return *r;
+}
+
+void mark_ready(const Tensor& buf, void* stream) {
+  auto& r = ready();
+  const int dev = buf.device().index();
+  hipEvent_t e = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(r.mu);
+    auto& fl = r.free[dev];
+    if (!fl.empty()) {
+      e = fl.back();
+      fl.pop_back();
+    }
+  }
+  if (e == nullptr && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+    throw std::runtime_error("pr_torch: hipEventCreateWithFlags failed");
+  if (hipEventRecord(e, static_cast<hipStream_t>(stream)) != hipSuccess)
+    throw std::runtime_error("pr_torch: hipEventRecord failed");
+  std::lock_guard<std::mutex> lk(r.mu);
+  auto old = r.pending.find(buf.data_ptr());
+  if (old != r.pending.end()) r.free[old->second.first].push_back(old->second.second);
+  r.pending[buf.data_ptr()] = {dev, e};
+}
+
+// g (3,) float on the device -> CPU (3,) float, waiting only for the event recorded for g
+Tensor host_copy(const Tensor& g) {
+  auto& r = ready();
+  const int dev = g.device().index();
+  hipEvent_t e = nullptr;
+  hipStream_t side = nullptr;
+  float* pinned = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(r.mu);
+    auto it = r.pending.find(g.data_ptr());
+    if (it != r.pending.end()) {
+      e = it->second.second;
+      r.pending.erase(it);
+    }
+    auto s = r.side.find(dev);
+    if (s != r.side.end()) {
+      side = s->second.first;
+      pinned = s->second.second;
+    }
+  }
+  auto gc = g.contiguous();
+  if (e == nullptr || gc.scalar_type() != at::kFloat || gc.numel() != 3) return gc.to(at::kCPU);
+  if (side == nullptr) {
+    if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&pinned), 4 * sizeof(float), hipHostMallocDefault) != hipSuccess)
+      throw std::runtime_error("pr_torch: side stream / pinned buffer");
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.side[dev] = {side, pinned};
+  }
+  if (hipStreamWaitEvent(side, e, 0) != hipSuccess ||
+      hipMemcpyAsync(pinned, gc.data_ptr(), 3 * sizeof(float), hipMemcpyDeviceToHost, side) != hipSuccess ||
+      hipStreamSynchronize(side) != hipSuccess)
+    throw std::runtime_error("pr_torch: scalar gradient copy failed");
+  {
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.free[dev].push_back(e);
+  }
+  auto out = at::empty({3}, at::TensorOptions().dtype(at::kFloat));
+  std::memcpy(out.data_ptr(), pinned, 3 * sizeof(float));
+  return out;
+}
+
+struct ScalarMeta {
+  bool defined = false;
+  at::ScalarType dtype = at::kFloat;
+  std::vector<int64_t> shape;
+};
+
+ScalarMeta meta_of(const Tensor& t) {
+  ScalarMeta m;
+  if (t.defined() && t.requires_grad()) {
+    m.defined = true;
+    m.dtype = t.scalar_type();
+    m.shape = t.sizes().vec();
+  }
+  return m;
+}
+
+struct ScalarLinkFn : public torch::autograd::Function<ScalarLinkFn> {
+  static Tensor forward(AutogradContext* ctx, Opt sigma, Opt gamma, Opt alpha, int64_t device) {
+    const Tensor ts[3] = {val(sigma), val(gamma), val(alpha)};
+    for (int i = 0; i < 3; ++i) {
+      auto m = meta_of(ts[i]);
+      ctx->saved_data[std::string("m") + char('0' + i)] =
+          m.defined ? c10::IValue(std::make_tuple(static_cast<int64_t>(m.dtype), m.shape)) : c10::IValue();
+    }
+    return at::empty({3}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device));
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    variable_list out(4);
+    if (!grads[0].defined()) return out;
+    auto host = host_copy(grads[0]);
+    for (int i = 0; i < 3; ++i) {
+      auto v = ctx->saved_data[std::string("m") + char('0' + i)];
+      if (v.isNone()) continue;
+      auto tup = v.toTuple();
+      auto dt = static_cast<at::ScalarType>(tup->elements()[0].toInt());
+      auto shape = tup->elements()[1].toIntVector();
+      out[i] = host[i].to(dt).reshape(shape);
+    }
+    return out;
+  }
+};
+
+Tensor scalar_link(Opt sigma, Opt gamma, Opt alpha, int64_t device) {
+  return ScalarLinkFn::apply(sigma, gamma, alpha, device);
+}
+
+// ------------------------------------------------------------------ pose: so3 exp, rotate
+struct SO3ExpFn : public torch::autograd::Function<SO3ExpFn> {
+  static Tensor forward(AutogradContext* ctx, Tensor log_rot, double eps) {
+    on_device({&log_rot});
+    auto w = dense(log_rot, at::kFloat);
+    auto R = empty({w.size(0), 3, 3}, at::kFloat, w);
+    PRSO3Args a{};
+    a.N = static_cast<int32_t>(w.size(0));
+    a.eps = static_cast<float>(eps);
+    a.log_rot = ptr<float>(w);
+    a.R = ptr<float>(R);
+    at::DeviceGuard dg(w.device());
+    check(api().so3_exp_fwd(&a, stream_of(w)), "pr_so3_exp_fwd");
+    keep(ctx, "w", w);
+    ctx->saved_data["eps"] = eps;
+    return R;
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto w = saved(ctx, "w");
+    if (!grads[0].defined()) return {Tensor(), Tensor()};
+    auto g = dense(grads[0], at::kFloat);
+    auto gw = at::empty_like(w);
+    PRSO3Args a{};
+    a.N = static_cast<int32_t>(w.size(0));
+    a.eps = static_cast<float>(ctx->saved_data["eps"].toDouble());
+    a.log_rot = ptr<float>(w);
+    a.grad_R = ptr<float>(g);
+    a.grad_log_rot = ptr<float>(gw);
+    at::DeviceGuard dg(w.device());
+    check(api().so3_exp_bwd(&a, stream_of(gw)), "pr_so3_exp_bwd");
+    return once(grads, {gw, Tensor()});
+  }
+};
+
+struct RotateFn : public torch::autograd::Function<RotateFn> {
+  static Tensor forward(AutogradContext* ctx, Tensor points, Tensor R) {
+    on_device({&points, &R});
+    auto p = dense(points, at::kFloat);
+    auto r = dense(R, at::kFloat);
+    auto out = at::empty_like(p);
+    PRRotateArgs a{};
+    a.N = static_cast<int32_t>(p.size(0));
+    a.P = static_cast<int32_t>(p.size(1));
+    a.R_batched = r.size(0) > 1;
+    a.points = ptr<float>(p);
+    a.R = ptr<float>(r);
+    a.out = ptr<float>(out);
+    at::DeviceGuard dg(p.device());
+    check(api().rotate_fwd(&a, stream_of(out)), "pr_rotate_fwd");
+    keep(ctx, "p", p);
+    keep(ctx, "r", r);
+    return out;
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto p = saved(ctx, "p"), r = saved(ctx, "r");
+    if (!grads[0].defined()) return {Tensor(), Tensor()};
+    auto g = dense(grads[0], at::kFloat);
+    Tensor gp = ctx->needs_input_grad(0) ? at::empty_like(p) : Tensor();
+    Tensor gr = ctx->needs_input_grad(1) ? at::empty_like(r) : Tensor();
+    PRRotateArgs a{};
+    a.N = static_cast<int32_t>(p.size(0));
+    a.P = static_cast<int32_t>(p.size(1));
+    a.R_batched = r.size(0) > 1;
+    a.points = ptr<float>(p);
+    a.R = ptr<float>(r);
+    a.grad_out = ptr<float>(g);
+    a.grad_points = ptr<float>(gp);
+    a.grad_R = ptr<float>(gr);
+    at::DeviceGuard dg(p.device());
+    check(api().rotate_bwd(&a, stream_of(g)), "pr_rotate_bwd");
+    return once(grads, {gp, gr});
+  }
+};
+
+Tensor so3_exp(const Tensor& log_rot, double eps) { return SO3ExpFn::apply(log_rot, eps); }
+Tensor rotate(const Tensor& points, const Tensor& R) { return RotateFn::apply(points, R); }
+
+// ------------------------------------------------------------------ projection + rasterizer
+// renderer/rasterizer.py _ProjectRasterizeFn: pr_project_rast_fwd, backward pr_rast_bwd then
+// pr_project_bwd into d verts (accumulators zeroed by the forward kernel)
+Tensor per_mesh(const Tensor& m, int64_t N, const char* name) {
+  auto f = m.detach().to(at::kFloat);
+  if (f.dim() != 3 || f.size(1) != 4 || f.size(2) != 4 || (f.size(0) != 1 && f.size(0) != N))
+    throw std::invalid_argument(std::string(name) + " matrices must be (1,4,4) or (N,4,4)");
+  return (f.size(0) != N ? f.expand({N, 4, 4}) : f).contiguous();
+}
+
+void rast_common(PRRastArgs& a, const Tensor& fv, const Tensor& first, const Tensor& nfaces,
+                 const std::vector<int64_t>& cfg, double blur) {
+  a.face_verts = ptr<float>(fv);
+  a.mesh_first_face = ptr<int64_t>(first);
+  a.mesh_num_faces = ptr<int64_t>(nfaces);
+  a.F = fv.size(0);
+  a.N = static_cast<int32_t>(first.size(0));
+  a.H = static_cast<int32_t>(cfg[0]);
+  a.W = static_cast<int32_t>(cfg[1]);
+  a.K = static_cast<int32_t>(cfg[2]);
+  a.blur_radius = static_cast<float>(blur);
+  a.perspective_correct = static_cast<int32_t>(cfg[3]);
+  a.clip_barycentric_coords = static_cast<int32_t>(cfg[4]);
+  a.cull_backfaces = static_cast<int32_t>(cfg[5]);
+  a.bin_size = static_cast<int32_t>(cfg[6]);
+  a.max_faces_per_bin = static_cast<int32_t>(cfg[7]);
+}
+
+void project_common(PRProjectArgs& pa, const Tensor& v, const Tensor& f, const Tensor& first, const Tensor& nfaces,
+                    const Tensor& m1, const Tensor& m2) {
+  pa.verts = ptr<float>(v);
+  pa.faces = ptr<int64_t>(f);
+  pa.mesh_first_face = ptr<int64_t>(first);
+  pa.mesh_num_faces = ptr<int64_t>(nfaces);
+  pa.world_to_view = ptr<float>(m1);
+  pa.proj = ptr<float>(m2);
+  pa.V = v.size(0);
+  pa.F = f.size(0);
+  pa.N = static_cast<int32_t>(first.size(0));
+}
+
+struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn> {
+  // cfg = (H, W, K, perspective_correct, clip, cull, bin_size, max_faces_per_bin)
+  static variable_list forward(AutogradContext* ctx, Tensor verts, Tensor faces, Tensor first, Tensor nfaces,
+                               Tensor w2v, Tensor proj, c10::optional<Tensor> csr_start,
+                               c10::optional<Tensor> csr_corners, std::vector<int64_t> cfg, double blur,
+                               bool need) {
+    if (cfg.size() != 8) throw std::invalid_argument("project_rasterize: cfg must have 8 entries");
+    Tensor cs = csr_start.has_value() ? *csr_start : Tensor(), cc = csr_corners.has_value() ? *csr_corners : Tensor();
+    on_device({&verts, &faces, &first, &nfaces, &w2v, &proj, &cs, &cc});
+    auto v = dense(verts, at::kFloat);
+    auto f = dense(faces, at::kLong);
+    const int64_t N = first.size(0), F = f.size(0);
+    const int64_t H = cfg[0], W = cfg[1], K = cfg[2];
+    auto m1 = per_mesh(w2v, N, "world_to_view"), m2 = per_mesh(proj, N, "projection");
+    auto fv = empty({F, 3, 3}, at::kFloat, v);
+    Tensor gfv = need ? empty({F, 3, 3}, at::kFloat, v) : Tensor();
+    Tensor gv = need ? at::empty_like(v) : Tensor();
+    PRProjectArgs pa{};
+    project_common(pa, v, f, first, nfaces, m1, m2);
+    pa.face_verts = ptr<float>(fv);
+    pa.grad_verts = ptr<float>(gv);
+    PRRastArgs a{};
+    rast_common(a, fv, first, nfaces, cfg, blur);
+    auto p2f = empty({N, H, W, K}, at::kLong, v);
+    auto zbuf = empty({N, H, W, K}, at::kFloat, v);
+    auto bary = empty({N, H, W, K, 3}, at::kFloat, v);
+    auto dists = empty({N, H, W, K}, at::kFloat, v);
+    auto counts = empty({N, H, W}, at::kInt, v);
+    a.pix_to_face = ptr<int64_t>(p2f);
+    a.zbuf = ptr<float>(zbuf);
+    a.bary = ptr<float>(bary);
+    a.dists = ptr<float>(dists);
+    a.pix_count = ptr<int32_t>(counts);
+    a.grad_face_verts = ptr<float>(gfv);
+    at::DeviceGuard dg(v.device());
+    auto ws = workspace(api().rast_fwd_workspace_size(&a), v);
+    a.workspace = ws.data_ptr();
+    a.workspace_bytes = static_cast<size_t>(ws.numel());
+    check(api().project_rast_fwd(&pa, &a, stream_of(v)), "pr_project_rast_fwd");
+    ctx->save_for_backward({p2f, counts});
+    keep(ctx, "v", v);
+    keep(ctx, "f", f);
+    keep(ctx, "first", first);
+    keep(ctx, "nfaces", nfaces);
+    keep(ctx, "m1", m1);
+    keep(ctx, "m2", m2);
+    keep(ctx, "fv", fv);
+    keep(ctx, "gfv", gfv);
+    keep(ctx, "gv", gv);
+    keep(ctx, "csr_start", csr_start.has_value() ? *csr_start : Tensor());
+    keep(ctx, "csr_corners", csr_corners.has_value() ? *csr_corners : Tensor());
+    ctx->saved_data["cfg"] = cfg;
+    ctx->saved_data["blur"] = blur;
+    ctx->saved_data["prezeroed"] = true;
+    ctx->mark_non_differentiable({p2f, counts});
+    ctx->set_materialize_grads(false);
+    return {p2f, zbuf, bary, dists, counts};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    variable_list out(11);
+    auto gfv = saved(ctx, "gfv"), gv = saved(ctx, "gv");
+    if (!gfv.defined()) return out;
+    auto sv = ctx->get_saved_variables();
+    auto p2f = sv[0], counts = sv[1];
+    auto v = saved(ctx, "v"), f = saved(ctx, "f"), first = saved(ctx, "first"), nfaces = saved(ctx, "nfaces");
+    auto m1 = saved(ctx, "m1"), m2 = saved(ctx, "m2"), fv = saved(ctx, "fv");
+    auto cfg = ctx->saved_data["cfg"].toIntVector();
+    // a second backward (retain_graph) finds the accumulators used: zero them again
+    const int32_t flags = ctx->saved_data["prezeroed"].toBool() ? PR_GRAD_PREZEROED : 0;
+    ctx->saved_data["prezeroed"] = false;
+    PRRastArgs a{};
+    rast_common(a, fv, first, nfaces, cfg, ctx->saved_data["blur"].toDouble());
+    a.pix_to_face = ptr<int64_t>(p2f);
+    a.pix_count = ptr<int32_t>(counts);
+    a.flags = flags;
+    auto gz = dense(grads[1], at::kFloat), gb = dense(grads[2], at::kFloat), gd = dense(grads[3], at::kFloat);
+    a.grad_zbuf = ptr<float>(gz);
+    a.grad_bary = ptr<float>(gb);
+    a.grad_dists = ptr<float>(gd);
+    a.grad_face_verts = ptr<float>(gfv);
+    at::DeviceGuard dg(v.device());
+    Tensor ws;
+    if (at::globalContext().deterministicAlgorithms()) {  // nat.deterministic(): slot-order face sums
+      a.flags |= PR_DETERMINISTIC;
+      ws = workspace(api().rast_bwd_workspace_size(&a), v);
+      a.workspace = ws.data_ptr();
+      a.workspace_bytes = static_cast<size_t>(ws.numel());
+    }
+    void* st = stream_of(v);
+    check(api().rast_bwd(&a, st), "pr_rast_bwd");
+    ws = Tensor();
+    PRProjectArgs pa{};
+    project_common(pa, v, f, first, nfaces, m1, m2);
+    pa.grad_face_verts = ptr<float>(gfv);
+    pa.grad_verts = ptr<float>(gv);
+    pa.flags = flags;
+    auto cs = saved(ctx, "csr_start"), cc = saved(ctx, "csr_corners");
+    pa.vert_corner_start = ptr<int64_t>(cs);
+    pa.vert_corners = ptr<int64_t>(cc);
+    check(api().project_bwd(&pa, st), "pr_project_bwd");
+    out[0] = gv;
+    return once(grads, out);
+  }
+};
+
+variable_list project_rasterize(const Tensor& verts, const Tensor& faces, const Tensor& first, const Tensor& nfaces,
+                                const Tensor& w2v, const Tensor& proj, c10::optional<Tensor> csr_start,
+                                c10::optional<Tensor> csr_corners, std::vector<int64_t> cfg, double blur) {
+  // the forward's gradient accumulators are sized when d verts will be wanted (Python's
+  // ctx.needs_input_grad[0]; the C++ context has no edges to ask before the node is executable)
+  const bool need = at::GradMode::is_enabled() && verts.requires_grad();
+  return ProjectRasterizeFn::apply(verts, faces, first, nfaces, w2v, proj, csr_start, csr_corners, cfg, blur, need);
+}
+
+// ------------------------------------------------------------------ fused perturbed blend
+// blend.py _FusedBlendFn (texel colours) / _FusedVertexBlendFn (vertex colours, vertex = true).
+// The parameter block (PRBlendParams: shape, samples, noise keys, by-value / device scalars,
+// planes) is packed by the Python caller and read here by address; every tensor it points to is an
+// argument of this call and is kept for the backward.
+constexpr int kIn = 20;  // forward arguments
+
+struct BlendFn : public torch::autograd::Function<BlendFn> {
+  // differentiable: 0 dists, 1 zbuf, 2 colours (texel) / bary (vertex), 3 vertex colours,
+  // 4 sigma, 5 gamma, 6 alpha (device or CPU 0-d leaves, undefined when passed by value), 7 link
+  // Absent optional arguments are no autograd inputs at all (an undefined tensor cannot be one), so
+  // the edges do not line up with the argument positions: the gradient mask is taken here, from
+  // requires_grad at the call (the meaning of Python's ctx.needs_input_grad)
+  static Tensor forward(AutogradContext* ctx, Tensor dists, Tensor zbuf, Tensor colors, Opt vert_colors_o,
+                        Opt sigma_o, Opt gamma_o, Opt alpha_o, Opt link_o, Tensor p2f, Opt faces_o, Opt counts_o,
+                        Tensor znear, Tensor zfar, Opt noise_r_o, Opt noise_a_o, Opt seeds_o, int64_t params,
+                        bool cache_on, bool sync_on, bool grad_on) {
+    const Tensor vert_colors = val(vert_colors_o), sigma = val(sigma_o), gamma = val(gamma_o), alpha = val(alpha_o);
+    const Tensor link = val(link_o), faces = val(faces_o), counts = val(counts_o);
+    const Tensor noise_r = val(noise_r_o), noise_a = val(noise_a_o), seeds = val(seeds_o);
+    on_device({&dists, &zbuf, &colors, &vert_colors, &p2f, &faces, &counts, &znear, &zfar, &noise_r, &noise_a, &seeds});
+    const Tensor diff[8] = {dists, zbuf, colors, vert_colors, sigma, gamma, alpha, link};
+    int64_t need = 0;
+    for (int i = 0; i < 8; ++i)
+      need |= (grad_on && diff[i].defined() && diff[i].requires_grad()) ? (int64_t{1} << i) : 0;
+    ctx->saved_data["need"] = need;
+    PRBlendParams p;
+    std::memcpy(&p, reinterpret_cast<const void*>(static_cast<intptr_t>(params)), sizeof(p));
+    const bool vertex = (p.flags & PR_BLEND_VERTEX) != 0, soft = (p.flags & PR_BLEND_SOFT) != 0;
+    const int64_t N = p.N, H = p.H, W = p.W, K = p.K;
+    auto p2f_c = dense(p2f, at::kLong);
+    auto d_c = dense(dists, at::kFloat), z_c = dense(zbuf, at::kFloat), c_c = dense(colors, at::kFloat);
+    auto v_c = vertex ? dense(vert_colors, at::kFloat) : Tensor();
+    auto f_c = vertex ? dense(faces, at::kLong) : Tensor();
+    auto image = empty({N, H, W, 4}, at::kFloat, p2f_c);
+    auto winners = empty({N * H * W, p.Sa}, at::kByte, p2f_c);
+    const bool any_grad = need != 0;
+    Tensor cache = cache_on && !soft && any_grad ? empty({N, H, W, K, 2}, at::kFloat, p2f_c) : Tensor();
+    PRBlendFwdArgs a{};
+    a.p = p;
+    a.pix_to_face = ptr<int64_t>(p2f_c);
+    a.dists = ptr<float>(d_c);
+    a.zbuf = ptr<float>(z_c);
+    if (vertex) {
+      a.bary = ptr<float>(c_c);
+      a.faces = ptr<int64_t>(f_c);
+      a.vert_colors = ptr<float>(v_c);
+    } else {
+      a.colors = ptr<float>(c_c);
+    }
+    a.image = ptr<float>(image);
+    a.winners = ptr<uint8_t>(winners);
+    a.rast_cache = ptr<float>(cache);
+    a.pix_count = ptr<int32_t>(counts);
+    at::DeviceGuard dg(p2f_c.device());
+    Tensor plan, sync;
+    if (!soft && counts.defined()) {
+      const size_t n = api().blend_plan_size(&p);
+      if (n) plan = at::empty({static_cast<int64_t>((n + 3) / 4)}, p2f_c.options().dtype(at::kInt));
+    }
+    if (!soft && sync_on) sync = at::empty({PR_BLEND_SYNC_BYTES / 4}, p2f_c.options().dtype(at::kInt));
+    a.plan = ptr<int32_t>(plan);
+    a.sync = ptr<int32_t>(sync);
+    check(api().blend_fwd(&a, stream_of(image)), "pr_blend_fwd");
+    ctx->saved_data["p"] = std::string(reinterpret_cast<const char*>(&p), sizeof(p));
+    const char* names[] = {"p2f", "d", "z", "c", "v", "f", "counts", "zn", "zf", "nr", "na", "seeds",
+                           "winners", "cache", "plan", "sync", "s0", "s1", "s2"};
+    const Tensor ts[] = {p2f_c, d_c, z_c, c_c, v_c, f_c, counts, znear, zfar, noise_r, noise_a, seeds,
+                         winners, cache, plan, sync, sigma, gamma, alpha};
+    for (size_t i = 0; i < sizeof(ts) / sizeof(ts[0]); ++i) keep(ctx, names[i], ts[i]);
+    return image;
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    variable_list out(kIn);
+    const auto pb = ctx->saved_data["p"].toStringRef();
+    PRBlendParams p;
+    std::memcpy(&p, pb.data(), sizeof(p));
+    if (p.flags & PR_BLEND_AGG_UNIFORM)
+      throw std::runtime_error("UniformAgg: the reference implements no gradient for uniform noise "
+                               "(smoothagg.py:64-70)");
+    if (!grads[0].defined()) return out;
+    const bool vertex = (p.flags & PR_BLEND_VERTEX) != 0;
+    const int64_t need = ctx->saved_data["need"].toInt();
+    auto needs = [need](int i) { return ((need >> i) & 1) != 0; };
+    auto p2f = saved(ctx, "p2f"), d = saved(ctx, "d"), z = saved(ctx, "z"), c = saved(ctx, "c");
+    auto v = saved(ctx, "v"), f = saved(ctx, "f");
+    auto g = dense(grads[0], at::kFloat);
+    auto gd = at::empty_like(d), gz = at::empty_like(z), gc = at::empty_like(c);
+    Tensor gv = vertex && needs(3) ? at::zeros_like(v) : Tensor();
+    auto gsc = at::empty({3}, d.options());
+    PRBlendBwdArgs a{};
+    a.p = p;
+    a.pix_to_face = ptr<int64_t>(p2f);
+    a.dists = ptr<float>(d);
+    a.zbuf = ptr<float>(z);
+    if (vertex) {
+      a.bary = ptr<float>(c);
+      a.faces = ptr<int64_t>(f);
+      a.vert_colors = ptr<float>(v);
+      a.grad_bary = ptr<float>(gc);
+      a.grad_vert_colors = ptr<float>(gv);
+    } else {
+      a.colors = ptr<float>(c);
+      a.grad_colors = ptr<float>(gc);
+    }
+    a.winners = ptr<uint8_t>(saved(ctx, "winners"));
+    a.grad_image = ptr<float>(g);
+    a.rast_cache = ptr<float>(saved(ctx, "cache"));
+    a.grad_dists = ptr<float>(gd);
+    a.grad_zbuf = ptr<float>(gz);
+    a.grad_scalars = ptr<float>(gsc);
+    a.pix_count = ptr<int32_t>(saved(ctx, "counts"));
+    a.plan = ptr<int32_t>(saved(ctx, "plan"));
+    a.sync = ptr<int32_t>(saved(ctx, "sync"));
+    at::DeviceGuard dg(d.device());
+    auto ws = workspace(api().blend_bwd_workspace_size(&a), d);
+    a.workspace = ws.data_ptr();
+    a.workspace_bytes = static_cast<size_t>(ws.numel());
+    void* st = stream_of(g);
+    check(api().blend_bwd(&a, st), "pr_blend_bwd");
+    if (needs(0)) out[0] = gd;
+    if (needs(1)) out[1] = gz;
+    if (needs(2)) out[2] = gc;
+    out[3] = gv;
+    // the smoothing scalars (blend.py _scalar_grads): CPU leaves get their three values in ONE copy
+    Tensor host;
+    for (int i = 0; i < 3; ++i) {
+      auto ref = saved(ctx, i == 0 ? "s0" : i == 1 ? "s1" : "s2");
+      if (!needs(4 + i) || !ref.defined()) continue;
+      if (ref.device().is_cpu()) {
+        if (!host.defined()) host = gsc.to(at::kCPU);
+        out[4 + i] = host[i].to(ref.scalar_type()).reshape(ref.sizes());
+      } else {
+        out[4 + i] = gsc[i].to(ref.scalar_type()).reshape(ref.sizes());
+      }
+    }
+    if (needs(7)) {  // the link's gradient, marked with the event after its kernels
+      mark_ready(gsc, st);
+      out[7] = gsc;
+    }
+    return once(grads, out);
+  }
+};
+
+Tensor blend(const Tensor& dists, const Tensor& zbuf, const Tensor& colors, Opt vert_colors, Opt sigma, Opt gamma,
+             Opt alpha, Opt link, const Tensor& p2f, Opt faces, Opt counts, const Tensor& znear, const Tensor& zfar,
+             Opt noise_r, Opt noise_a, Opt seeds, int64_t params, bool cache_on, bool sync_on) {
+  return BlendFn::apply(dists, zbuf, colors, vert_colors, sigma, gamma, alpha, link, p2f, faces, counts, znear, zfar,
+                        noise_r, noise_a, seeds, params, cache_on, sync_on, at::GradMode::is_enabled());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "C++ autograd layer over libpertrender's C ABI (eager step host path)";
+  m.attr("ABI_VERSION") = PR_ABI_VERSION;
+  m.attr("PARAMS_BYTES") = static_cast<int64_t>(sizeof(PRBlendParams));
+  m.def("bind", &bind, "entry-point addresses {name: address} of the loaded libpertrender");
+  m.def("so3_exp", &so3_exp);
+  m.def("rotate", &rotate);
+  m.def("project_rasterize", &project_rasterize);
+  m.def("blend", &blend);
+  m.def("scalar_link", &scalar_link);
+}

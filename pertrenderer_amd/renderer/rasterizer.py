@@ -14,6 +14,7 @@ from typing import NamedTuple, Optional
 import torch
 
 from .. import _native as nat
+from .. import host_layer
 from .. import timing as _timing
 from .mesh import gather_faces
 from .project import project_faces
@@ -312,12 +313,20 @@ class MeshRasterizer(torch.nn.Module):
             nfaces = meshes_world.num_faces_per_mesh()
             H, W = _hw(rs.image_size)
             faces = meshes_world.faces_packed()
-            p2f, zbuf, bary, dists, counts = _ProjectRasterizeFn.apply(
-                meshes_world.verts_packed(), faces, first, nfaces,
-                cameras.world_to_view_matrix(), cameras.projection_matrix(), H, W, int(rs.faces_per_pixel),
-                float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces),
-                bin_params(rs.bin_size, rs.max_faces_per_bin, H, W, faces.shape[0], first.shape[0]),
-                *meshes_world.corner_csr("gather"))
+            bins = bin_params(rs.bin_size, rs.max_faces_per_bin, H, W, faces.shape[0], first.shape[0])
+            ext = host_layer.get()
+            if ext is not None:  # the C++ autograd layer (host_layer.py): same kernels and arguments
+                p2f, zbuf, bary, dists, counts = ext.project_rasterize(
+                    meshes_world.verts_packed(), faces, first, nfaces, cameras.world_to_view_matrix(),
+                    cameras.projection_matrix(), *meshes_world.corner_csr("gather"),
+                    [H, W, int(rs.faces_per_pixel), int(bool(rs.perspective_correct)), int(bool(clip)),
+                     int(bool(rs.cull_backfaces)), bins[0], bins[1]], float(rs.blur_radius))
+            else:
+                p2f, zbuf, bary, dists, counts = _ProjectRasterizeFn.apply(
+                    meshes_world.verts_packed(), faces, first, nfaces,
+                    cameras.world_to_view_matrix(), cameras.projection_matrix(), H, W, int(rs.faces_per_pixel),
+                    float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces),
+                    bins, *meshes_world.corner_csr("gather"))
             return Fragments(pix_to_face=attach_valid_counts(p2f, counts), zbuf=zbuf, bary_coords=bary, dists=dists)
         meshes_screen = self.transform(meshes_world, **kwargs)
         p2f, zbuf, bary, dists = rasterize_meshes(

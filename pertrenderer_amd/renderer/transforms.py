@@ -10,6 +10,7 @@ import math
 import torch
 
 from .. import _native as nat
+from .. import host_layer
 
 F32 = torch.float32
 
@@ -78,7 +79,8 @@ def hat(v):
 
 def so3_exponential_map(log_rot, eps=0.0001):
     if log_rot.is_cuda:
-        return _SO3ExpFn.apply(log_rot, eps)
+        ext = host_layer.get()
+        return ext.so3_exp(log_rot, float(eps)) if ext is not None else _SO3ExpFn.apply(log_rot, eps)
     nrms = (log_rot * log_rot).sum(1)
     angles = torch.clamp(nrms, eps).sqrt()
     inv = 1.0 / angles
@@ -142,7 +144,8 @@ class Rotate:
         pts = points if points.dim() == 3 else points[None]
         R = self.R.to(pts.device)
         if pts.is_cuda and R.shape[0] in (1, pts.shape[0]):
-            out = _RotateFn.apply(pts, R)
+            ext = host_layer.get()
+            out = ext.rotate(pts, R) if ext is not None else _RotateFn.apply(pts, R)
         else:
             out = torch.bmm(pts, R.expand(pts.shape[0], 3, 3))
         return out if points.dim() == 3 else out[0]

@@ -57,9 +57,12 @@ def test_soft_blend_matches_oracle(shape, packed, counts, device):
     # is exactly 0 in real arithmetic (a softmax is shift-invariant): both sides hold only its
     # fp32 rounding residue (~K ulp of the largest term), so that slot's bar is 1e-4 of the max
     assert_close(zz.grad, og["zbuf"], atol_rel=1e-4, name="zbuf")
+    # the smoothing scalars are sums over all N*H*W*K slots of signed terms, reduced by the kernel's
+    # workgroup tree and by the oracle's torch.sum: fp32 summation order alone moves them by ~1e-5
+    # relative on the larger frames (measured 1.4e-5), so their bar is 5e-5
     for k, t in (("sigma", s), ("gamma", gm), ("alpha", al)):
         assert t.grad.device.type == "cpu"
-        assert_close(t.grad, og[k], name=k)
+        assert_close(t.grad, og[k], rtol=5e-5, name=k)
 
 
 def test_soft_blend_device_scalars_and_capture(device):

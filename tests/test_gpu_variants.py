@@ -60,7 +60,9 @@ def test_variant_heaviside_matches_oracle(kind, vr, device):
     oP, odd, ods = bo.rasterize_forward_backward(D, e, torch.tensor(1e-3), gP, kind, vr)
     np.testing.assert_array_equal(P.detach().cpu().numpy(), oP.numpy())
     assert_close(d.grad, odd, name="dists")
-    assert_close(sig.grad, ods, name="sigma")
+    # d sigma sums 7 x 540 signed terms (Cauchy: heavy cancellation) in another order than the
+    # oracle's torch.sum: measured 2.2e-5 relative, bar 5e-5 as for every smoothing-scalar reduction
+    assert_close(sig.grad, ods, rtol=5e-5, name="sigma")
 
 
 @pytest.mark.parametrize("kind,vr", [("cauchy", True), ("gaussian", False)])
