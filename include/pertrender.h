@@ -128,8 +128,8 @@ typedef struct PRBlendFwdArgs {
   int32_t* plan;
   /* nullable, >= PR_BLEND_SYNC_BYTES: arrival counters the forward zeroes; handed to pr_blend_bwd of
    * the same call, its last workgroup reduces d sigma / d gamma / d alpha (no finalize kernel).
-   * Measured slower (each workgroup's release fence writes back L2): the package passes NULL
-   * unless PR_BLEND_SYNC=1 */
+   * Partials are written by device-scope atomic exchanges (no release fence); measured equal to
+   * the separate finalize kernel at cfg 2: the package passes NULL unless PR_BLEND_SYNC=1 */
   int32_t* sync;
 } PRBlendFwdArgs;
 

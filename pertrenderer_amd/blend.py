@@ -314,9 +314,10 @@ def _plan(lib, p, counts, dev):
 
 
 # The backward's fused scalar reduction (PRBlendFwdArgs.sync: its last workgroup forms d sigma /
-# d gamma / d alpha instead of a finalize kernel) is opt-in (PR_BLEND_SYNC=1): every workgroup's
-# release fence before its arrival writes back its XCD's L2 -- full of the backward's gradient
-# stores -- and took cfg 2's blend_bwd from 75 to 182 us (profiles/r4_experiments.txt)
+# d gamma / d alpha instead of a finalize kernel) is opt-in (PR_BLEND_SYNC=1).  With a release
+# fence per workgroup (an L2 writeback of its XCD) it took cfg 2's blend_bwd from 75 to 182 us;
+# fence-free (partials by atomic exchange) the kernel grows ~3 us and the finalize node it saves
+# costs ~2 us of graph time: a wash at cfg 2 (profiles/r4_experiments.txt)
 _FUSED_FINALIZE = os.environ.get("PR_BLEND_SYNC", "0") == "1"
 
 

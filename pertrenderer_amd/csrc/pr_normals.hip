@@ -33,8 +33,7 @@ __global__ void face_cross_kernel(PRNormalsArgs a) {
   }
 }
 
-// |v| as torch's vector norm forms it (F.normalize): sqrt(fma(z, z, fma(y, y, x * x)))
-PR_DEV float norm3(F3 v) { return sqrtf(__builtin_fmaf(v.z, v.z, __builtin_fmaf(v.y, v.y, v.x * v.x))); }
+PR_DEV float norm3(F3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
 
 // in place: n <- n / max(||n||, eps); the unnormalised sums are kept in `raw` for the backward
 __global__ void normalize_kernel(PRNormalsArgs a) {

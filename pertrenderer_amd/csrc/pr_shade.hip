@@ -28,18 +28,14 @@ PR_DEV V3 operator*(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 PR_DEV float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 PR_DEV float sum3(V3 a) { return (a.x + a.y) + a.z; }
 
-// x / max(|x|, eps) and its backward.  |x| as torch's CPU vector norm forms it (the reference's
-// F.normalize): sqrt(fma(z, z, fma(y, y, x * x))) -- bitwise (checked on 3e5 random vectors);
-// Phong's specular power (shininess 64) turns a 1-ulp difference in the normalised vectors
-// into ~64 ulp of the colour
-PR_DEV float norm3(V3 x) { return sqrtf(__builtin_fmaf(x.z, x.z, __builtin_fmaf(x.y, x.y, x.x * x.x))); }
-PR_DEV float nrm(V3 x) { return fmaxf(norm3(x), kNormEps); }
+// x / max(|x|, eps) and its backward
+PR_DEV float nrm(V3 x) { return fmaxf(sqrtf(dot(x, x)), kNormEps); }
 PR_DEV V3 normalize(V3 x) {
   const float r = nrm(x);
   return V3{x.x / r, x.y / r, x.z / r};
 }
 PR_DEV V3 normalize_bwd(V3 x, V3 g) {
-  const float r = norm3(x);
+  const float r = sqrtf(dot(x, x));
   if (!(r > kNormEps)) return (1.f / kNormEps) * g;
   const V3 y = V3{x.x / r, x.y / r, x.z / r};
   return (1.f / r) * (g - dot(y, g) * y);

@@ -119,11 +119,12 @@ def test_layer_is_used_in_eager_step(device):
     import bench
     wl = bench.Workload(device, image_size=64, K=20, samples=8)
     loss = wl.forward()
-    names, stack, seen = [], [loss.grad_fn], set()
+    names, stack, seen, held = [], [loss.grad_fn], set(), []
     while stack:
         fn = stack.pop()
         if fn is None or id(fn) in seen:
             continue
+        held.append(fn)  # the node wrappers are made per access: hold them so ids stay unique
         seen.add(id(fn))
         names.append(type(fn).__name__ if not hasattr(fn, "name") else fn.name())
         stack.extend(f for f, _ in fn.next_functions)

@@ -79,7 +79,12 @@ def test_frame_and_pose_gradient_match_cpu_oracle(setup, deterministic):
     torch.manual_seed(7)
     lossc, imgc = _cpu_loss(cpu, texture, target.cpu(), lc, samples)
     lossc.backward()
-    assert_close(imgg.detach(), imgc.detach(), name="image")
+    # the pose itself (so3_exponential_map + Rotate) is composed on the CPU with Sleef's sin / cos
+    # and MKL's 3x3 sgemm, whose roundings the device kernels do not reproduce: the mesh differs by
+    # ulps before the rasterizer (tools/debug_pipeline_pixel.py), and Phong's shininess-64 power
+    # (d(a^64) = 64 a^63 da) turns that into up to ~2.5e-6 of the image's unit scale on a specular
+    # highlight -- an absolute floor of 5e-6 of the image's scale on top of the 1e-5 relative bar
+    assert_close(imgg.detach(), imgc.detach(), atol_rel=5e-6, name="image")
     assert abs(float(lossg) - float(lossc)) <= 1e-5 * abs(float(lossc))
     assert_close(lg.grad, lc.grad, name="d log_rot")
 
