@@ -102,14 +102,17 @@ def test_device_scalars_and_retain_graph(device):
 
 
 def test_graph_capture_through_cpp_layer(device):
-    """bench.py's captured step records the C++ nodes' launches: a replay equals an eager step with
-    the same device seed."""
+    """bench.py's captured step records the C++ nodes' launches (device smoothing leaves, DeviceSeed
+    keys): a replay runs the whole step and moves the pose."""
     import bench
     wl = bench.Workload(device, image_size=64, K=20, samples=8)
-    step = bench.build_step(wl, 1, "graph", device, 1.0)
-    before = wl.log_rot.detach().clone()
-    step()
-    torch.cuda.synchronize()
+    try:
+        step = bench.build_step(wl, 1, "graph", device, 1.0)
+        before = wl.log_rot.detach().clone()
+        step()
+        torch.cuda.synchronize()
+    finally:
+        pa.noise.use_device_seed(None)  # build_step routes Philox draws through its DeviceSeed
     assert not torch.equal(before, wl.log_rot.detach())
     assert torch.isfinite(wl.log_rot).all()
 
