@@ -52,6 +52,11 @@ struct Api {
   decltype(&pr_blend_plan_size) blend_plan_size = nullptr;
   decltype(&pr_blend_bwd_workspace_size) blend_bwd_workspace_size = nullptr;
   decltype(&pr_blend_bwd) blend_bwd = nullptr;
+  decltype(&pr_shade_fwd) shade_fwd = nullptr;
+  decltype(&pr_shade_bwd_workspace_size) shade_bwd_workspace_size = nullptr;
+  decltype(&pr_shade_bwd) shade_bwd = nullptr;
+  decltype(&pr_vert_normals_fwd) vert_normals_fwd = nullptr;
+  decltype(&pr_vert_normals_bwd) vert_normals_bwd = nullptr;
 };
 Api g_api;
 bool g_bound = false;
@@ -80,6 +85,11 @@ void bind(const std::unordered_map<std::string, int64_t>& addrs) {
   bind_one(addrs, "pr_blend_plan_size", a.blend_plan_size);
   bind_one(addrs, "pr_blend_bwd_workspace_size", a.blend_bwd_workspace_size);
   bind_one(addrs, "pr_blend_bwd", a.blend_bwd);
+  bind_one(addrs, "pr_shade_fwd", a.shade_fwd);
+  bind_one(addrs, "pr_shade_bwd_workspace_size", a.shade_bwd_workspace_size);
+  bind_one(addrs, "pr_shade_bwd", a.shade_bwd);
+  bind_one(addrs, "pr_vert_normals_fwd", a.vert_normals_fwd);
+  bind_one(addrs, "pr_vert_normals_bwd", a.vert_normals_bwd);
   if (a.abi_version() != PR_ABI_VERSION)
     throw std::runtime_error("pr_torch: built for ABI " + std::to_string(PR_ABI_VERSION) + ", library has " +
                              std::to_string(a.abi_version()));
@@ -674,6 +684,174 @@ Tensor blend(const Tensor& dists, const Tensor& zbuf, const Tensor& colors, Opt 
                         noise_r, noise_a, seeds, params, cache_on, sync_on, at::GradMode::is_enabled());
 }
 
+// ------------------------------------------------------------------ Phong shading, vertex normals
+// renderer/shading.py _ShadeFn (pr_shade_fwd / pr_shade_bwd) and renderer/mesh.py _VertNormalsFn
+// (pr_vert_normals_fwd / pr_vert_normals_bwd): eval.py's RandomPhongShader path
+void shade_common(PRShadeArgs& a, const Tensor& p2f, const Tensor& counts, const Tensor& faces, const Tensor& face_uvs,
+                  const Tensor* t /* bary verts normals tex light camera */, const Tensor* rows, int64_t mode,
+                  bool directional) {
+  a.N = static_cast<int32_t>(p2f.size(0));
+  a.H = static_cast<int32_t>(p2f.size(1));
+  a.W = static_cast<int32_t>(p2f.size(2));
+  a.K = static_cast<int32_t>(p2f.size(3));
+  a.pix_to_face = ptr<int64_t>(p2f);
+  a.pix_count = ptr<int32_t>(counts);
+  a.faces = ptr<int64_t>(faces);
+  a.bary = ptr<float>(t[0]);
+  a.verts = ptr<float>(t[1]);
+  a.normals = ptr<float>(t[2]);
+  a.V = t[1].size(0);
+  a.F = faces.size(0);
+  a.texture = static_cast<int32_t>(mode);
+  if (mode == PR_TEX_GIVEN) {
+    a.texels = ptr<float>(t[3]);
+  } else if (mode == PR_TEX_VERTEX) {
+    a.vert_colors = ptr<float>(t[3]);
+  } else {
+    a.maps = ptr<float>(t[3]);
+    a.face_uvs = ptr<float>(face_uvs);
+    a.Hm = static_cast<int32_t>(t[3].size(1));
+    a.Wm = static_cast<int32_t>(t[3].size(2));
+  }
+  a.directional = directional ? 1 : 0;
+  a.light = ptr<float>(t[4]);
+  a.camera = ptr<float>(t[5]);
+  a.ambient = ptr<float>(rows[0]);
+  a.diffuse_color = ptr<float>(rows[1]);
+  a.specular_color = ptr<float>(rows[2]);
+  a.mat_diffuse = ptr<float>(rows[3]);
+  a.mat_specular = ptr<float>(rows[4]);
+  a.shininess = ptr<float>(rows[5]);
+}
+
+const char* kShadeKeys[6] = {"bary", "verts", "normals", "tex", "light", "camera"};
+const char* kShadeRows[6] = {"ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular", "shininess"};
+
+struct ShadeFn : public torch::autograd::Function<ShadeFn> {
+  static Tensor forward(AutogradContext* ctx, Tensor bary, Tensor verts, Tensor normals, Tensor tex, Tensor light,
+                        Tensor camera, Tensor p2f, Opt counts_o, Tensor faces, Opt face_uvs_o, std::vector<Tensor> rows,
+                        int64_t mode, bool directional) {
+    const Tensor counts = val(counts_o), face_uvs = val(face_uvs_o);
+    if (rows.size() != 6) throw std::invalid_argument("shade: 6 parameter rows expected");
+    on_device({&bary, &verts, &normals, &tex, &light, &camera, &p2f, &counts, &faces, &face_uvs});
+    for (const auto& r : rows) on_device({&r});
+    Tensor t[6] = {dense(bary, at::kFloat), dense(verts, at::kFloat), dense(normals, at::kFloat),
+                   dense(tex, at::kFloat),  dense(light, at::kFloat), dense(camera, at::kFloat)};
+    auto p2f_c = dense(p2f, at::kLong);
+    auto colors = at::empty({p2f_c.size(0), p2f_c.size(1), p2f_c.size(2), p2f_c.size(3), 3},
+                            t[0].options().dtype(at::kFloat));
+    PRShadeArgs a{};
+    shade_common(a, p2f_c, counts, faces, face_uvs, t, rows.data(), mode, directional);
+    a.colors = ptr<float>(colors);
+    at::DeviceGuard dg(colors.device());
+    check(api().shade_fwd(&a, stream_of(colors)), "pr_shade_fwd");
+    for (int i = 0; i < 6; ++i) keep(ctx, kShadeKeys[i], t[i]);
+    for (int i = 0; i < 6; ++i) keep(ctx, kShadeRows[i], rows[i]);
+    keep(ctx, "p2f", p2f_c);
+    keep(ctx, "counts", counts);
+    keep(ctx, "faces", faces);
+    keep(ctx, "face_uvs", face_uvs);
+    ctx->saved_data["mode"] = mode;
+    ctx->saved_data["directional"] = directional;
+    return colors;
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    variable_list out(13);
+    if (!grads[0].defined()) return out;
+    Tensor t[6], rows[6];
+    for (int i = 0; i < 6; ++i) t[i] = saved(ctx, kShadeKeys[i]);
+    for (int i = 0; i < 6; ++i) rows[i] = saved(ctx, kShadeRows[i]);
+    const int64_t mode = ctx->saved_data["mode"].toInt();
+    auto g = dense(grads[0], at::kFloat);
+    PRShadeArgs a{};
+    shade_common(a, saved(ctx, "p2f"), saved(ctx, "counts"), saved(ctx, "faces"), saved(ctx, "face_uvs"), t, rows,
+                 mode, ctx->saved_data["directional"].toBool());
+    a.grad_colors = ptr<float>(g);
+    for (int i = 0; i < 6; ++i) out[i] = ctx->needs_input_grad(i) ? at::empty_like(t[i]) : Tensor();
+    a.grad_bary = ptr<float>(out[0]);
+    a.grad_verts = ptr<float>(out[1]);
+    a.grad_normals = ptr<float>(out[2]);
+    if (mode == PR_TEX_GIVEN) a.grad_texels = ptr<float>(out[3]);
+    else if (mode == PR_TEX_VERTEX) a.grad_vert_colors = ptr<float>(out[3]);
+    else a.grad_maps = ptr<float>(out[3]);
+    a.grad_light = ptr<float>(out[4]);
+    a.grad_camera = ptr<float>(out[5]);
+    at::DeviceGuard dg(g.device());
+    Tensor ws;
+    if (at::globalContext().deterministicAlgorithms()) {  // in-order sums, no float atomics
+      a.flags = PR_DETERMINISTIC;
+      ws = workspace(api().shade_bwd_workspace_size(&a), g);
+      a.workspace = ws.data_ptr();
+      a.workspace_bytes = static_cast<size_t>(ws.numel());
+    }
+    check(api().shade_bwd(&a, stream_of(g)), "pr_shade_bwd");
+    return once(grads, out);
+  }
+};
+
+Tensor shade(const Tensor& bary, const Tensor& verts, const Tensor& normals, const Tensor& tex, const Tensor& light,
+             const Tensor& camera, const Tensor& p2f, Opt counts, const Tensor& faces, Opt face_uvs,
+             std::vector<Tensor> rows, int64_t mode, bool directional) {
+  return ShadeFn::apply(bary, verts, normals, tex, light, camera, p2f, counts, faces, face_uvs, rows, mode,
+                        directional);
+}
+
+struct VertNormalsFn : public torch::autograd::Function<VertNormalsFn> {
+  static Tensor forward(AutogradContext* ctx, Tensor verts, Tensor faces, Opt csr_start_o, Opt csr_corners_o) {
+    const Tensor cs = val(csr_start_o), cc = val(csr_corners_o);
+    on_device({&verts, &faces, &cs, &cc});
+    auto v = verts.contiguous();
+    auto f = dense(faces, at::kLong);
+    auto n = at::empty_like(v), raw = at::empty_like(v);
+    PRNormalsArgs a{};
+    a.verts = ptr<float>(v);
+    a.faces = ptr<int64_t>(f);
+    a.V = v.size(0);
+    a.F = f.size(0);
+    a.normals = ptr<float>(n);
+    a.raw = ptr<float>(raw);
+    a.vert_corner_start = ptr<int64_t>(cs);
+    a.vert_corners = ptr<int64_t>(cc);
+    at::DeviceGuard dg(v.device());
+    check(api().vert_normals_fwd(&a, stream_of(v)), "pr_vert_normals_fwd");
+    keep(ctx, "v", v);
+    keep(ctx, "f", f);
+    keep(ctx, "raw", raw);
+    keep(ctx, "cs", cs);
+    keep(ctx, "cc", cc);
+    return n;
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    variable_list out(4);
+    if (!grads[0].defined()) return out;
+    auto v = saved(ctx, "v"), f = saved(ctx, "f"), raw = saved(ctx, "raw");
+    auto cs = saved(ctx, "cs"), cc = saved(ctx, "cc");
+    auto g = dense(grads[0], at::kFloat);
+    auto graw = at::empty_like(v), gv = at::empty_like(v);
+    PRNormalsArgs a{};
+    a.verts = ptr<float>(v);
+    a.faces = ptr<int64_t>(f);
+    a.V = v.size(0);
+    a.F = f.size(0);
+    a.raw = ptr<float>(raw);
+    a.grad_normals = ptr<float>(g);
+    a.grad_raw = ptr<float>(graw);
+    a.grad_verts = ptr<float>(gv);
+    a.vert_corner_start = ptr<int64_t>(cs);
+    a.vert_corners = ptr<int64_t>(cc);
+    at::DeviceGuard dg(g.device());
+    check(api().vert_normals_bwd(&a, stream_of(g)), "pr_vert_normals_bwd");
+    out[0] = gv;
+    return once(grads, out);
+  }
+};
+
+Tensor vert_normals(const Tensor& verts, const Tensor& faces, Opt csr_start, Opt csr_corners) {
+  return VertNormalsFn::apply(verts, faces, csr_start, csr_corners);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -686,4 +864,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("project_rasterize", &project_rasterize);
   m.def("blend", &blend);
   m.def("scalar_link", &scalar_link);
+  m.def("shade", &shade);
+  m.def("vert_normals", &vert_normals);
 }

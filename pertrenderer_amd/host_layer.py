@@ -1,6 +1,6 @@
 """The C++ autograd layer (csrc/pr_torch.cpp -> _pr_torch*.so) for the eager step.
 
-The pose, rasterizer, fused-blend and smoothing-scalar-link nodes of an eager step
+The pose, rasterizer, fused-blend, smoothing-scalar-link, Phong-shading and vertex-normal nodes of an eager step
 (experiments/eval.py:343-376) run as torch C++ autograd Functions that fill the C-ABI structs and
 launch through the loaded libpertrender's entry points: no ctypes packing, no Python
 ``Function.apply`` per op.  Same kernels, same arguments, same results as
@@ -27,7 +27,8 @@ _ERROR = None
 _ENTRIES = ("pr_abi_version", "pr_last_error", "pr_so3_exp_fwd", "pr_so3_exp_bwd", "pr_rotate_fwd",
             "pr_rotate_bwd", "pr_project_rast_fwd", "pr_project_bwd", "pr_rast_fwd_workspace_size",
             "pr_rast_bwd_workspace_size", "pr_rast_bwd", "pr_blend_fwd", "pr_blend_plan_size",
-            "pr_blend_bwd_workspace_size", "pr_blend_bwd")
+            "pr_blend_bwd_workspace_size", "pr_blend_bwd", "pr_shade_fwd", "pr_shade_bwd_workspace_size", "pr_shade_bwd",
+            "pr_vert_normals_fwd", "pr_vert_normals_bwd")
 
 
 def _path():

@@ -189,6 +189,10 @@ class Meshes:
         v = self.verts_packed()
         f = self.faces_packed()
         if NATIVE_NORMALS and v.is_cuda and v.dtype == torch.float32:
+            from .. import host_layer
+            ext = host_layer.get()
+            if ext is not None:  # the C++ autograd layer (host_layer.py): same kernels
+                return ext.vert_normals(v, f, *self._topo.corner_csr("normals"))
             return _VertNormalsFn.apply(v, f, *self._topo.corner_csr("normals"))
         fv = gather_faces(v, f)
         n = torch.zeros_like(v)

@@ -11,10 +11,13 @@ check_differentiability flows).  ``phong_shading_reference`` is the torch compos
 formulas (PyTorch3D's op order); it serves inputs the kernel does not cover (gradients w.r.t. the
 light / material colours) and is the tests' reference.
 """
+import collections
+
 import torch
 import torch.nn.functional as Fn
 
 from .. import _native as nat
+from .. import host_layer
 from .interp import interpolate_vertex_attributes
 from .mesh import TexturesVertex
 
@@ -155,6 +158,33 @@ def _rows(t, N, device):
     return t
 
 
+_ROW_CACHE = collections.OrderedDict()
+_ROW_CACHE_MAX = 32
+
+
+def _param_rows(lights, materials, N, dev):
+    """The six per-batch material / light colour rows of the shading kernel, made once per
+    (source tensors and their versions, N, device): an eager step then launches no product / copy
+    kernels for constant materials.  The sources (no gradient: _native_ok) are held by the entry,
+    so their ids are not reused while it lives; an in-place change bumps a version and misses."""
+    srcs = (materials.ambient_color, lights.ambient_color, lights.diffuse_color, lights.specular_color,
+            materials.diffuse_color, materials.specular_color, materials.shininess)
+    key = tuple((id(t), t._version) if torch.is_tensor(t) else ("v", float(t)) for t in srcs) + (N, str(dev))
+    hit = _ROW_CACHE.get(key)
+    if hit is not None:
+        _ROW_CACHE.move_to_end(key)
+        return hit[0]
+    rows = lambda x: _rows(x, N, dev).contiguous()
+    out = dict(ambient=rows(materials.ambient_color * lights.ambient_color),
+               diffuse_color=rows(lights.diffuse_color), specular_color=rows(lights.specular_color),
+               mat_diffuse=rows(materials.diffuse_color), mat_specular=rows(materials.specular_color),
+               shininess=rows(materials.shininess.reshape(-1, 1)).reshape(N).contiguous())
+    _ROW_CACHE[key] = (out, srcs)
+    while len(_ROW_CACHE) > _ROW_CACHE_MAX:
+        _ROW_CACHE.popitem(last=False)
+    return out
+
+
 def _native_ok(fragments, lights, materials):
     if not fragments.pix_to_face.is_cuda:
         return False
@@ -173,15 +203,16 @@ def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face
         counts = None
     verts = meshes.verts_packed()
     faces = meshes.faces_packed().to(torch.int64).contiguous()
-    rows = lambda x: _rows(x, N, dev).contiguous()
     cfg = dict(p2f=nat.dense(p2f, torch.int64), counts=counts, faces=faces, mode=mode,
-               face_uvs=face_uvs, directional=_is_directional(lights),
-               ambient=rows(materials.ambient_color * lights.ambient_color),
-               diffuse_color=rows(lights.diffuse_color), specular_color=rows(lights.specular_color),
-               mat_diffuse=rows(materials.diffuse_color), mat_specular=rows(materials.specular_color),
-               shininess=rows(materials.shininess.reshape(-1, 1)).reshape(N).contiguous())
+               face_uvs=face_uvs, directional=_is_directional(lights), **_param_rows(lights, materials, N, dev))
     light = _rows(lights.location, N, dev)
     camera = _rows(cameras.get_camera_center(), N, dev)
+    ext = host_layer.get()
+    if ext is not None:  # the C++ autograd layer (host_layer.py): same kernel, same arguments
+        return ext.shade(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg["p2f"],
+                         counts, faces, face_uvs,
+                         [cfg[k] for k in ("ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular",
+                                           "shininess")], int(mode), bool(cfg["directional"]))
     return _ShadeFn.apply(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg)
 
 

@@ -19,10 +19,11 @@ def _cpp_layer():
     assert host_layer.layer() == "c++", host_layer.error()
 
 
-def _step(device, size=96, K=30, seed=3):
+def _step(device, size=96, K=30, seed=3, eval_scene=False):
     import bench
     torch.manual_seed(seed)
-    wl = bench.Workload(device, image_size=size, K=K, samples=8)
+    wl = bench.Workload(device, image_size=size, K=K, samples=8, eval_scene=eval_scene,
+                        rast_samples=16 if eval_scene else None)
     torch.manual_seed(seed + 1)  # the Philox keys of the blend
     loss = wl.forward()
     loss.backward()
@@ -30,13 +31,15 @@ def _step(device, size=96, K=30, seed=3):
     return loss.detach(), wl.log_rot.grad.clone(), [p.grad.clone() for p in wl.params()[1:]]
 
 
-@pytest.mark.parametrize("size,K", [(96, 30), (256, 50)])
-def test_eager_step_matches_python_layer(device, size, K):
-    torch.use_deterministic_algorithms(True)
+@pytest.mark.parametrize("size,K,eval_scene", [(96, 30, False), (256, 50, False), (128, 50, True)])
+def test_eager_step_matches_python_layer(device, size, K, eval_scene):
+    """eval_scene: eval.py's renderer (RandomPhongShader over the TexturesUV cube: the C++ shading
+    and vertex-normal nodes too)."""
+    torch.use_deterministic_algorithms(True, warn_only=True)
     try:
-        a = _step(device, size, K)
+        a = _step(device, size, K, eval_scene=eval_scene)
         with host_layer.disabled():
-            b = _step(device, size, K)
+            b = _step(device, size, K, eval_scene=eval_scene)
     finally:
         torch.use_deterministic_algorithms(False)
     assert torch.equal(a[0], b[0]), "loss"
@@ -134,3 +137,20 @@ def test_layer_is_used_in_eager_step(device):
     assert not any(n.startswith("_") and n.endswith("Backward") for n in names), names
     assert any("BlendFn" in n for n in names), names
     assert any("ProjectRasterizeFn" in n for n in names), names
+
+
+def test_eval_scene_uses_cpp_shading_and_normals(device):
+    import bench
+    wl = bench.Workload(device, image_size=64, K=20, samples=8, eval_scene=True, rast_samples=16)
+    loss = wl.forward()
+    names, stack, seen, held = [], [loss.grad_fn], set(), []
+    while stack:
+        fn = stack.pop()
+        if fn is None or id(fn) in seen:
+            continue
+        held.append(fn)
+        seen.add(id(fn))
+        names.append(fn.name())
+        stack.extend(f for f, _ in fn.next_functions)
+    assert any("ShadeFn" in n for n in names) and any("VertNormalsFn" in n for n in names), names
+    assert not any(n.startswith("_") and n.endswith("Backward") for n in names), names

@@ -156,19 +156,42 @@ def test_native_shading_camera_gradient(device):
     assert float(ga.abs().sum()) > 0
 
 
-def test_renderer_uses_native_shading(device):
-    """RandomPhongShader / HardPhongShader route TexturesUV and TexturesVertex through pr_shade."""
+@pytest.mark.parametrize("layer", ["python", "c++"])
+def test_renderer_uses_native_shading(device, layer):
+    """RandomPhongShader / HardPhongShader route TexturesUV and TexturesVertex through pr_shade, in
+    the Python Functions and in the C++ autograd layer (host_layer.py)."""
     import pertrenderer_amd.renderer.shading as shm
+    from pertrenderer_amd import _native as nat
+    from pertrenderer_amd import host_layer
+    from pertrenderer_amd.renderer import HardPhongShader
+    mesh, frag, lights, cams, mats, *_ = _scene(device, "uv")
     calls = []
+    if layer == "c++":
+        ext = host_layer.get()
+        assert ext is not None, host_layer.error()
+
+        class Counting:
+            def __getattr__(self, name):
+                fn = getattr(ext, name)
+                if name != "shade":
+                    return fn
+                return lambda *a: calls.append(a[-2]) or fn(*a)
+
+        orig_get = host_layer.get
+        try:
+            host_layer.get = lambda: Counting()
+            HardPhongShader(device=device, cameras=cams, lights=lights)(frag, mesh)
+        finally:
+            host_layer.get = orig_get
+        assert calls == [nat.PR_TEX_UV]
+        return
     orig = shm._ShadeFn.apply
     try:
         shm._ShadeFn.apply = lambda *a: calls.append(a[-1]["mode"]) or orig(*a)
-        mesh, frag, lights, cams, mats, *_ = _scene(device, "uv")
-        from pertrenderer_amd.renderer import HardPhongShader
-        HardPhongShader(device=device, cameras=cams, lights=lights)(frag, mesh)
+        with host_layer.disabled():
+            HardPhongShader(device=device, cameras=cams, lights=lights)(frag, mesh)
     finally:
         shm._ShadeFn.apply = orig
-    from pertrenderer_amd import _native as nat
     assert calls == [nat.PR_TEX_UV]
 
 

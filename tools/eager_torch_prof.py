@@ -30,6 +30,23 @@ def main():
             step()
         torch.cuda.synchronize()
         print(f"eager: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/step", flush=True)
+    # host time per phase (no synchronisation inside a step: the backward's includes the wait of
+    # the smoothing scalars' gradient copy for the blend kernels)
+    ph = [0.0, 0.0, 0.0]
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        loss = wl.forward()
+        t1 = time.perf_counter()
+        loss.backward()
+        t2 = time.perf_counter()
+        wl.opt.step()
+        wl.zero_grad()
+        t3 = time.perf_counter()
+        ph[0] += t1 - t0
+        ph[1] += t2 - t1
+        ph[2] += t3 - t2
+    torch.cuda.synchronize()
+    print("host ms/step: forward %.3f  backward %.3f  adam+zero %.3f" % tuple(1e3 * v / steps for v in ph), flush=True)
     with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
         for _ in range(steps):
             step()
