@@ -129,7 +129,8 @@ typedef struct PRBlendFwdArgs {
   /* nullable, >= PR_BLEND_SYNC_BYTES: arrival counters the forward zeroes; handed to pr_blend_bwd of
    * the same call, its last workgroup reduces d sigma / d gamma / d alpha (no finalize kernel).
    * Partials are written by device-scope atomic exchanges (no release fence); measured equal to
-   * the separate finalize kernel at cfg 2: the package passes NULL unless PR_BLEND_SYNC=1 */
+   * the separate finalize kernel at cfg 2 in graph mode, one launch fewer in eager mode: the
+   * package passes it unless PR_BLEND_SYNC=0 */
   int32_t* sync;
 } PRBlendFwdArgs;
 

@@ -314,11 +314,12 @@ def _plan(lib, p, counts, dev):
 
 
 # The backward's fused scalar reduction (PRBlendFwdArgs.sync: its last workgroup forms d sigma /
-# d gamma / d alpha instead of a finalize kernel) is opt-in (PR_BLEND_SYNC=1).  With a release
-# fence per workgroup (an L2 writeback of its XCD) it took cfg 2's blend_bwd from 75 to 182 us;
-# fence-free (partials by atomic exchange) the kernel grows ~3 us and the finalize node it saves
-# costs ~2 us of graph time: a wash at cfg 2 (profiles/r4_experiments.txt)
-_FUSED_FINALIZE = os.environ.get("PR_BLEND_SYNC", "0") == "1"
+# d gamma / d alpha instead of a finalize kernel; PR_BLEND_SYNC=0 restores the kernel).  With a
+# release fence per workgroup (an L2 writeback of its XCD) it took cfg 2's blend_bwd from 75 to
+# 182 us; fence-free (partials by atomic exchange) the kernel grows ~3 us and the finalize node it
+# saves costs ~2 us of graph time: equal in graph mode, one launch fewer per eager backward
+# (profiles/r4_experiments.txt).  Bitwise equal either way (tests/test_gpu_fused_finalize.py).
+_FUSED_FINALIZE = os.environ.get("PR_BLEND_SYNC", "1") == "1"
 
 
 def _sync(dev):

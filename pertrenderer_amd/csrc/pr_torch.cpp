@@ -15,6 +15,7 @@
 // libpertrender.so it loaded (bind()), so both layers drive the one library instance.
 #include <torch/extension.h>
 #include <torch/csrc/autograd/functions/basic_ops.h>
+#include <torch/csrc/autograd/functions/utils.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 
@@ -266,35 +267,35 @@ ScalarMeta meta_of(const Tensor& t) {
   return m;
 }
 
-struct ScalarLinkFn : public torch::autograd::Function<ScalarLinkFn> {
-  static Tensor forward(AutogradContext* ctx, Opt sigma, Opt gamma, Opt alpha, int64_t device) {
-    const Tensor ts[3] = {val(sigma), val(gamma), val(alpha)};
-    for (int i = 0; i < 3; ++i) {
-      auto m = meta_of(ts[i]);
-      ctx->saved_data[std::string("m") + char('0' + i)] =
-          m.defined ? c10::IValue(std::make_tuple(static_cast<int64_t>(m.dtype), m.shape)) : c10::IValue();
-    }
-    return at::empty({3}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device));
-  }
-
-  static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    variable_list out(4);
-    if (!grads[0].defined()) return out;
+// The link is a raw autograd Node with sequence number 0: the engine runs ready nodes in
+// decreasing sequence order, so once the rasterizer's backward is launched it takes the pose
+// backward (Rotate, so3, d log_rot) before the link, and the link's wait for the blend kernels
+// overlaps those launches (a Function node made in the renderer would outrank them).
+struct ScalarLinkNode : public torch::autograd::Node {
+  ScalarMeta meta[3];
+  explicit ScalarLinkNode(torch::autograd::edge_list&& next) : Node(/*sequence_nr=*/0, std::move(next)) {}
+  std::string name() const override { return "ScalarLinkBackward"; }
+  variable_list apply(variable_list&& grads) override {
+    variable_list out(3);
+    if (grads.empty() || !grads[0].defined()) return out;
     auto host = host_copy(grads[0]);
-    for (int i = 0; i < 3; ++i) {
-      auto v = ctx->saved_data[std::string("m") + char('0' + i)];
-      if (v.isNone()) continue;
-      auto tup = v.toTuple();
-      auto dt = static_cast<at::ScalarType>(tup->elements()[0].toInt());
-      auto shape = tup->elements()[1].toIntVector();
-      out[i] = host[i].to(dt).reshape(shape);
-    }
+    for (int i = 0; i < 3; ++i)
+      if (meta[i].defined && should_compute_output(i)) out[i] = host[i].to(meta[i].dtype).reshape(meta[i].shape);
     return out;
   }
 };
 
 Tensor scalar_link(Opt sigma, Opt gamma, Opt alpha, int64_t device) {
-  return ScalarLinkFn::apply(sigma, gamma, alpha, device);
+  auto out = at::empty({3}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device));
+  const Tensor ts[3] = {val(sigma), val(gamma), val(alpha)};
+  bool any = false;
+  for (const auto& t : ts) any = any || (t.defined() && t.requires_grad());
+  if (!at::GradMode::is_enabled() || !any) return out;
+  auto node = std::shared_ptr<ScalarLinkNode>(
+      new ScalarLinkNode(torch::autograd::collect_next_edges(ts[0], ts[1], ts[2])), torch::autograd::deleteNode);
+  for (int i = 0; i < 3; ++i) node->meta[i] = meta_of(ts[i]);
+  torch::autograd::set_history(out, node);
+  return out;
 }
 
 // ------------------------------------------------------------------ pose: so3 exp, rotate
