@@ -528,9 +528,12 @@ def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, s
         raise ValueError("dists / zbuf must match pix_to_face's shape")
     vflags = variant_flags(rast_kind, rast_vr, agg_kind, agg_vr)
     if noise is None:
-        nr = noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device, rast_kind)
-        na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind)
-        noise = _merge(nr, na)
+        pair = noise_mod.draw_pair(shape, nb_samples_rast, nb_samples_agg, pix_to_face.device, fixed_noise, rast_kind,
+                                   agg_kind)
+        if pair is None:
+            pair = (noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device, rast_kind),
+                    noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind))
+        noise = _merge(*pair)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
@@ -555,9 +558,12 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
         raise ValueError("dists / zbuf must match pix_to_face's shape")
     vflags = variant_flags(rast_kind, rast_vr, agg_kind, agg_vr)
     if noise is None:
-        nr = noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device, rast_kind)
-        na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind)
-        noise = _merge(nr, na)
+        pair = noise_mod.draw_pair(shape, nb_samples_rast, nb_samples_agg, pix_to_face.device, fixed_noise, rast_kind,
+                                   agg_kind)
+        if pair is None:
+            pair = (noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device, rast_kind),
+                    noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind))
+        noise = _merge(*pair)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))

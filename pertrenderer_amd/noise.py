@@ -170,3 +170,16 @@ def draw_agg(shape, Sa, device, fixed_noise=False, kind="gaussian"):
     if _DEVICE_SEED is not None and not fixed_noise:
         return Noise.philox(seed_a=_DEVICE_SEED.stream_id(), seeds=_DEVICE_SEED.tensor, offset_a=_offset(Sa, 1))
     return Noise.philox(seed_a=draw_key(), offset_a=_offset(Sa, 1))
+
+
+def draw_pair(shape, Sr, Sa, device, fixed_noise=False, rast_kind="gaussian", agg_kind="gaussian"):
+    """(rast draw, agg draw) of one fused blend call, as draw_rast then draw_agg.  With host-keyed
+    Philox and no fixed_noise both keys come from ONE randint of two values: the CPU generator
+    yields the same two 64-bit draws in the same order as two one-value calls (checked in
+    tests/test_noise_pair.py), for half the host time.  None in the other modes (the caller draws
+    one by one)."""
+    if _SOURCE != "philox" or _DEVICE_SEED is not None or fixed_noise:
+        return None
+    k = torch.randint(0, 2 ** 62, (2,), dtype=torch.int64).tolist()
+    return (Noise.philox(seed_r=k[0], offset_r=_offset(Sr, 0)), Noise.philox(seed_a=k[1], offset_a=_offset(Sa, 1)))
+
