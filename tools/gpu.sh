@@ -98,7 +98,8 @@ case "$CMD" in
     HIP_LAUNCH_BLOCKING=1 bench "eager_blocking_$T" --mode eager --no-cpu-baseline --no-dense || exit 1
     timeout -k 10 60 python tools/launch_blocking_check.py > "$OUT/launch_blocking_$T.txt" 2>&1 &&
       CUDA_LAUNCH_BLOCKING=1 timeout -k 10 60 python tools/launch_blocking_check.py >> "$OUT/launch_blocking_$T.txt" 2>&1 &&
-      HIP_LAUNCH_BLOCKING=1 timeout -k 10 60 python tools/launch_blocking_check.py >> "$OUT/launch_blocking_$T.txt" 2>&1 || exit 1
+      HIP_LAUNCH_BLOCKING=1 timeout -k 10 60 python tools/launch_blocking_check.py >> "$OUT/launch_blocking_$T.txt" 2>&1 &&
+      timeout -k 10 60 python tools/launch_blocking_check.py --eval-order >> "$OUT/launch_blocking_$T.txt" 2>&1 || exit 1
     for c in eval cfg3 cfg4; do bench "${c}_$T" --config $c --no-cpu-baseline || exit 1; done
     bench "eager_eval_$T" --config eval --mode eager --no-cpu-baseline --no-dense || exit 1
     # BASELINE cfg5: eval.py's pose benchmark, 100 problems x 800 iterations x {softras, gaussian}
