@@ -242,7 +242,7 @@ def prelink(vals, device):
     if not _linkable(vals, device):
         return None
     key = _key(vals, device)
-    _state()["pre"] = (key, _new_link(device, vals))
+    _state()["pre"] = (key, _new_link(device, vals), _floats(vals))
     return key
 
 
@@ -263,19 +263,23 @@ def prelink_shader(shader, meshes):
     return prelink((sr.sigma, sa.gamma, sa.alpha), torch.device(device)) if device is not None else None
 
 
+def _floats(vals):
+    return tuple(float(v.detach()) if torch.is_tensor(v) else float(v) for v in vals)
+
+
 def _link_scalars(vals, device):
     """(values, link): with a link, the scalars go to the kernel as host floats and their gradients
-    through the link; otherwise the tensors themselves (the blend copies their gradients)."""
+    through the link; otherwise the tensors themselves (the blend copies their gradients).  The
+    renderer's prelink of the same scalars (same ids and versions: checked linkable when it was
+    made, in this forward) is taken with the host values it read."""
+    st = _state()
+    pre = st.get("pre")
+    if pre is not None and pre[0] == _key(vals, device):
+        del st["pre"]
+        return pre[2], pre[1]
     if not _linkable(vals, device):
         return vals, None
-    st = _state()
-    key, pre = _key(vals, device), st.get("pre")
-    if pre is not None and pre[0] == key:
-        del st["pre"]
-        link = pre[1]
-    else:
-        link = _new_link(device, vals)
-    return tuple(float(v.detach()) if torch.is_tensor(v) else float(v) for v in vals), link
+    return _floats(vals), _new_link(device, vals)
 
 
 def _link_grad(gsc, need):

@@ -381,6 +381,10 @@ Tensor rotate(const Tensor& points, const Tensor& R) { return RotateFn::apply(po
 // renderer/rasterizer.py _ProjectRasterizeFn: pr_project_rast_fwd, backward pr_rast_bwd then
 // pr_project_bwd into d verts (accumulators zeroed by the forward kernel)
 Tensor per_mesh(const Tensor& m, int64_t N, const char* name) {
+  // the cameras' cached (N,4,4) float matrices: used as they are (no alias, no copy)
+  if (m.scalar_type() == at::kFloat && m.dim() == 3 && m.size(0) == N && m.size(1) == 4 && m.size(2) == 4 &&
+      m.is_contiguous())
+    return m;
   auto f = m.detach().to(at::kFloat);
   if (f.dim() != 3 || f.size(1) != 4 || f.size(2) != 4 || (f.size(0) != 1 && f.size(0) != N))
     throw std::invalid_argument(std::string(name) + " matrices must be (1,4,4) or (N,4,4)");
