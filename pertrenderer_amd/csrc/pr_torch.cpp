@@ -206,6 +206,10 @@ void mark_ready(const Tensor& buf, void* stream) {
   std::lock_guard<std::mutex> lk(r.mu);
   auto old = r.pending.find(buf.data_ptr());
   if (old != r.pending.end()) r.free[old->second.first].push_back(old->second.second);
+  if (r.pending.size() > 256) {  // links whose backward never ran (grad taken w.r.t. other inputs): recycle
+    for (auto& kv : r.pending) r.free[kv.second.first].push_back(kv.second.second);
+    r.pending.clear();
+  }
   r.pending[buf.data_ptr()] = {dev, e};
 }
 
