@@ -317,13 +317,25 @@ PR_DEV bool face_test(const FaceRec& r, V2 p, float blur, float& pz) {
 // with certainty, then the exact face_test for the survivors.
 //  * inside: b_i = e_i / area > 0  <=>  e_i != 0 and sign(e_i) == sign(area) (area != 0 for
 //    every uncull'd face).  So "not inside by signs" implies "not inside" exactly.
-//  * edge distance with t = dot * rcp(l2) instead of dot / l2: the squared distance differs
-//    from the exact one by a few ulp of its terms (it is stationary in t at interior
-//    optima, continuous at the clamps); 1e-3 relative is a wide safety band.
+//  * edge distance with t = dot * rcp(l2) instead of dot / l2: the two squared distances differ
+//    by at most the face's margin m = 4 sqrt(blur) delta + 2 delta^2 + blur 2^-20, where
+//    delta = 2^-19 U bounds the difference of the computed dx (and dy) and U is the largest
+//    coordinate magnitude of the face's corners and the tile's pixels (t differs by <= 2^-22;
+//    t * (b - a), a + t (b - a) and p - q round at <= 2^-24 of magnitudes <= 2U; where the exact
+//    distance is below blur, |dx| and |dy| are below sqrt(blur)).  dist_margin computes m per
+//    staged face: proportional to blur for the usual NDC-sized faces, unbounded for faces with
+//    huge corners (partly behind the camera), which then always take the exact test.  (A fixed
+//    band of 1e-3 blur, rounds 1-4, was too narrow for such faces: tests/test_gpu_rast.py
+//    test_rasterizer_forward_division_fallbacks_bitwise.)
 // A lane is rejected only if it is outside its box, or outside the face by signs and
-// farther than blur * (1 + 1e-3).  Everything else runs the exact test, so every decision
-// and every value equals face_test's.
-constexpr float kDistBand = 1e-3f;
+// farther than blur + m.  Everything else runs the exact test, so every decision and every
+// value equals face_test's.
+PR_DEV float dist_margin(float4 ra, float4 rb, float ptile, float sqrt_blur, float blur) {
+  const float m = fmaxf(fmaxf(fmaxf(fabsf(ra.x), fabsf(ra.y)), fmaxf(fabsf(ra.w), fabsf(rb.x))),
+                        fmaxf(fmaxf(fabsf(rb.z), fabsf(rb.w)), ptile));
+  const float delta = m * 0x1p-19f;
+  return 4.f * sqrt_blur * delta + 2.f * delta * delta + blur * 0x1p-20f;
+}
 
 PR_DEV float seg_dist2_fast(V2 p, V2 a, float bax, float bay, float l2, V2 b) {
   const float bx = p.x - b.x, by = p.y - b.y;
@@ -336,7 +348,7 @@ PR_DEV float seg_dist2_fast(V2 p, V2 a, float bax, float bay, float l2, V2 b) {
   return l2 <= kEps ? db : ds;
 }
 
-PR_DEV bool face_maybe(const FaceRec& r, V2 p, float blur, float& dfast) {
+PR_DEV bool face_maybe(const FaceRec& r, V2 p, float blur, float margin, float& dfast) {
   const bool inbox = !(p.x < r.c.y || p.x > r.c.z || p.y < r.c.w || p.y > r.d.x);
   const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
   const float e0 = (p.x - v1.x) * r.e.w - (p.y - v1.y) * r.e.z;
@@ -351,15 +363,15 @@ PR_DEV bool face_maybe(const FaceRec& r, V2 p, float blur, float& dfast) {
   float d = d01 < d02 ? d01 : d02;
   d = d < d12 ? d : d12;
   dfast = d;
-  return inbox && (ins || !(d > blur * (1.f + kDistBand)));
+  return inbox && (ins || !(d > blur + margin));
 }
 
 // The exact test for a lane that face_maybe kept (no perspective correction): barycentrics,
 // clipping, pz and the inside flag with face_test's operations; the exact edge distance
-// only where the fast one is inside the safety band around blur (a branch that is rarely
-// taken by any lane of the wave).
+// only where the fast one is within the face's margin of blur (a branch that is rarely
+// taken by any lane of the wave: below blur - m the exact distance is below blur too).
 template <bool CLIP>
-PR_DEV bool face_test_kept(const FaceRec& r, V2 p, float blur, float dfast, float& pz) {
+PR_DEV bool face_test_kept(const FaceRec& r, V2 p, float blur, float margin, float dfast, float& pz) {
   const V2 v0{r.a.x, r.a.y}, v1{r.a.w, r.b.x}, v2{r.b.z, r.b.w};
   const float z0 = r.a.z, z1 = r.b.y, z2 = r.c.x;
   const float area = r.d.y;
@@ -375,8 +387,8 @@ PR_DEV bool face_test_kept(const FaceRec& r, V2 p, float blur, float dfast, floa
   }
   pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
   const bool inside = b[0] > 0.f && b[1] > 0.f && b[2] > 0.f;
-  bool near = dfast < blur * (1.f - kDistBand);
-  if (!inside && !near && !(dfast > blur * (1.f + kDistBand))) {  // in the band: exact distance
+  bool near = dfast < blur - margin;
+  if (!inside && !near && !(dfast > blur + margin)) {  // in the band: exact distance
     const float d01 = seg_dist2_d(p, v0, r.e.x, r.e.y, r.d.z, v1);
     const float d02 = seg_dist2_d(p, v0, -r.f.x, -r.f.y, r.f.z, v2);
     const float d12 = seg_dist2_d(p, v1, r.e.z, r.e.w, r.d.w, v2);
@@ -514,7 +526,7 @@ PR_DEV bool ekey_less(float2 x, float2 y) { return key_less(x.x, __float_as_int(
 template <int SL>
 size_t rast_fwd_lds_sl(int K) {
   using C = RastCfg<SL>;
-  return C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL + rast_qpad<SL>()) * 8 + (size_t)C::CAP * 12 + 64 * 4 + C::CH * 8 + 16;
+  return C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL + rast_qpad<SL>()) * 8 + (size_t)C::CAP * 12 + 64 * 4 + C::CH * 12 + 16;
 }
 
 size_t rast_fwd_lds(int K, int SL) {
@@ -614,6 +626,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
   int* qsz = lidx + kCap;                                           // [64] queue sizes (per pixel)
   int* lcf = qsz + 64;                                              // [CH] staged chunk face ids
   float* lcs = reinterpret_cast<float*>(lcf + CH);                  // [CH] staged chunk suffix mins
+  float* lmg = lcs + CH;                                            // [CH] staged faces' distance margins
   const int n = blockIdx.z;
   const int H = a.H, W = a.W;
   int tile_x = blockIdx.x, tile_y = blockIdx.y;
@@ -635,6 +648,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
   const float txmax = ndc(W - 1 - col0, W, H), txmin = ndc(W - 1 - c1, W, H);
   const float tymax = ndc(H - 1 - row0, H, W), tymin = ndc(H - 1 - r1, H, W);
   const float tcx = 0.5f * (txmin + txmax), tcy = 0.5f * (tymin + tymax);
+  const float ptile = fmaxf(fmaxf(fabsf(txmin), fabsf(txmax)), fmaxf(fabsf(tymin), fabsf(tymax)));
   const int64_t fb = a.mesh_first_face[n];
   // the faces to cull: the tile's bin list, or the whole mesh (no bins, or the bin overflowed)
   const int* ids = nullptr;
@@ -645,7 +659,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     if (c <= bins.cap) { ids = bins.list + (int64_t)b * bins.cap; fe = c; }
   }
   constexpr bool clip = CLIP;
-  const float blur = a.blur_radius;
+  const float blur = a.blur_radius, sqrt_blur = sqrtf(blur);
   // the pixel's queue state, replicated in its SL lanes
   int qs = 0;
   float qlast_z = __builtin_inff();
@@ -785,6 +799,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
         d.a = nra; d.b = nrb; d.c = nrc; d.d = nrd; d.e = nre; d.f = nrf;
         lcf[lane] = nfid;
         lcs[lane] = nsuf;
+        if constexpr (!PERSP) lmg[lane] = dist_margin(nra, nrb, ptile, sqrt_blur, blur);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -809,13 +824,14 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
           rr[j] = lrec[min(idx[j], cnt - 1)];  // one LDS wait per group
         }
         bool maybe[kGroup];
-        float dfast[kGroup];
+        float dfast[kGroup], mg[kGroup];
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           // the cheap certain-reject stage (non-perspective; the box test otherwise)
           dfast[j] = 0.f;
+          mg[j] = PERSP ? 0.f : lmg[min(idx[j], cnt - 1)];
           if constexpr (PERSP) maybe[j] = ok[j] && in_bbox(rr[j], p);
-          else maybe[j] = ok[j] && face_maybe(rr[j], p, blur, dfast[j]);
+          else maybe[j] = ok[j] && face_maybe(rr[j], p, blur, mg[j], dfast[j]);
           any |= __ballot(maybe[j]) != 0;
         }
         if (!any) continue;
@@ -825,7 +841,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           if constexpr (PERSP) cand[j] = face_test<PERSP, CLIP>(rr[j], p, blur, pzv[j]) && maybe[j];
-          else cand[j] = face_test_kept<CLIP>(rr[j], p, blur, dfast[j], pzv[j]) && maybe[j];
+          else cand[j] = face_test_kept<CLIP>(rr[j], p, blur, mg[j], dfast[j], pzv[j]) && maybe[j];
         }
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {

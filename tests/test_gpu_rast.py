@@ -105,6 +105,43 @@ def test_rasterizer_forward_matches_oracle_bitwise(cfg, bins, device):
     np.testing.assert_array_equal(bary.detach().cpu().numpy(), rb)
 
 
+def _extreme_soup(seed):
+    """Faces with corners on pixel centres (zero edge functions and projections), huge corners (a mesh
+    partly behind the camera projects to such), very long edges and slivers: the forward's fast
+    certain-reject stage must keep every pixel the exact test takes (pr_rast.hip dist_margin)."""
+    rng = np.random.default_rng(seed)
+    c = lambda i: -1.0 + (2 * i + 1) / 32.0  # pixel-centre NDC coordinate of a 32-pixel axis (exact)
+    faces = []
+    for _ in range(24):  # axis-aligned right triangles with corners on pixel centres
+        i, j, w, h = rng.integers(0, 28), rng.integers(0, 28), rng.integers(1, 6), rng.integers(1, 6)
+        faces.append([[c(i), c(j), 1.0], [c(i + w), c(j), 1.5], [c(i), c(j + h), 2.0]])
+    for _ in range(16):  # huge corners crossing the image
+        a = rng.uniform(-1, 1, 2)
+        faces.append([[a[0], a[1], 1.0], [a[0] + 3e6, a[1] - 2e6, 2.0], [a[0] - 2e6, a[1] + 4e6, 1.5]])
+    for _ in range(16):  # one very long edge
+        a = rng.uniform(-1, 1, 2)
+        faces.append([[a[0], a[1], 1.0], [a[0] + 5e5, a[1] + 0.3, 2.0], [a[0] + 0.2, a[1] + 0.4, 1.5]])
+    for _ in range(24):  # slivers: tiny area, long edges
+        a, d = rng.uniform(-0.8, 0.8, 2), rng.uniform(-1, 1, 2)
+        e = rng.uniform(2e-8, 2e-6)
+        faces.append([[a[0], a[1], 1.0], [a[0] + d[0], a[1] + d[1], 1.2], [a[0] + d[0] / 2 + e, a[1] + d[1] / 2, 0.8]])
+    return np.asarray(faces, dtype=np.float32)
+
+
+@pytest.mark.parametrize("blur,clip", [(0.0, False), (2e-3, True), (5e-2, True)])
+def test_rasterizer_forward_extreme_faces_bitwise(blur, clip, device):
+    """(A fixed 1e-3 blur band around the fast distance, rounds 1-4, failed here at blur 2e-3.)"""
+    fv = np.concatenate([_extreme_soup(3), _soup(60, 4)])
+    first, nf = np.array([0]), np.array([len(fv)])
+    _, (p2f, zbuf, bary, dists) = _run_native(fv, first, nf, 32, 32, 24, blur, False, clip, False, device)
+    rp, rz, rb, rd = rast_ref.rast_fwd(fv, first, nf, 32, 32, 24, blur, False, clip, False)
+    assert (rp >= 0).sum() > 100
+    np.testing.assert_array_equal(p2f.cpu().numpy(), rp)
+    np.testing.assert_array_equal(zbuf.detach().cpu().numpy(), rz)
+    np.testing.assert_array_equal(dists.detach().cpu().numpy(), rd)
+    np.testing.assert_array_equal(bary.detach().cpu().numpy(), rb)
+
+
 @pytest.mark.parametrize("persp,clip", [(False, False), (False, True), (True, True)])
 def test_rasterizer_backward_matches_oracle(persp, clip, device):
     fv = _soup(120, 3)
