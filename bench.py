@@ -263,12 +263,14 @@ class WorkloadCPU:
 
 
 # ------------------------------------------------------------------ the step
-def build_step(wl, world, mode, device, grad_weight):
+def build_step(wl, world, mode, device, grad_weight, dist_on=None):
     """Returns step() for eager or HIP-graph mode.  A step is one full pose-optimisation
     iteration of eval.py:343-376: forward, loss, backward, (N>1: the gradient all-reduce),
     Adam step on the pose (lr 5e-2, eval.py:320,337).  In graph mode forward+backward
     (incl. the Philox key advance) and the Adam step are captured HIP graphs (one graph at
-    N=1); sigma/gamma/alpha live on the device so no host synchronisation remains."""
+    N=1); sigma/gamma/alpha live on the device so no host synchronisation remains.  dist_on (default
+    world > 1): the gradient all-reduce between the captured forward/backward and Adam graphs."""
+    dist_on = world > 1 if dist_on is None else dist_on
     if mode == "eager":
         # the same Adam update as eval.py:320's torch.optim.Adam, as one fused kernel (the default
         # multi-tensor path spends ~120 us of host time per step on a single (N,3) parameter)
@@ -276,7 +278,7 @@ def build_step(wl, world, mode, device, grad_weight):
 
         def step():
             wl.forward().backward()
-            if world > 1:
+            if dist_on:
                 average_gradients(wl.params(), weight=grad_weight)
             wl.opt.step()
             wl.zero_grad()
@@ -302,10 +304,10 @@ def build_step(wl, world, mode, device, grad_weight):
     with torch.cuda.graph(graph, capture_error_mode="thread_local"):
         ds.advance()
         wl.forward().backward()
-        if world == 1:
+        if not dist_on:
             wl.opt.step()
     wl.graph = graph
-    if world == 1:
+    if not dist_on:
         return graph.replay
     opt_graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(opt_graph, capture_error_mode="thread_local"):
@@ -319,7 +321,7 @@ def build_step(wl, world, mode, device, grad_weight):
     return step
 
 
-def split_fwd_bwd(wl, steps, world):
+def split_fwd_bwd(wl, steps, world, dist_on=None):
     """Forward and backward(+Adam) as two separately captured graphs sharing one pool, replayed
     in order with events recorded between the replays: (ms_forward, ms_backward)."""
     pool = torch.cuda.graph_pool_handle()
@@ -329,7 +331,7 @@ def split_fwd_bwd(wl, steps, world):
         loss = wl.forward()
     with torch.cuda.graph(gb, pool=pool, capture_error_mode="thread_local"):
         loss.backward(retain_graph=True)
-        if world == 1:
+        if not (world > 1 if dist_on is None else dist_on):
             wl.opt.step()
     for _ in range(3):
         gf.replay()
@@ -432,7 +434,10 @@ def main():
     backend = os.environ.get("PR_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local = local % torch.cuda.device_count()
-    if world > 1:
+    # PR_BENCH_DIST=1: the process group, the gradient all-reduce and the max-over-ranks timing at
+    # N = 1 too (one RCCL rank: the N > 1 code path on a one-GPU box, tests/test_gpu_rccl.py)
+    dist_on = world > 1 or os.environ.get("PR_BENCH_DIST", "0") == "1"
+    if dist_on:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -463,34 +468,34 @@ def main():
     P = cfg["batch"] * cfg["image_size"] * cfg["image_size"]
     mode, note = args.mode, None
     try:
-        step = build_step(wl, world, mode, device, grad_weight)
+        step = build_step(wl, world, mode, device, grad_weight, dist_on)
     except Exception as e:  # graph capture unavailable: measure eagerly and say so
         note = f"graph capture failed ({type(e).__name__}: {e}); eager fallback"
         pa.noise.use_device_seed(None)
         wl = mk_wl()
         mode = "eager"
-        step = build_step(wl, world, mode, device, grad_weight)
+        step = build_step(wl, world, mode, device, grad_weight, dist_on)
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     n_split = min(args.steps, 20)
     if mode == "graph":
-        ms_fwd, ms_bwd = split_fwd_bwd(wl, n_split, world)
+        ms_fwd, ms_bwd = split_fwd_bwd(wl, n_split, world, dist_on)
         split_from = ("HIP events around separately captured forward and backward(+Adam) graphs, replayed "
                       "after the timed region")
     else:
@@ -553,7 +558,8 @@ def main():
         meshes = f"{B} meshes alternating sphere_642 / cube2 ({wl.F} faces), one pose each"
     samples_txt = f"Sr={Sr} Sa={S}" if Sr != S else f"Sr=Sa={S}"
     if world == 1:
-        par = "single GPU"
+        par = "single GPU" + (f" (process group: one {backend} rank, gradient all-reduce between the forward/"
+                              "backward and Adam graphs)" if dist_on else "")
     elif shard == "frames":
         par = (f"frame-parallel x{world}: each rank renders its own view (azimuth 120 + 360 r / {world}) of the "
                "shared pose; one RCCL all-reduce averages the gradients")
@@ -609,7 +615,7 @@ def main():
         out["speedup_vs_cpu"] = round(value / v, 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -39,9 +39,13 @@ def _inputs(dev, S):
     return to(p2f), to(dists, True), to(zbuf, True), to(colors, True), to(gimg), leaves, S
 
 
-def _worker(rank, world, port, S, out_path):
+def _worker(rank, world, port, S, out_path, backend="gloo"):
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: one rank per GPU, so world 1 on the one-GPU box
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         from pertrenderer_amd import Noise, perturbed_blend
         from pertrenderer_amd.parallel import exact_sharded_blend, reduce_scalar_grads
@@ -81,10 +85,10 @@ def _worker(rank, world, port, S, out_path):
         dist.destroy_process_group()
 
 
-def _run(world, S):
+def _run(world, S, backend="gloo"):
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "out.pt")
-        mp.spawn(_worker, args=(world, _free_port(), S, path), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), S, path, backend), nprocs=world, join=True)
         return torch.load(path, weights_only=True)
 
 
@@ -112,3 +116,13 @@ def test_exact_mode_composition_matches_fused_blend():
     for k in ("dists", "zbuf", "colors"):
         _close(one[k], one["f_" + k], name=k)
     _close(one["scalars"], one["f_scalars"], rtol=2e-5, name="scalars")
+
+
+def test_exact_mode_on_one_rccl_rank():
+    """The same exact-mode step over an RCCL (torch.distributed "nccl") process group of one rank:
+    its collectives (device all-reduces in both autograd directions, the smoothing-scalar completion)
+    run through RCCL and return the gloo run's values bit for bit."""
+    one = _run(1, 8)
+    rccl = _run(1, 8, backend="nccl")
+    for k in ("image", "dists", "zbuf", "colors", "scalars", "scalars2", "scalars3"):
+        assert torch.equal(rccl[k], one[k]), k
