@@ -1777,19 +1777,41 @@ PR_DEV void project_vertex_bwd(const float* M, const float* P, const float* v, f
 
 // CSR form: each vertex sums its corners' d face_verts in corner order (the verts[faces]
 // backward), then one Jacobian per vertex.  Deterministic, no atomics, every row written.
+// The corners go in batches of kGatherB: the batch's corner ids, then their gradients, each
+// level's loads in flight together (a vertex has ~6 corners: two load round trips instead of a
+// dependent pair per corner); the sums keep the corner order.
+constexpr int kGatherB = 8;
 __global__ void project_bwd_gather_kernel(PRProjectArgs a) {
   for (int64_t vi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; vi < a.V; vi += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = a.vert_corner_start[vi], e = a.vert_corner_start[vi + 1];
     float g[3] = {0.f, 0.f, 0.f};
     if (s < e) {
       float gx = 0.f, gy = 0.f, gz = 0.f;
-      for (int64_t j = s; j < e; ++j) {
-        const int64_t t = a.vert_corners[j];
-        gx += a.grad_face_verts[t * 3];
-        gy += a.grad_face_verts[t * 3 + 1];
-        gz += a.grad_face_verts[t * 3 + 2];
+      int64_t t0 = 0;
+      for (int64_t j0 = s; j0 < e; j0 += kGatherB) {
+        int64_t t[kGatherB];
+#pragma unroll
+        for (int u = 0; u < kGatherB; ++u) t[u] = j0 + u < e ? a.vert_corners[j0 + u] : -1;
+        if (j0 == s) t0 = t[0];
+        float c[kGatherB][3];
+#pragma unroll
+        for (int u = 0; u < kGatherB; ++u) {
+          if (t[u] >= 0) {
+            c[u][0] = a.grad_face_verts[t[u] * 3];
+            c[u][1] = a.grad_face_verts[t[u] * 3 + 1];
+            c[u][2] = a.grad_face_verts[t[u] * 3 + 2];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kGatherB; ++u) {
+          if (t[u] >= 0) {
+            gx += c[u][0];
+            gy += c[u][1];
+            gz += c[u][2];
+          }
+        }
       }
-      const int n = mesh_of(a.mesh_first_face, a.mesh_num_faces, a.N, a.vert_corners[s] / 3);
+      const int n = mesh_of(a.mesh_first_face, a.mesh_num_faces, a.N, t0 / 3);
       project_vertex_bwd(a.world_to_view + n * 16, a.proj + n * 16, a.verts + vi * 3, gx, gy, gz, g);
     }
     a.grad_verts[vi * 3] = g[0];
