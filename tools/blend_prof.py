@@ -49,3 +49,9 @@ for w, name, ph in ((0, "blend_fwd", ["setup", "slots", "rast", "pixel", "argmax
     print("  phase us mean", dict(zip(ph, pm.tolist())), "\n  phase us max ", dict(zip(ph, px.tolist())))
     hist = np.histogram(st, bins=8)[0]
     print("  start histogram", hist.tolist())
+    dur = en - st
+    for q in (50, 90, 99):
+        print(f"  duration p{q} {np.percentile(dur, q):.1f} us")
+    for i in np.argsort(-dur)[:5]:  # the longest blocks: start, duration, phases
+        print(f"  long block start {st[i]:.1f} dur {dur[i]:.1f} phases",
+              dict(zip(ph, (r[i, 2:2 + len(ph)] / 2400).round(2).tolist())))
