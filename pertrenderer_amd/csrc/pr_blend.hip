@@ -176,6 +176,21 @@ PR_DEV int image_of(int n0, int rem0, int pl, int HW) {
   return n;
 }
 
+// znear / zfar of block pixel pl: the pass's first image's from registers (zf0 / zn0, loaded once
+// per pass with a uniform address), another image's from memory (a block crossing an image edge:
+// a branch no lane takes on single-frame batches).  The per-entry loads this replaces were a
+// dependent global round trip in every slot iteration of 1a, B1 and B8.
+PR_DEV void planes_of(const PRBlendParams& p, int n0, int rem0, int pl, int HW, float zf0, float zn0, float& zf,
+                      float& zn) {
+  const int n = image_of(n0, rem0, pl, HW);
+  zf = zf0;
+  zn = zn0;
+  if (n != n0) {
+    zf = p.zfar[n];
+    zn = p.znear[n];
+  }
+}
+
 // slot loop over [0, n) of a block with row length L: thread walks i = tid + 256*it,
 // (pl, k) = divmod(i, L) maintained incrementally
 #define PR_FOR_SLOTS(L, Q, R, NTOT)                                                      \
@@ -574,6 +589,7 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
   const int* ea = EA + ps;
   const int eb = uni(ea[0]);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
+  const float zf0 = p.zfar[n0], zn0 = p.znear[n0];
   if (tid == 0) *QN = 0;
   fill_owner(OWN, ea, eb, cl, npix, lsh, lpp);
   __syncthreads();
@@ -615,8 +631,8 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
         if (bt.ok[u]) {
           const int64_t gs = (pix0 + pl) * K + k;
           const bool m = mk[u];
-          const int n = image_of(n0, rem0, pl, g.HW);
-          const float zf = p.zfar[n], zn = p.znear[n];
+          float zf, zn;
+          planes_of(p, n0, rem0, pl, g.HW, zf0, zn0, zf, zn);
           B[li] = ((zf - zb[u]) / (zf - zn)) * (m ? 1.f : 0.f);
           if constexpr (RAST) {
             const int sat = m && sat_ok ? rast_saturated(dd[u], sc.sigma) : 0;
@@ -923,6 +939,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   const int* ea = EA + ps;
   const int eb = uni(ea[0]), nent = uni(ea[npix]) - eb;
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
+  const float zf0 = p.zfar[n0], zn0 = p.znear[n0];
   fill_owner(OWN, ea, eb, cl, npix, lsh, lpp, CN);
   __syncthreads();
   PR_BSTAMP(0);
@@ -991,8 +1008,8 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
             gm = mf;
           }
         }
-        const int n = image_of(n0, rem0, pl, g.HW);
-        const float zf = p.zfar[n], zn = p.znear[n];
+        float zf, zn;
+        planes_of(p, n0, rem0, pl, g.HW, zf0, zn0, zf, zn);
         PR[li] = prob;
         ZZ[li] = ((zf - zb[u]) / (zf - zn)) * mf;
         GM[li] = gm;
@@ -1302,9 +1319,10 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
     const float mf = m ? 1.f : 0.f;
     const float dzk = ZZ[li];
     const float dzinv = dzk + (k == (int)PX[pl * 12 + 2] ? PX[pl * 12 + 4] : 0.f);
-    const int n = image_of(n0, rem0, pl, g.HW);
+    float zf, zn;
+    planes_of(p, n0, rem0, pl, g.HW, zf0, zn0, zf, zn);
     // gradient only: hardware reciprocal of (zfar - znear) instead of an IEEE division
-    a.grad_zbuf[gs] = -((dzinv * mf) * __builtin_amdgcn_rcpf(p.zfar[n] - p.znear[n]));
+    a.grad_zbuf[gs] = -((dzinv * mf) * __builtin_amdgcn_rcpf(zf - zn));
     const float prob = PR[li];
     // L and 1/prob feed only gradients (tolerance, not winners): hardware log2 / rcp
     // (prob = count / Sr: never denormal; log2(1) = 0 and rcp(0) = inf exactly)
