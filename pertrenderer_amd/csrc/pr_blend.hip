@@ -81,6 +81,7 @@ struct Geo {
   int seg;                       // segment plan: entries per part E (0: static grid, passes of cap)
   int lsh_max;                   // segment plan: log2 of the most lanes per pixel a part may use
   int plan_fwd_list, plan_bwd_list;  // segment plan: int offsets of the two segment lists
+  int pm, pmNBI, pmW, pmA;           // interleaved pixel blocks (block_pixel; pm = 0: consecutive)
 };
 
 // a value every lane holds alike (read from LDS: a vector register) into a scalar register
@@ -139,6 +140,26 @@ PR_DEV int64_t pixel_block(const Geo& g) {
   if (g.bpi == 0) return blockIdx.x;
   const int64_t n = blockIdx.x / g.bpi;
   return n * g.bpi + centre_out((int)(blockIdx.x - n * g.bpi), g.bpi);
+}
+
+// Pixel j of pixel block blk.  Consecutive (pm = 0): blk * PB + j.  Interleaved (pm = 1, blocks
+// tiling images): within its image, block b takes pixel t = j * NBI + b (NBI = HW / PB blocks per
+// image: one pixel from each NBI-pixel band), its column rotated by j * A when the bands are whole
+// rows, so every block samples the whole frame and holds about the mean number of valid slots
+// instead of the heaviest blocks setting the span; a bijection within each image.  Every global
+// access and every Philox counter uses this physical index, so the outputs are those of the
+// consecutive blocks (the scalar gradients' per-block partial sums regroup).
+PR_DEV int block_pixel(const Geo& g, int64_t blk, int j) {
+  if (!g.pm) return (int)(blk * g.PB + j);
+  const int n = (int)(blk / g.pmNBI), b = (int)(blk - (int64_t)n * g.pmNBI);
+  int t = j * g.pmNBI + b;
+  if (g.pmA) {
+    const int row = t / g.pmW;
+    int col = t - row * g.pmW + (int)(((int64_t)j * g.pmA) % g.pmW);
+    if (col >= g.pmW) col -= g.pmW;
+    t = row * g.pmW + col;
+  }
+  return n * g.HW + t;
 }
 
 struct Sc {
@@ -247,10 +268,13 @@ PR_DEV int pixel_entries(const int32_t* pcnt, int64_t gp, int K, bool compact) {
 }
 
 // E > 0: the passes are the block's entry-balanced segment parts instead (see below).
-PR_DEV void block_entries(const int32_t* pcnt, int64_t pix0, int npix, int K, bool compact, int CAP, int PB,
-                          int* CL, int* CP, int* EA, int* PS, int E = 0) {
+// GPX[0..npix): the block's physical pixels (block_pixel).
+PR_DEV void block_entries(const Geo& g, int64_t blk, const int32_t* pcnt, int npix, int K, bool compact, int CAP,
+                          int PB, int* CL, int* CP, int* EA, int* PS, int* GPX, int E = 0) {
   const int tid = threadIdx.x;
-  const int cp = tid < npix ? (pcnt ? min(max((int)pcnt[pix0 + tid], 0), K) : K) : 0;
+  const int gpv = tid < npix ? block_pixel(g, blk, tid) : 0;
+  if (tid < npix) GPX[tid] = gpv;
+  const int cp = tid < npix ? (pcnt ? min(max((int)pcnt[gpv], 0), K) : K) : 0;
   const int c = compact ? cp : K;
   const int v = tid < npix ? c + 1 : 0;
   int x = v;
@@ -535,7 +559,8 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
   int* CP = CL + PB;                                        // [PB] valid-prefix count (K without pix_count)
   int* EA = CP + PB;                                        // [PB+1] exclusive prefix of entries (CL + 1)
   int* PS = EA + PB + 1;                                    // [PB+2] pass starts; [PB+1] = pass count
-  int* QN = PS + PB + 2;                                    // rast queue length
+  int* GPX = PS + PB + 2;                                   // [PB] physical pixel (block_pixel)
+  int* QN = GPX + PB;                                       // rast queue length
   uint16_t* Q = reinterpret_cast<uint16_t*>(QN + 4);        // [CAP] rast queue (pl << 8 | k)
   uint8_t* LC = reinterpret_cast<uint8_t*>(Q);              // [CAP] argmax candidates (after 1b)
   uint8_t* OWN = reinterpret_cast<uint8_t*>(Q + CAP);       // [CAP] pixel of each entry
@@ -546,24 +571,27 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
   const int64_t bpix0 = blk * PB;
   const int bnpix = (int)min((int64_t)PB, g.P - bpix0);
   const int32_t* pcnt = a.pix_count;
-  if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, pcnt != nullptr, CAP, PB, CL, CP, EA, PS, SEG ? g.seg : 0);
+  if (tid < 64) block_entries(g, blk, pcnt, bnpix, K, pcnt != nullptr, CAP, PB, CL, CP, EA, PS, GPX, SEG ? g.seg : 0);
   __syncthreads();
   const float gal = sc.gamma / sc.alpha;
   // ---- empty block (no pixel has a valid slot: only background entries): every sample's
   //      argmax is the background, W_bg = Sa / Sa = 1, alpha = 1 - (empty product) = 0; the
   //      same values the phases below would produce, without them
   if (pcnt && g.empty && uni(EA[bnpix]) == bnpix) {
-    for (int i = tid; i < bnpix * p.Sa; i += kThreads) a.winners[bpix0 * p.Sa + i] = (uint8_t)K;
+    for (int i = tid; i < bnpix * p.Sa; i += kThreads) {
+      const int pl = i / p.Sa;
+      a.winners[(int64_t)GPX[pl] * p.Sa + (i - pl * p.Sa)] = (uint8_t)K;
+    }
     if constexpr (CM != 0) {
       if (tid < bnpix) {
         const float wb = (float)p.Sa / (float)p.Sa;
-        reinterpret_cast<float4*>(a.image)[bpix0 + tid] =
+        reinterpret_cast<float4*>(a.image)[GPX[tid]] =
             make_float4(0.f + wb * p.background[0], 0.f + wb * p.background[1], 0.f + wb * p.background[2], 1.f - 1.f);
       }
     } else {
       for (int i = tid; i < bnpix * KP1; i += kThreads) {
-        const int k = i - (i / KP1) * KP1;
-        a.weights[bpix0 * KP1 + i] = k == K ? (float)p.Sa / (float)p.Sa : 0.f / (float)p.Sa;
+        const int pl = i / KP1, k = i - pl * KP1;
+        a.weights[(int64_t)GPX[pl] * KP1 + k] = k == K ? (float)p.Sa / (float)p.Sa : 0.f / (float)p.Sa;
       }
     }
     __syncthreads();  // (SEG: the next segment rewrites this block's LDS)
@@ -583,10 +611,11 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
     while (NC < 64 && npix * ng * NC * 2 <= kThreads && (KP1 + NC * 2 - 1) / (NC * 2) >= 4) NC <<= 1;
   }
   const int lpp = 1 << lsh;
-  const int64_t pix0 = bpix0 + ps;
+  const int64_t pix0 = bpix0 + ps;  // logical: image / plane lookups (blocks keep to one image when interleaved)
   const int* cl = CL + ps;
   const int* cpv = CP + ps;
   const int* ea = EA + ps;
+  const int* gpx = GPX + ps;
   const int eb = uni(ea[0]);
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   const float zf0 = p.zfar[n0], zn0 = p.znear[n0];
@@ -615,7 +644,7 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
         mk[u] = false;
         dd[u] = zb[u] = 0.f;
         if (bt.ok[u]) {
-          const int64_t gs = (pix0 + bt.pl[u]) * K + bt.k[u];
+          const int64_t gs = (int64_t)gpx[bt.pl[u]] * K + bt.k[u];
           // with valid-prefix counts nothing is read at a masked slot
           mk[u] = pcnt ? bt.k[u] < cpv[bt.pl[u]] : slot_mask(a.pix_to_face, a.mask, gs);
           if (mk[u] || !pcnt) {
@@ -629,7 +658,7 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
         const int pl = bt.pl[u], k = bt.k[u], li = i0 + u * kThreads;  // entry index
         bool want = false;
         if (bt.ok[u]) {
-          const int64_t gs = (pix0 + pl) * K + k;
+          const int64_t gs = (int64_t)gpx[pl] * K + k;
           const bool m = mk[u];
           float zf, zn;
           planes_of(p, n0, rem0, pl, g.HW, zf0, zn0, zf, zn);
@@ -664,7 +693,7 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
     const int nq = *QN;
     for (int i = tid; i < nq; i += kThreads) {
       const int e = Q[i], pl = e >> 8, k = e & 255, li = ea[pl] - eb + k;
-      const int64_t gp = pix0 + pl, gs = gp * K + k;
+      const int64_t gp = gpx[pl], gs = gp * K + k;
       const float dist = A[li];
       float prob;
       if (a.rast_cache) {  // also keep the score mean for the backward (same arithmetic as its B1)
@@ -755,7 +784,7 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
       const int c = t & (NC - 1), pg = t / NC;
       const int pl = act ? pg / ng : 0, gi = act ? pg - pl * ng : 0;
       const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
-      const int64_t gp = pix0 + pl;
+      const int64_t gp = act ? gpx[pl] : 0;
       const int e0 = ea[pl] - eb, cpl = cl[pl];
       float best[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
       int bidx[4] = {-1, -1, -1, -1};
@@ -811,7 +840,7 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
         if (cw == 0) continue;
         const float w = (float)cw / fSa;
         float c[3];
-        slot_color<CM>(a, (pix0 + pl) * K + k, c);
+        slot_color<CM>(a, (int64_t)gpx[pl] * K + k, c);
         acc0 += w * c[0];
         acc1 += w * c[1];
         acc2 += w * c[2];
@@ -829,13 +858,13 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
       o.y = acc1 + wb * p.background[1];
       o.z = acc2 + wb * p.background[2];
       o.w = 1.f - PX[pl * 4 + 1];
-      reinterpret_cast<float4*>(a.image)[pix0 + pl] = o;
+      reinterpret_cast<float4*>(a.image)[gpx[pl]] = o;
     }
   } else {
     PR_FOR_SLOTS(KP1, g.qK1, g.rK1, npix * KP1) {  // dense K+1 weights: 0 past the slot entries
       const int c = cl[pl];
       const int cw = (k < c || k == K) ? CNT[ea[pl] - eb + (k == K ? c : k)] : 0;
-      a.weights[(pix0 + pl) * KP1 + k] = (float)cw / fSa;
+      a.weights[(int64_t)gpx[pl] * KP1 + k] = (float)cw / fSa;
     }
   }
   __syncthreads();  // the next pass reuses every LDS record
@@ -894,7 +923,8 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   int* CP = CL + PB;                   // [PB] valid-prefix count (K without pix_count)
   int* EA = CP + PB;                   // [PB+1] exclusive prefix of entries (CL + 1)
   int* PS = EA + PB + 1;               // [PB+2] pass starts; [PB+1] = pass count
-  uint8_t* OWN = reinterpret_cast<uint8_t*>(PS + PB + 2);  // [CAP] pixel of each entry
+  int* GPX = PS + PB + 2;              // [PB] physical pixel (block_pixel)
+  uint8_t* OWN = reinterpret_cast<uint8_t*>(GPX + PB);  // [CAP] pixel of each entry
   uint8_t* WN = OWN + CAP;             // [PB][Sa] the forward's winners of the pass
   const int tid = threadIdx.x;
   PR_BPROF_DECL;
@@ -906,7 +936,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   // B6 draws the masked tail jointly (tail_pair) in Philox Gaussian mode when the valid
   // prefix is known; injected noise (parity) and Cauchy noise keep one row per slot
   const bool tail = NOISE == PR_NOISE_PHILOX && !agg_cauchy && pcnt != nullptr && g.tail;
-  if (tid < 64) block_entries(pcnt, bpix0, bnpix, K, tail, CAP, PB, CL, CP, EA, PS, SEG ? g.seg : 0);
+  if (tid < 64) block_entries(g, blk, pcnt, bnpix, K, tail, CAP, PB, CL, CP, EA, PS, GPX, SEG ? g.seg : 0);
   __syncthreads();
   const float gal = sc.gamma / sc.alpha;
   float part_sigma = 0.f, part_q = 0.f, part_a = 0.f, part_gal = 0.f;
@@ -915,11 +945,22 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   //      no scalar partials; masked slots get zero d zbuf / d dists / d colour (the values B8m
   //      writes).  Without the baseline (GaussianAgg_wovr) a_s = dW_bg and the full path runs.
   if (RAST && tail && g.empty && !(p.flags & PR_BLEND_AGG_WOVR) && uni(EA[bnpix]) == bnpix) {
-    const int64_t s0 = bpix0 * K, n = (int64_t)bnpix * K;
-    block_fill(a.grad_zbuf + s0, n, 0.f);
-    block_fill(a.grad_dists + s0, n, 0.f);
-    if constexpr (CM == 1) block_fill(a.grad_colors + 3 * s0, 3 * n, 0.f);
-    if constexpr (CM == 2) block_fill(a.grad_bary + 3 * s0, 3 * n, 0.f);
+    if (!g.pm) {
+      const int64_t s0 = bpix0 * K, n = (int64_t)bnpix * K;
+      block_fill(a.grad_zbuf + s0, n, 0.f);
+      block_fill(a.grad_dists + s0, n, 0.f);
+      if constexpr (CM == 1) block_fill(a.grad_colors + 3 * s0, 3 * n, 0.f);
+      if constexpr (CM == 2) block_fill(a.grad_bary + 3 * s0, 3 * n, 0.f);
+    } else {  // interleaved: one K-slot row per pixel
+      for (int i = tid; i < bnpix * K; i += kThreads) {
+        const int pl = i / K;
+        const int64_t s = (int64_t)GPX[pl] * K + (i - pl * K);
+        a.grad_zbuf[s] = 0.f;
+        a.grad_dists[s] = 0.f;
+        if constexpr (CM == 1) a.grad_colors[3 * s] = a.grad_colors[3 * s + 1] = a.grad_colors[3 * s + 2] = 0.f;
+        if constexpr (CM == 2) a.grad_bary[3 * s] = a.grad_bary[3 * s + 1] = a.grad_bary[3 * s + 2] = 0.f;
+      }
+    }
     if (tid < 4) put_partial(a, partials + pidx * 4 + tid, 0.f);
     __syncthreads();  // (SEG: the next segment rewrites this block's LDS)
     return;
@@ -933,10 +974,11 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   if constexpr (SEG)
     while (lsh < g.lsh_max && (2 << lsh) * npix <= kThreads) ++lsh;
   const int lpp = 1 << lsh;
-  const int64_t pix0 = bpix0 + ps;
+  const int64_t pix0 = bpix0 + ps;  // logical: image / plane lookups (blocks keep to one image when interleaved)
   const int* cl = CL + ps;
   const int* cpv = CP + ps;
   const int* ea = EA + ps;
+  const int* gpx = GPX + ps;
   const int eb = uni(ea[0]), nent = uni(ea[npix]) - eb;
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   const float zf0 = p.zfar[n0], zn0 = p.znear[n0];
@@ -963,7 +1005,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
         zb[u] = dw[u] = 0.f;
         if (!bt.ok[u]) continue;
         const int pl = bt.pl[u], k = bt.k[u];
-        const int64_t gp = pix0 + pl;
+        const int64_t gp = gpx[pl];
         if (k < K) {
           const int64_t gs = gp * K + k;
           // with valid-prefix counts nothing is read at a masked slot (prob, score, z_inv are 0)
@@ -1024,7 +1066,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
           if (k >= cl[pl]) continue;
           float prob = 0.f, gm = 0.f;
           if (GM[li] != 0.f) {
-            const int64_t gp = pix0 + pl, gs = gp * K + k;
+            const int64_t gp = gpx[pl], gs = gp * K + k;
             float gacc;
             const int cnt = rast_count_score<NOISE>(p, sc, PR[li], (uint32_t)gp, k, gs, g.PK, gacc);
             prob = ((float)cnt / (float)p.Sr) * 1.f;
@@ -1037,18 +1079,21 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
     }
     // the pass's winners (one contiguous byte range) into LDS for B5, with their win counts
     // (CN zeroed with the owner map); kU loads in flight per thread
-    const uint8_t* wsrc = a.winners + pix0 * Sa;
     const int nw = npix * Sa;
     for (int i0 = tid; i0 < nw; i0 += kU * kThreads) {
-      int w[kU];
+      int w[kU], wp[kU];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) w[u] = i0 + u * kThreads < nw ? wsrc[i0 + u * kThreads] : 0;
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + u * kThreads;
+        wp[u] = i / Sa;  // (Sa: runtime divisor, once per winner)
+        w[u] = i < nw ? a.winners[(int64_t)gpx[min(wp[u], npix - 1)] * Sa + (i - wp[u] * Sa)] : 0;
+      }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int i = i0 + u * kThreads;
         if (i >= nw) continue;
         WN[i] = (uint8_t)w[u];
-        const int pl = i / Sa;  // (Sa: runtime divisor, once per winner)
+        const int pl = wp[u];
         atomicAdd(&CN[ea[pl] - eb + (w[u] == K ? cl[pl] : w[u])], 1);
       }
     }
@@ -1178,7 +1223,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
         for (int e = l; e < c; e += lpp) {
           if (CN[e0 + e] == 0 && e != jb) continue;
           float cc[3];
-          slot_color<CM>(a, (pix0 + pl) * K + e, cc);
+          slot_color<CM>(a, (int64_t)gpx[pl] * K + e, cc);
           DW[e0 + e] = (gi[0] * cc[0] + gi[1] * cc[1]) + gi[2] * cc[2];
         }
       }
@@ -1224,7 +1269,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
         const int pl = OWN[row];
         const int r = row - (ea[pl] - eb);
         const int j = r == cl[pl] ? K : r;
-        const int64_t gp = pix0 + pl;
+        const int64_t gp = gpx[pl];
         for (int gi = c; gi < ng; gi += nch) {
           const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
           const int sbase = (int)(4 * gg) - (NOISE == PR_NOISE_INJECTED ? 0 : p.sample_offset_a);
@@ -1261,7 +1306,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
         float t = 0.f;
         if (m > 0 && as != 0.f) {
           float s1, s2;
-          tail_pair(sc.ka, (uint32_t)(pix0 + pl), (uint32_t)(p.sample_offset_a + s), m, s1, s2);
+          tail_pair(sc.ka, (uint32_t)gpx[pl], (uint32_t)(p.sample_offset_a + s), m, s1, s2);
           t = (as * s1) * inv_gamma;
           part_q += as * s2;
         }
@@ -1305,7 +1350,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   for (int li = tid; li < nent; li += kThreads) {
     const int pl = OWN[li], k = li - (ea[pl] - eb);
     if (k >= cl[pl]) continue;  // the background entry
-    const int64_t gp = pix0 + pl, gs = gp * K + k;
+    const int64_t gp = gpx[pl], gs = gp * K + k;
     int64_t fk = -1;
     bool m;
     if (pcnt) {  // the face id is read below, for the (few) slots that won a sample
@@ -1382,7 +1427,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   if (tail) {
     const int lane = tid & 63;
     for (int mpl = tid >> 6; mpl < npix; mpl += kThreads / 64) {
-      const int64_t gp = pix0 + mpl;
+      const int64_t gp = gpx[mpl];
       float dprob = 0.f;
       if constexpr (!RAST && CM != 0) dprob = PX[mpl * 12 + 11] * PX[mpl * 12 + 5];
       for (int k = cl[mpl] + lane; k < K; k += 64) {
@@ -1705,10 +1750,10 @@ struct Shape {
   int PB, cap;
 };
 size_t fwd_lds(int PB, int cap) {
-  return (size_t)(2 * cap + 8 * PB + 7) * sizeof(float) + (size_t)cap * (sizeof(uint16_t) + 1);
+  return (size_t)(2 * cap + 9 * PB + 7) * sizeof(float) + (size_t)cap * (sizeof(uint16_t) + 1);
 }
 size_t bwd_lds(int PB, int cap, int Sa) {
-  return (size_t)(6 * cap + PB * Sa + 16 * PB + 3) * sizeof(float) + (size_t)cap + (size_t)PB * Sa;
+  return (size_t)(6 * cap + PB * Sa + 17 * PB + 3) * sizeof(float) + (size_t)cap + (size_t)PB * Sa;
 }
 constexpr size_t kLdsTargetFwd = 20 * 1024, kLdsTargetBwd = 24 * 1024, kLdsMax = 60 * 1024;
 
@@ -1819,6 +1864,14 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   g.tail = tail;
   const char* empty = getenv("PR_BLEND_EMPTY");  // read per call: tests compare both paths in one process
   g.empty = empty ? atoi(empty) : 1;
+  // interleaved pixel blocks (block_pixel): blocks must tile images; PR_BLEND_INTERLEAVE=0|1
+  // (read per call: tests compare both layouts in one process); the segment plan turns it off
+  const char* il = getenv("PR_BLEND_INTERLEAVE");
+  g.pm = (il ? atoi(il) : 1) != 0 && PB > 1 && g.HW % PB == 0;
+  g.pmNBI = g.pm ? g.HW / PB : 1;
+  g.pmW = p.W;
+  g.pmA = g.pm && g.pmNBI % p.W == 0 ? ((int)(0.6180339887 * p.W) | 1) % p.W : 0;
+  if (g.pm) g.bpi = 0;  // balanced blocks: no dispatch order to choose
   return g;
 }
 
@@ -1966,6 +2019,7 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
     if (int e = check_launch("blend_plan")) return e;
     geo.lsh_max = pc.lsh_max[0];
     geo.plan_fwd_list = pc.q.list[0];
+    geo.pm = 0;  // the plan cuts consecutive pixel blocks
     nblk = pc.q.T[0] + pc.q.X[0];  // the plan's bound on the segments
     if (a.p.noise_mode == PR_NOISE_INJECTED) launch_fwd<PR_NOISE_INJECTED, false, true>(a, geo, NC, st, lds, (int)nblk);
     else launch_fwd<PR_NOISE_PHILOX, false, true>(a, geo, NC, st, lds, (int)nblk);
@@ -2025,6 +2079,7 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
   if (pc.on) {  // the forward's plan: entry-balanced segments taken by resident workgroups
     geo.lsh_max = pc.lsh_max[1];
     geo.plan_bwd_list = pc.q.list[1];
+    geo.pm = 0;  // the plan cuts consecutive pixel blocks
     nblk = pc.q.T[1] + pc.q.X[1];  // the plan's bound on the segments
     if (a.p.noise_mode == PR_NOISE_INJECTED) launch_bwd<PR_NOISE_INJECTED, false, true>(a, geo, st, lds, (int)nblk, part);
     else launch_bwd<PR_NOISE_PHILOX, false, true>(a, geo, st, lds, (int)nblk, part);
