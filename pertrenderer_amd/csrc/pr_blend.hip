@@ -1864,15 +1864,18 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   g.tail = tail;
   const char* empty = getenv("PR_BLEND_EMPTY");  // read per call: tests compare both paths in one process
   g.empty = empty ? atoi(empty) : 1;
-  // interleaved pixel blocks (block_pixel): blocks must tile images.  Default: grids of more than
-  // 8192 blocks (batches: cfg 3 4646 -> 4777, cfg 4 817 -> 841 frames/s, the backward's blocks even
-  // out over many generations); one-frame grids keep consecutive blocks, whose empty-block shortcut
+  // interleaved pixel blocks (block_pixel): blocks must tile images.  Default: the backward's grids
+  // of more than 8192 blocks (batches: cfg 3 4646 -> 4777, cfg 4 817 -> 841 frames/s with both
+  // kernels interleaved, the backward's blocks even out over many generations: cfg 3 blend_bwd
+  // 1.21 -> 1.07 ms; the forward lost there, 0.56 -> 0.60 ms, so it keeps consecutive blocks --
+  // the two layouts are independent, winners and caches are indexed by physical pixel and slot);
+  // one-frame grids keep consecutive blocks, whose empty-block shortcut
   // frees half the grid at once (interleaved, every block carries work and the forward's 2048
   // blocks outnumber the 1792 resident: cfg 2 3197 -> 3060, eval 3460 -> 3205;
   // profiles/r4_experiments.txt).  PR_BLEND_INTERLEAVE=0|1 forces it (read per call: tests compare
   // both layouts in one process); the segment plan turns it off.
   const char* il = getenv("PR_BLEND_INTERLEAVE");
-  g.pm = (il ? atoi(il) != 0 : g.P / PB > 8192) && PB > 1 && g.HW % PB == 0;
+  g.pm = (il ? atoi(il) != 0 : bwd && g.P / PB > 8192) && PB > 1 && g.HW % PB == 0;
   g.pmNBI = g.pm ? g.HW / PB : 1;
   g.pmW = p.W;
   g.pmA = g.pm && g.pmNBI % p.W == 0 ? ((int)(0.6180339887 * p.W) | 1) % p.W : 0;

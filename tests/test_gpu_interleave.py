@@ -131,3 +131,29 @@ def test_interleaved_blocks_aggregate(device):
     a = _with("1", run)
     b = _with("0", run)
     _compare(a, b, ("weights", "d prob", "d zbuf", "d gamma", "d alpha"), loose=("d prob", "d zbuf", "d gamma", "d alpha"))
+
+
+def test_default_layout_on_a_batch_grid(device):
+    """The default on a batch grid (5 x 256^2, backward grid > 8192 blocks): consecutive forward,
+    interleaved backward -- the forward's winners and rast cache are read by physical pixel / slot,
+    so the mixed pair equals the consecutive one (image bitwise, gradients to summation order)."""
+    p2f, d0, z0, c0 = _frags(device, 5, 256, 256, 8, seed=21)
+
+    def run():
+        dists, zbuf, colors = (t.clone().requires_grad_(True) for t in (d0, z0, c0))
+        sig, gam, alp = (torch.tensor(v, device=device, requires_grad=True) for v in (1e-3, 1e-2, 1.0))
+        img = pa.perturbed_blend(colors, p2f, dists, zbuf, sig, gam, alp, 8, 8, background=(0.1, 0.2, 0.3),
+                                 noise=Noise.philox(seed_r=3, seed_a=4))
+        g = torch.randn(img.shape, device=device, generator=torch.Generator(device).manual_seed(5))
+        img.backward(g)
+        torch.cuda.synchronize()
+        return [img.detach(), dists.grad, zbuf.grad, colors.grad, sig.grad, gam.grad, alp.grad]
+    old = os.environ.pop("PR_BLEND_INTERLEAVE", None)
+    try:
+        a = run()
+    finally:
+        if old is not None:
+            os.environ["PR_BLEND_INTERLEAVE"] = old
+    b = _with("0", run)
+    _compare(a, b, ("image", "d dists", "d zbuf", "d colours", "d sigma", "d gamma", "d alpha"),
+             loose=("d dists", "d zbuf", "d colours", "d sigma", "d gamma", "d alpha"))
