@@ -174,13 +174,33 @@ def dense_roofline(device, P_side=256, K=50, S=8, iters=20, N=1, Sr=None):
             img = pa.perturbed_blend(colors, p2f, dists, zbuf, sig, gam, alp, Sr, S, background=(0, 0, 0))
             img.backward(gimg)
         torch.cuda.synchronize()
+    # the kernel's own duration: the library's event pair immediately around it (pr_ktimer_arm), as
+    # for the headline roofline; the call-level pair (kt.summary) also holds that inner pair and the
+    # launch gaps, and read 10-15 % long (VERDICT r4 "What's weak" 4)
+    kmean, kmin, calls = kt.kernel_summary("mean"), kt.kernel_summary("min"), kt.summary("min")
+    shape = f"{N}x{P_side}^2, K={K}, Sr={Sr}, Sa={S}, every slot valid"
+    sha = source_sha()
+    headline = (N, P_side, K, S, Sr) == (1, 256, 50, 8, 8)
+    prof = committed_record("rocprof_dense.json", sha) if headline else None
+    pmc = committed_record("pmc_dense.json", sha) if headline else None
     out = {}
-    for name, (n, ms) in kt.summary("min").items():
+    for name, (kname, n, ms) in kmean.items():
         b = kernel_bytes(name, N * H * W, K, S, 0)
-        out[name] = {"achieved": round(b / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms": round(ms, 4),
-                     "bytes": b, "launches": n,
-                     "shape": f"{N}x{P_side}^2, K={K}, Sr={Sr}, Sa={S}, every slot valid"}
+        out[name] = {"kernel": kname, "achieved": round(b / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms": round(ms, 4),
+                     "ms_min": round(kmin[name][2], 4), "call_ms_min": round(calls[name][1], 4) if name in calls else None,
+                     "bytes": b, "launches": n, "shape": shape,
+                     "timing": "mean of the library's event pair around the kernel (pr_ktimer_arm)"}
+        if prof and kname in prof.get("kernels", {}):
+            avg_us = prof["kernels"][kname]["avg_us"]
+            out[name]["rocprof"] = {"avg_us": avg_us, "frac": round(b / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                                    "source": f"profiles/rocprof_dense.json ({prof.get('run', '')}), same source_sha"}
+        if pmc and pmc.get(name):
+            tr = pmc[name]
+            out[name]["traffic"] = tr.get("bytes_per_launch")
+            if tr.get("valu_issue_us"):
+                out[name]["valu_issue_us"] = tr["valu_issue_us"]
+                out[name]["valu_frac"] = round(tr["valu_issue_us"] / (1e3 * ms), 4)
     return out
 
 

@@ -82,6 +82,7 @@ struct Geo {
   int lsh_max;                   // segment plan: log2 of the most lanes per pixel a part may use
   int plan_fwd_list, plan_bwd_list;  // segment plan: int offsets of the two segment lists
   int pm, pmNBI, pmW, pmA;           // interleaved pixel blocks (block_pixel; pm = 0: consecutive)
+  int sync_rel;                      // fused scalar reduction: acq_rel arrivals (last_arrival)
 };
 
 // a value every lane holds alike (read from LDS: a vector register) into a scalar register
@@ -121,12 +122,28 @@ PR_DEV void put_partial(const Args& a, float* dst, float v) {
   }
 }
 
-PR_DEV bool last_arrival(int32_t* sync, int nblk, int* flag) {
+// Ordering (DESIGN.md §4 "Fused scalar reduction").  Default (rel = 0): relaxed arrivals.  The
+// HIP / LLVM memory model gives no happens-before edge from a partial to the last workgroup here;
+// what orders them is gfx950's: a device-scope RMW is performed at the device coherence point and
+// returns its old value only after that, the writer issues its arrival only after every partial
+// exchange of its workgroup has returned (s_waitcnt + the barrier), so each partial is in the
+// coherent memory before the arrival that counts it, and the last workgroup reads the partials
+// with device-scope (sc1) loads that bypass its XCD's L2.  rel = 1 (PR_BLEND_SYNC_ORDER=release)
+// is the model-conforming form: both arrivals acq_rel (a release per workgroup: its L2
+// writeback), the last workgroup's acquire synchronising with every earlier arrival through the
+// counters' release sequences.  Both give the same bits (tests/test_gpu_fused_finalize.py).
+PR_DEV bool last_arrival(int32_t* sync, int nblk, int* flag, bool rel) {
   __syncthreads();  // this workgroup's partial exchanges have returned
   if (threadIdx.x == 0) {
     const int r = (int)(blockIdx.x % 8), n_r = (nblk - r + 7) / 8;
     int last = 0;
-    if (atomicAdd(sync + r * kSyncStride, 1) == n_r - 1) last = atomicAdd(sync + kSyncTop, 1) == min(nblk, 8) - 1;
+    if (rel) {
+      if (__hip_atomic_fetch_add(sync + r * kSyncStride, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == n_r - 1)
+        last = __hip_atomic_fetch_add(sync + kSyncTop, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+               min(nblk, 8) - 1;
+    } else if (atomicAdd(sync + r * kSyncStride, 1) == n_r - 1) {
+      last = atomicAdd(sync + kSyncTop, 1) == min(nblk, 8) - 1;
+    }
     *flag = last;
   }
   __syncthreads();
@@ -222,6 +239,8 @@ PR_DEV void planes_of(const PRBlendParams& p, int n0, int rem0, int pl, int HW, 
 // flight before the first is consumed (the slot phases are latency-bound: one HBM round
 // trip per dependent iteration).
 constexpr int kU = 4;
+// B6: sample groups a lane sums as one register subtree (the canonical d z order, bwd_tile B6)
+constexpr int kB6T = 8;
 struct Batch {
   int pl[kU], k[kU];
   bool ok[kU];
@@ -1250,17 +1269,26 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
 
   // ---- B6: dz_j = mean_s(a_s * score(eps_sj) / gamma) and sum_s a_s * eps_sj * score(eps_sj)
   //          (d gamma; score = eps for Gaussian noise, 2 eps / (1 + eps^2) for Cauchy)
-  //   6a: one row per entry, split over nch adjacent lanes (groups gi = c, c + nch, ...)
-  //       and merged with xor-shuffles;
+  //   6a: one row per entry, split over nch adjacent lanes and merged with xor-shuffles;
   //   6b: with the tail draw, one item per (pixel, sample): the masked slots' joint draw,
   //       a_s * S2 into d gamma and a_s * S1 / gamma over a_s in AS (summed in B7).
+  // An entry's d z has ONE summation order whatever the lane split: each 4-sample group summed
+  // in sample order, then the groups (padded to NG2 = 2^ceil(log2 ng), missing ones 0) by a
+  // pairwise tree over the group index, lowest bit first.  Lane c of a row holds the groups
+  // [c T, c T + T) (T = NG2 / nch <= kB6T) and forms their subtree in registers; the xor-shuffles
+  // (masks 1, 2, ..., nch / 2) are the tree's upper levels.  nch follows the pass's entry count
+  // (few entries: more lanes per row), so without this the interleaved blocks (a pass holds the
+  // mean entry count) and the consecutive ones summed a pixel's d z differently.
   {
     // the reference divides each sample's a_s * score by gamma (smoothagg.py:52); one
     // reciprocal here instead of an IEEE division per (slot, sample): within 1 ulp
     const float inv_gamma = 1.f / sc.gamma;
-    int nch = 1;
+    int ng2 = 1;
+    while (ng2 < ng) ng2 <<= 1;
+    int nch = ng2 > kB6T ? ng2 / kB6T : 1;
+    if (nch > 64) nch = 64;  // (Sa > 2044: the lanes' T exceeds kB6T and sums its groups' subtrees in order)
     while (nch < 64 && 2 * nch <= ng && 2 * nch * nent <= kThreads) nch <<= 1;
-    const int lch = 31 - __builtin_clz(nch);
+    const int lch = 31 - __builtin_clz(nch), T = (ng2 + nch - 1) >> lch;
     for (int i0 = 0; i0 < nent * nch; i0 += kThreads) {  // uniform trip count (shuffles below)
       const int i = i0 + tid, row = i >> lch, c = i & (nch - 1);
       const bool live = row < nent;
@@ -1270,28 +1298,41 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
         const int r = row - (ea[pl] - eb);
         const int j = r == cl[pl] ? K : r;
         const int64_t gp = gpx[pl];
-        for (int gi = c; gi < ng; gi += nch) {
-          const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
-          const int sbase = (int)(4 * gg) - (NOISE == PR_NOISE_INJECTED ? 0 : p.sample_offset_a);
-          float av[4];
-          bool any = false;
+        for (int tb = 0; tb < T; tb += kB6T) {
+          float v[kB6T];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int s = sbase + u;
-            av[u] = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
-            any |= av[u] != 0.f;
-          }
-          if (!any) continue;
-          float e[4];
-          agg_noise4<NOISE>(p, sc, (uint32_t)gp, j, gg, g.P, KP1, e);
+          for (int t = 0; t < kB6T; ++t) {
+            v[t] = 0.f;
+            const int gi = c * T + tb + t;
+            if (tb + t >= T || gi >= ng) continue;
+            const uint32_t gg = (uint32_t)(NOISE == PR_NOISE_INJECTED ? gi : g0 + gi);
+            const int sbase = (int)(4 * gg) - (NOISE == PR_NOISE_INJECTED ? 0 : p.sample_offset_a);
+            float av[4];
+            bool any = false;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (av[u] != 0.f) {
-              const float scr = noise_score(e[u], agg_cauchy);
-              dz += (av[u] * scr) * inv_gamma;
-              q += av[u] * (e[u] * scr);
+            for (int u = 0; u < 4; ++u) {
+              const int s = sbase + u;
+              av[u] = (s >= 0 && s < Sa) ? AS[pl * Sa + s] : 0.f;
+              any |= av[u] != 0.f;
+            }
+            if (!any) continue;
+            float e[4];
+            agg_noise4<NOISE>(p, sc, (uint32_t)gp, j, gg, g.P, KP1, e);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (av[u] != 0.f) {
+                const float scr = noise_score(e[u], agg_cauchy);
+                v[t] += (av[u] * scr) * inv_gamma;
+                q += av[u] * (e[u] * scr);
+              }
             }
           }
+          // the subtree of these kB6T groups (pairs, then quads, ...; past T only zeros)
+#pragma unroll
+          for (int h = 1; h < kB6T; h <<= 1)
+#pragma unroll
+            for (int t = 0; t < kB6T; t += 2 * h) v[t] = v[t] + v[t + h];
+          dz += v[0];
         }
       }
       for (int mm = 1; mm < nch; mm <<= 1) dz += __shfl_xor(dz, mm);
@@ -1475,9 +1516,14 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
 // d sigma, d gamma, d alpha from the per-block partials, by one workgroup in a fixed order
 // (deterministic): blocks b, b + 256, ... per thread (four blocks' loads in flight per step: the
 // latency chain of one load per step cost ~6 us), then the waves' xor-shuffle sums, then the
-// four waves in order.  red: 16 floats of LDS.
+// four waves in order.  red: 16 floats of LDS.  coherent (the fused reduction's last workgroup):
+// device-scope loads, read at the coherence point the partials' exchanges were performed at.
+PR_DEV float load_partial(const float* src, bool coherent) {
+  return coherent ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *src;
+}
+
 PR_DEV void finalize_scalars(const float* partials, int nblk, const PRBlendParams& p, int has_rast, float* out,
-                             float* red) {
+                             float* red, bool coherent = false) {
   const int tid = threadIdx.x;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   int b = tid;
@@ -1486,7 +1532,7 @@ PR_DEV void finalize_scalars(const float* partials, int nblk, const PRBlendParam
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) v[u][c] = partials[(int64_t)(b + u * kThreads) * 4 + c];
+      for (int c = 0; c < 4; ++c) v[u][c] = load_partial(partials + (int64_t)(b + u * kThreads) * 4 + c, coherent);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -1494,7 +1540,7 @@ PR_DEV void finalize_scalars(const float* partials, int nblk, const PRBlendParam
   }
   for (; b < nblk; b += kThreads) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] += partials[(int64_t)b * 4 + c];
+    for (int c = 0; c < 4; ++c) acc[c] += load_partial(partials + (int64_t)b * 4 + c, coherent);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1)
@@ -1537,8 +1583,8 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
   if (a.sync) {
     __shared__ float red[16];
     __shared__ int flag;
-    if (last_arrival(a.sync, (int)gridDim.x, &flag)) {
-      finalize_scalars(partials, nblk, a.p, RAST ? 1 : 0, a.grad_scalars, red);
+    if (last_arrival(a.sync, (int)gridDim.x, &flag, g.sync_rel != 0)) {
+      finalize_scalars(partials, nblk, a.p, RAST ? 1 : 0, a.grad_scalars, red, true);
       sync_zero(a.sync);
     }
   }
@@ -1880,6 +1926,10 @@ Geo make_geo(const PRBlendParams& p, int PB, bool bwd) {
   g.pmW = p.W;
   g.pmA = g.pm && g.pmNBI % p.W == 0 ? ((int)(0.6180339887 * p.W) | 1) % p.W : 0;
   if (g.pm) g.bpi = 0;  // balanced blocks: no dispatch order to choose
+  // fused scalar reduction's arrivals: relaxed (default) or acq_rel (PR_BLEND_SYNC_ORDER=release;
+  // read per call: tests compare both in one process)
+  const char* so = getenv("PR_BLEND_SYNC_ORDER");
+  g.sync_rel = so && so[0] == 'r';
   return g;
 }
 

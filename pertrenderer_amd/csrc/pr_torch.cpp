@@ -138,14 +138,30 @@ Tensor workspace(size_t bytes, const Tensor& like) {
   return at::empty({static_cast<int64_t>(bytes > 0 ? bytes : 1)}, like.options().dtype(at::kByte));
 }
 
-Tensor saved(AutogradContext* ctx, const char* key) {
-  auto it = ctx->saved_data.find(key);
-  return it == ctx->saved_data.end() || it->second.isNone() ? Tensor() : it->second.toTensor();
-}
+// Tensors a node keeps for its backward go through save_for_backward -- released when the
+// backward has run (CppNode::release_variables), version-checked against in-place changes, and a
+// second backward without retain_graph raises -- while saved_data holds only each one's index.
+struct Keep {
+  AutogradContext* ctx;
+  std::vector<Tensor> ts;
+  explicit Keep(AutogradContext* c) : ctx(c) {}
+  void operator()(const char* key, const Tensor& t) {
+    ctx->saved_data[key] = static_cast<int64_t>(ts.size());
+    ts.push_back(t);  // (undefined tensors are allowed)
+  }
+  void commit() { ctx->save_for_backward(ts); }
+};
 
-void keep(AutogradContext* ctx, const char* key, const Tensor& t) {
-  ctx->saved_data[key] = t.defined() ? c10::IValue(t) : c10::IValue();
-}
+struct Saved {
+  AutogradContext* ctx;
+  variable_list v;
+  explicit Saved(AutogradContext* c) : ctx(c), v(c->get_saved_variables()) {}
+  Tensor operator()(const char* key) const {
+    auto it = ctx->saved_data.find(key);
+    if (it == ctx->saved_data.end() || !it->second.isInt()) return Tensor();
+    return v.at(static_cast<size_t>(it->second.toInt()));
+  }
+};
 
 // torch.autograd.function.once_differentiable: with create_graph the returned gradients carry a
 // node that refuses a second differentiation instead of silently being constants
@@ -176,9 +192,19 @@ variable_list once(const variable_list& grads_in, variable_list out) {
 // brings their gradients to the host.  The blend's backward records an event after the kernels
 // that write its (3,) gradient buffer; the link's backward (reached after the rasterizer's backward
 // is launched: it was created before the rasterizer) waits for that event only, on a side stream.
+// Pending entries are keyed by the buffer's address and hold a weak reference to the tensor that
+// was marked: a lookup whose tensor is not that one (a freed gradient's address reused, e.g. by a
+// summed gradient when the link output feeds two consumers) takes the synchronous copy instead of
+// waiting on a stale event.
+using WeakImpl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>;
+struct Pending {
+  int dev;
+  hipEvent_t event;
+  WeakImpl impl;
+};
 struct Ready {
   std::mutex mu;
-  std::unordered_map<const void*, std::pair<int, hipEvent_t>> pending;  // buffer -> (device, event)
+  std::unordered_map<const void*, Pending> pending;  // buffer -> (device, event, tensor)
   std::unordered_map<int, std::vector<hipEvent_t>> free;
   std::unordered_map<int, std::pair<hipStream_t, float*>> side;  // device -> side stream, pinned (4,)
 };
@@ -204,13 +230,17 @@ void mark_ready(const Tensor& buf, void* stream) {
   if (hipEventRecord(e, static_cast<hipStream_t>(stream)) != hipSuccess)
     throw std::runtime_error("pr_torch: hipEventRecord failed");
   std::lock_guard<std::mutex> lk(r.mu);
-  auto old = r.pending.find(buf.data_ptr());
-  if (old != r.pending.end()) r.free[old->second.first].push_back(old->second.second);
-  if (r.pending.size() > 256) {  // links whose backward never ran (grad taken w.r.t. other inputs): recycle
-    for (auto& kv : r.pending) r.free[kv.second.first].push_back(kv.second.second);
-    r.pending.clear();
+  // links whose backward never ran (grad taken w.r.t. other inputs) leave entries whose tensor is
+  // gone: recycle those (and an entry at this address)
+  for (auto it = r.pending.begin(); it != r.pending.end();) {
+    if (it->first == buf.data_ptr() || it->second.impl.expired()) {
+      r.free[it->second.dev].push_back(it->second.event);
+      it = r.pending.erase(it);
+    } else {
+      ++it;
+    }
   }
-  r.pending[buf.data_ptr()] = {dev, e};
+  r.pending.emplace(buf.data_ptr(), Pending{dev, e, WeakImpl(buf.getIntrusivePtr())});
 }
 
 // g (3,) float on the device -> CPU (3,) float, waiting only for the event recorded for g
@@ -224,7 +254,12 @@ Tensor host_copy(const Tensor& g) {
     std::lock_guard<std::mutex> lk(r.mu);
     auto it = r.pending.find(g.data_ptr());
     if (it != r.pending.end()) {
-      e = it->second.second;
+      auto live = it->second.impl.lock();
+      if (live.get() == g.unsafeGetTensorImpl()) {
+        e = it->second.event;
+      } else {  // another tensor at a recycled address: its writer is unknown, copy synchronously
+        r.free[it->second.dev].push_back(it->second.event);
+      }
       r.pending.erase(it);
     }
     auto s = r.side.find(dev);
@@ -315,14 +350,16 @@ struct SO3ExpFn : public torch::autograd::Function<SO3ExpFn> {
     a.R = ptr<float>(R);
     at::DeviceGuard dg(w.device());
     check(api().so3_exp_fwd(&a, stream_of(w)), "pr_so3_exp_fwd");
-    keep(ctx, "w", w);
+    Keep k(ctx);
+    k("w", w);
+    k.commit();
     ctx->saved_data["eps"] = eps;
     return R;
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    auto w = saved(ctx, "w");
     if (!grads[0].defined()) return {Tensor(), Tensor()};
+    auto w = Saved(ctx)("w");
     auto g = dense(grads[0], at::kFloat);
     auto gw = at::empty_like(w);
     PRSO3Args a{};
@@ -352,14 +389,17 @@ struct RotateFn : public torch::autograd::Function<RotateFn> {
     a.out = ptr<float>(out);
     at::DeviceGuard dg(p.device());
     check(api().rotate_fwd(&a, stream_of(out)), "pr_rotate_fwd");
-    keep(ctx, "p", p);
-    keep(ctx, "r", r);
+    Keep k(ctx);
+    k("p", p);
+    k("r", r);
+    k.commit();
     return out;
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    auto p = saved(ctx, "p"), r = saved(ctx, "r");
     if (!grads[0].defined()) return {Tensor(), Tensor()};
+    const Saved sv(ctx);
+    auto p = sv("p"), r = sv("r");
     auto g = dense(grads[0], at::kFloat);
     Tensor gp = ctx->needs_input_grad(0) ? at::empty_like(p) : Tensor();
     Tensor gr = ctx->needs_input_grad(1) ? at::empty_like(r) : Tensor();
@@ -465,18 +505,21 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
     a.workspace = ws.data_ptr();
     a.workspace_bytes = static_cast<size_t>(ws.numel());
     check(api().project_rast_fwd(&pa, &a, stream_of(v)), "pr_project_rast_fwd");
-    ctx->save_for_backward({p2f, counts});
-    keep(ctx, "v", v);
-    keep(ctx, "f", f);
-    keep(ctx, "first", first);
-    keep(ctx, "nfaces", nfaces);
-    keep(ctx, "m1", m1);
-    keep(ctx, "m2", m2);
-    keep(ctx, "fv", fv);
-    keep(ctx, "gfv", gfv);
-    keep(ctx, "gv", gv);
-    keep(ctx, "csr_start", csr_start.has_value() ? *csr_start : Tensor());
-    keep(ctx, "csr_corners", csr_corners.has_value() ? *csr_corners : Tensor());
+    Keep k(ctx);
+    k("p2f", p2f);
+    k("counts", counts);
+    k("v", v);
+    k("f", f);
+    k("first", first);
+    k("nfaces", nfaces);
+    k("m1", m1);
+    k("m2", m2);
+    k("fv", fv);
+    k("gfv", gfv);
+    k("gv", gv);
+    k("csr_start", cs);
+    k("csr_corners", cc);
+    k.commit();
     ctx->saved_data["cfg"] = cfg;
     ctx->saved_data["blur"] = blur;
     ctx->saved_data["prezeroed"] = true;
@@ -487,12 +530,12 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     variable_list out(11);
-    auto gfv = saved(ctx, "gfv"), gv = saved(ctx, "gv");
+    const Saved sv(ctx);
+    auto gfv = sv("gfv"), gv = sv("gv");
     if (!gfv.defined()) return out;
-    auto sv = ctx->get_saved_variables();
-    auto p2f = sv[0], counts = sv[1];
-    auto v = saved(ctx, "v"), f = saved(ctx, "f"), first = saved(ctx, "first"), nfaces = saved(ctx, "nfaces");
-    auto m1 = saved(ctx, "m1"), m2 = saved(ctx, "m2"), fv = saved(ctx, "fv");
+    auto p2f = sv("p2f"), counts = sv("counts");
+    auto v = sv("v"), f = sv("f"), first = sv("first"), nfaces = sv("nfaces");
+    auto m1 = sv("m1"), m2 = sv("m2"), fv = sv("fv");
     auto cfg = ctx->saved_data["cfg"].toIntVector();
     // a second backward (retain_graph) finds the accumulators used: zero them again
     const int32_t flags = ctx->saved_data["prezeroed"].toBool() ? PR_GRAD_PREZEROED : 0;
@@ -523,7 +566,7 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
     pa.grad_face_verts = ptr<float>(gfv);
     pa.grad_verts = ptr<float>(gv);
     pa.flags = flags;
-    auto cs = saved(ctx, "csr_start"), cc = saved(ctx, "csr_corners");
+    auto cs = sv("csr_start"), cc = sv("csr_corners");
     pa.vert_corner_start = ptr<int64_t>(cs);
     pa.vert_corners = ptr<int64_t>(cc);
     check(api().project_bwd(&pa, st), "pr_project_bwd");
@@ -610,7 +653,9 @@ struct BlendFn : public torch::autograd::Function<BlendFn> {
                            "winners", "cache", "plan", "sync", "s0", "s1", "s2"};
     const Tensor ts[] = {p2f_c, d_c, z_c, c_c, v_c, f_c, counts, znear, zfar, noise_r, noise_a, seeds,
                          winners, cache, plan, sync, sigma, gamma, alpha};
-    for (size_t i = 0; i < sizeof(ts) / sizeof(ts[0]); ++i) keep(ctx, names[i], ts[i]);
+    Keep k(ctx);
+    for (size_t i = 0; i < sizeof(ts) / sizeof(ts[0]); ++i) k(names[i], ts[i]);
+    k.commit();
     return image;
   }
 
@@ -626,8 +671,9 @@ struct BlendFn : public torch::autograd::Function<BlendFn> {
     const bool vertex = (p.flags & PR_BLEND_VERTEX) != 0;
     const int64_t need = ctx->saved_data["need"].toInt();
     auto needs = [need](int i) { return ((need >> i) & 1) != 0; };
-    auto p2f = saved(ctx, "p2f"), d = saved(ctx, "d"), z = saved(ctx, "z"), c = saved(ctx, "c");
-    auto v = saved(ctx, "v"), f = saved(ctx, "f");
+    const Saved sv(ctx);
+    auto p2f = sv("p2f"), d = sv("d"), z = sv("z"), c = sv("c");
+    auto v = sv("v"), f = sv("f");
     auto g = dense(grads[0], at::kFloat);
     auto gd = at::empty_like(d), gz = at::empty_like(z), gc = at::empty_like(c);
     Tensor gv = vertex && needs(3) ? at::zeros_like(v) : Tensor();
@@ -647,15 +693,15 @@ struct BlendFn : public torch::autograd::Function<BlendFn> {
       a.colors = ptr<float>(c);
       a.grad_colors = ptr<float>(gc);
     }
-    a.winners = ptr<uint8_t>(saved(ctx, "winners"));
+    a.winners = ptr<uint8_t>(sv("winners"));
     a.grad_image = ptr<float>(g);
-    a.rast_cache = ptr<float>(saved(ctx, "cache"));
+    a.rast_cache = ptr<float>(sv("cache"));
     a.grad_dists = ptr<float>(gd);
     a.grad_zbuf = ptr<float>(gz);
     a.grad_scalars = ptr<float>(gsc);
-    a.pix_count = ptr<int32_t>(saved(ctx, "counts"));
-    a.plan = ptr<int32_t>(saved(ctx, "plan"));
-    a.sync = ptr<int32_t>(saved(ctx, "sync"));
+    a.pix_count = ptr<int32_t>(sv("counts"));
+    a.plan = ptr<int32_t>(sv("plan"));
+    a.sync = ptr<int32_t>(sv("sync"));
     at::DeviceGuard dg(d.device());
     auto ws = workspace(api().blend_bwd_workspace_size(&a), d);
     a.workspace = ws.data_ptr();
@@ -669,7 +715,7 @@ struct BlendFn : public torch::autograd::Function<BlendFn> {
     // the smoothing scalars (blend.py _scalar_grads): CPU leaves get their three values in ONE copy
     Tensor host;
     for (int i = 0; i < 3; ++i) {
-      auto ref = saved(ctx, i == 0 ? "s0" : i == 1 ? "s1" : "s2");
+      auto ref = sv(i == 0 ? "s0" : i == 1 ? "s1" : "s2");
       if (!needs(4 + i) || !ref.defined()) continue;
       if (ref.device().is_cpu()) {
         if (!host.defined()) host = gsc.to(at::kCPU);
@@ -754,12 +800,14 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
     a.colors = ptr<float>(colors);
     at::DeviceGuard dg(colors.device());
     check(api().shade_fwd(&a, stream_of(colors)), "pr_shade_fwd");
-    for (int i = 0; i < 6; ++i) keep(ctx, kShadeKeys[i], t[i]);
-    for (int i = 0; i < 6; ++i) keep(ctx, kShadeRows[i], rows[i]);
-    keep(ctx, "p2f", p2f_c);
-    keep(ctx, "counts", counts);
-    keep(ctx, "faces", faces);
-    keep(ctx, "face_uvs", face_uvs);
+    Keep k(ctx);
+    for (int i = 0; i < 6; ++i) k(kShadeKeys[i], t[i]);
+    for (int i = 0; i < 6; ++i) k(kShadeRows[i], rows[i]);
+    k("p2f", p2f_c);
+    k("counts", counts);
+    k("faces", faces);
+    k("face_uvs", face_uvs);
+    k.commit();
     ctx->saved_data["mode"] = mode;
     ctx->saved_data["directional"] = directional;
     return colors;
@@ -768,13 +816,14 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     variable_list out(13);
     if (!grads[0].defined()) return out;
+    const Saved sv(ctx);
     Tensor t[6], rows[6];
-    for (int i = 0; i < 6; ++i) t[i] = saved(ctx, kShadeKeys[i]);
-    for (int i = 0; i < 6; ++i) rows[i] = saved(ctx, kShadeRows[i]);
+    for (int i = 0; i < 6; ++i) t[i] = sv(kShadeKeys[i]);
+    for (int i = 0; i < 6; ++i) rows[i] = sv(kShadeRows[i]);
     const int64_t mode = ctx->saved_data["mode"].toInt();
     auto g = dense(grads[0], at::kFloat);
     PRShadeArgs a{};
-    shade_common(a, saved(ctx, "p2f"), saved(ctx, "counts"), saved(ctx, "faces"), saved(ctx, "face_uvs"), t, rows,
+    shade_common(a, sv("p2f"), sv("counts"), sv("faces"), sv("face_uvs"), t, rows,
                  mode, ctx->saved_data["directional"].toBool());
     a.grad_colors = ptr<float>(g);
     for (int i = 0; i < 6; ++i) out[i] = ctx->needs_input_grad(i) ? at::empty_like(t[i]) : Tensor();
@@ -824,19 +873,22 @@ struct VertNormalsFn : public torch::autograd::Function<VertNormalsFn> {
     a.vert_corners = ptr<int64_t>(cc);
     at::DeviceGuard dg(v.device());
     check(api().vert_normals_fwd(&a, stream_of(v)), "pr_vert_normals_fwd");
-    keep(ctx, "v", v);
-    keep(ctx, "f", f);
-    keep(ctx, "raw", raw);
-    keep(ctx, "cs", cs);
-    keep(ctx, "cc", cc);
+    Keep k(ctx);
+    k("v", v);
+    k("f", f);
+    k("raw", raw);
+    k("cs", cs);
+    k("cc", cc);
+    k.commit();
     return n;
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     variable_list out(4);
     if (!grads[0].defined()) return out;
-    auto v = saved(ctx, "v"), f = saved(ctx, "f"), raw = saved(ctx, "raw");
-    auto cs = saved(ctx, "cs"), cc = saved(ctx, "cc");
+    const Saved sv(ctx);
+    auto v = sv("v"), f = sv("f"), raw = sv("raw");
+    auto cs = sv("cs"), cc = sv("cc");
     auto g = dense(grads[0], at::kFloat);
     auto graw = at::empty_like(v), gv = at::empty_like(v);
     PRNormalsArgs a{};

@@ -2,12 +2,12 @@
 the consecutive blocks) against the consecutive layout.
 
 Every pixel is computed from its own fragments with Philox counters keyed by its physical index,
-so the forward image must be bitwise equal in both layouts.  The backward's per-slot gradients
-are equal up to summation order (1e-5 of their scale): B6 splits a slot's sample groups over
-nch lanes, nch chosen from the pass's entry count (a light block of the consecutive layout uses
-more lanes per entry than an interleaved one), so the d z sums of those pixels regroup.  The
-smoothing scalars' gradients are per-block partial sums reduced in another grouping (1e-5), and
-the vertex-colour gradient is a float-atomic scatter (1e-5 of its scale).  Cases: the bench frame
+so the forward image must be bitwise equal in both layouts, and so must the backward's per-slot
+gradients: B6 splits a slot's sample groups over nch lanes (nch chosen from the pass's entry
+count, which differs between the layouts), but sums them in one canonical order (a pairwise tree
+over the group index) whatever the split.  The smoothing scalars' gradients are per-block partial
+sums reduced in another grouping, and the vertex-colour gradient is a float-atomic scatter: those
+two compare at conftest.assert_close (1e-5 elementwise relative).  Cases: the bench frame
 at 128^2 (vertex colours, Gaussian pair with and without variance reduction), a batch of two
 frames whose blocks must keep to their own image (texel colours, scattered valid prefixes,
 per-image planes), a shape whose pixel count is no multiple of the block (layout off: identical),
@@ -19,6 +19,7 @@ import pytest
 import torch
 
 import pertrenderer_amd as pa
+from conftest import assert_close
 from pertrenderer_amd.blend import Noise, perturbed_aggregate
 
 pytestmark = pytest.mark.gpu
@@ -39,8 +40,7 @@ def _with(value, fn):
 def _compare(a, b, names, loose):
     for x, y, n in zip(a, b, names):
         if n in loose:
-            tol = 1e-5 * max(float(y.abs().max()), 1e-30)
-            assert float((x - y).abs().max()) <= tol, n
+            assert_close(x, y, rtol=2e-5 if x.dim() == 0 else 1e-5, name=n)
         else:
             assert torch.equal(x, y), n
 
@@ -76,7 +76,7 @@ def test_interleaved_blocks_bench_frame(device, agg_vr):
     b = _with("0", run)
     assert int((a[1] != 0).sum()) > 1000  # the frame has real coverage
     _compare(a, b, ("image", "d dists", "d zbuf", "d bary", "d vertex colours", "d sigma", "d gamma", "d alpha"),
-             loose=("d dists", "d zbuf", "d bary", "d vertex colours", "d sigma", "d gamma", "d alpha"))
+             loose=("d vertex colours", "d sigma", "d gamma", "d alpha"))
 
 
 def _frags(device, N, H, W, K, seed):
@@ -110,7 +110,7 @@ def test_interleaved_blocks_texel_batch(device, N, H, W, K):
     a = _with("1", run)
     b = _with("0", run)
     _compare(a, b, ("image", "d dists", "d zbuf", "d colours", "d sigma", "d gamma", "d alpha"),
-             loose=("d dists", "d zbuf", "d colours", "d sigma", "d gamma", "d alpha"))
+             loose=("d sigma", "d gamma", "d alpha"))
 
 
 def test_interleaved_blocks_aggregate(device):
@@ -130,13 +130,14 @@ def test_interleaved_blocks_aggregate(device):
         return [Wt.detach(), prob.grad, z.grad, gam.grad, alp.grad]
     a = _with("1", run)
     b = _with("0", run)
-    _compare(a, b, ("weights", "d prob", "d zbuf", "d gamma", "d alpha"), loose=("d prob", "d zbuf", "d gamma", "d alpha"))
+    _compare(a, b, ("weights", "d prob", "d zbuf", "d gamma", "d alpha"), loose=("d gamma", "d alpha"))
 
 
 def test_default_layout_on_a_batch_grid(device):
     """The default on a batch grid (5 x 256^2, backward grid > 8192 blocks): consecutive forward,
     interleaved backward -- the forward's winners and rast cache are read by physical pixel / slot,
-    so the mixed pair equals the consecutive one (image bitwise, gradients to summation order)."""
+    so the mixed pair equals the consecutive one (image and per-slot gradients bitwise, the
+    smoothing scalars to the per-block partials' grouping)."""
     p2f, d0, z0, c0 = _frags(device, 5, 256, 256, 8, seed=21)
 
     def run():
@@ -156,4 +157,4 @@ def test_default_layout_on_a_batch_grid(device):
             os.environ["PR_BLEND_INTERLEAVE"] = old
     b = _with("0", run)
     _compare(a, b, ("image", "d dists", "d zbuf", "d colours", "d sigma", "d gamma", "d alpha"),
-             loose=("d dists", "d zbuf", "d colours", "d sigma", "d gamma", "d alpha"))
+             loose=("d sigma", "d gamma", "d alpha"))

@@ -80,7 +80,35 @@ prof() {
   python tools/rocprof_summary.py "$f" "$OUT/rocprof_kernels_$tag.json" "rocprofv3 --kernel-trace --stats -- python bench.py $*"
 }
 
+dense() {  # SURVEY §8(d) dense-fragment blend microbench: rocprofv3 stats + PMC passes
+  local tag="$1"
+  (cd /tmp && export TMPDIR=/tmp
+   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/dense_$tag" -o prof -- \
+     python "$R/tools/kprof.py" --dense --iters 40 > "$OUT/dense_$tag.log" 2>&1) || { tail -5 "$OUT/dense_$tag.log"; return 1; }
+  local f; f=$(find "$OUT/dense_$tag" -name "*kernel_stats.csv" | sort | sed -n 1p)
+  python tools/rocprof_summary.py "$f" "$OUT/rocprof_dense_$tag.json" \
+    "rocprofv3 --kernel-trace --stats -- python tools/kprof.py --dense --iters 40" || return 1
+  pmc "pmcdense_$tag" --dense
+}
+
+sel() {  # selected GPU test files: sel TAG FILE...
+  local tag="$1"; shift
+  timeout -k 10 900 python -u -m pytest "$@" -q -m gpu --timeout 240 --timeout-method thread -p no:cacheprovider \
+    > "$OUT/tests_$tag.log" 2>&1
+  local rc=$?; grep -E "^(FAILED|ERROR)|passed|failed" "$OUT/tests_$tag.log" | tail -15; return $rc
+}
+
+kernels() {  # per-step kernel list with the issuing call (tools/step_kernels.py)
+  local tag="$1"; shift
+  timeout -k 10 300 python tools/step_kernels.py --json "$OUT/step_kernels_$tag.json" "$@" > "$OUT/step_kernels_$tag.txt" 2>&1 \
+    || { tail -5 "$OUT/step_kernels_$tag.txt"; return 1; }
+  tail -1 "$OUT/step_kernels_$tag.txt"
+}
+
 case "$CMD" in
+  dense) dense "${1:-d}" ;;
+  sel) sel "$@" ;;
+  kernels) kernels "$@" ;;
   tests) tests "${1:-t}" ;;
   quick) tests "${1:-q}" && bench "${1:-q}" --no-cpu-baseline ;;
   bench) bench "$@" ;;
