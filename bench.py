@@ -11,13 +11,15 @@ pose (lr 5e-2, eval.py:337).  The whole step is one captured HIP graph.
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
 Multi-GPU (--shard):
-  frames  (default at N > 1, weak scaling): every rank renders its OWN view of the shared pose
-          (camera azimuth 120 + 360 r / N: a multi-view pose optimisation step) and one RCCL
-          all-reduce averages the pose / smoothing gradients.  value = distinct frames / s.
-  samples (strong scaling): every rank renders the same frame with its shard of the config's
-          Monte-Carlo samples (parallel.sample_shard: global sample offsets, shared Philox keys)
-          and the all-reduce forms the full-S gradient estimate (weights n_r / S).  value =
-          distinct frames / s (each frame counted once).
+  samples (default at N > 1, the north star's partition, strong scaling): every rank renders the
+          same frame with its shard of the config's Monte-Carlo samples (parallel.sample_shard:
+          global sample offsets, shared Philox keys) and one RCCL all-reduce forms the full-S
+          gradient estimate (weights n_r / S).  value = distinct frames / s (each frame counted
+          once).  The rasterizer and pose kernels are replicated on every rank: the line reports
+          their per-rank time ("strong_scaling": replicated vs sharded ms, and the speed-up bound).
+  frames  (weak scaling): every rank renders its OWN view of the shared pose (camera azimuth
+          120 + 360 r / N: a multi-view pose optimisation step) and one RCCL all-reduce averages
+          the pose / smoothing gradients.  value = distinct frames / s.
 
 Prints ONE JSON line on rank 0: `value` = frames/s (forward + backward per frame) over all
 ranks; `ms_forward` / `ms_backward` = HIP events around separately captured forward and
@@ -429,8 +431,8 @@ def main():
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
                     help="BASELINE.json configuration (cfg2 = the metric's headline workload)")
-    ap.add_argument("--shard", choices=["frames", "samples"], default="frames",
-                    help="N > 1: distinct views per rank (weak) or the Monte-Carlo samples (strong)")
+    ap.add_argument("--shard", choices=["frames", "samples"], default="samples",
+                    help="N > 1: the Monte-Carlo samples (strong, default) or distinct views per rank (weak)")
     ap.add_argument("--image-size", type=int, default=None)
     ap.add_argument("--faces-per-pixel", type=int, default=None)
     ap.add_argument("--samples", type=int, default=None, help="Monte-Carlo samples (global in --shard samples)")
@@ -618,6 +620,16 @@ def main():
                   "peak_normals_per_s": RNG_PEAK_NORMALS_PER_S * world,
                   "frac": round(normals * args.steps / elapsed / (RNG_PEAK_NORMALS_PER_S * world), 4),
                   "peak_from": "tools/philox_bench.hip on one MI355X: 511 G Philox blocks/s x 4 normals"}
+    if shard == "samples":
+        # strong scaling: the rasterizer (and the tiny pose kernels) run in full on every rank, the
+        # blend on this rank's sample shard; T(N) >= T_rep + T_shard(1) / N bounds the speed-up
+        rep_ms = sum(kern[k].get("kernel_ms", kern[k]["ms"]) for k in ("rast_fwd", "rast_bwd") if k in kern)
+        sh_ms = sum(kern[k].get("kernel_ms", kern[k]["ms"]) for k in ("blend_fwd", "blend_bwd") if k in kern)
+        out["strong_scaling"] = {
+            "replicated_ms_per_rank": round(rep_ms, 4), "sharded_ms_per_rank": round(sh_ms, 4),
+            "speedup_bound_vs_1gpu": round((rep_ms + sh_ms * world) / rep_ms, 2) if rep_ms > 0 else None,
+            "from": "this rank's kernel events (rast_fwd + rast_bwd replicated; blend_fwd + blend_bwd over "
+                    f"{S_local} of {S} agg samples)"}
     if note:
         out["note"] = note
     if rank == 0 and world == 1 and not args.no_dense and args.config != "eval":

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 15
+#define PR_ABI_VERSION 16
 
 /* error codes */
 #define PR_OK 0
@@ -249,6 +249,12 @@ typedef struct PRProjectArgs {
   /* per vertex: deterministic, no atomics.  Else one float atomic per corner component.         */
   const int64_t* vert_corner_start; /* (V+1) */
   const int64_t* vert_corners;      /* (3F) */
+  /* nullable: deferred noise-key advances (ABI 16).  pr_project_rast_fwd's face pass applies     */
+  /* pr_seed_advance's update to seed_advance[0], seed_advance_n times, before it returns: the    */
+  /* caller's per-step key advance (pertrenderer_amd.noise.DeviceSeed) rides on the step's first  */
+  /* native kernel instead of a launch of its own.  Ignored by pr_project_fwd / pr_project_bwd.   */
+  uint64_t* seed_advance;
+  int32_t seed_advance_n;
 } PRProjectArgs;
 
 /* Phong shading of every fragment slot: PyTorch3D 0.4.0 phong_shading (+ the texel lookup of

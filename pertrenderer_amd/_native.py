@@ -90,7 +90,8 @@ class PRProjectArgs(C.Structure):
     _fields_ = [("verts", _vp), ("faces", _vp), ("mesh_first_face", _vp), ("mesh_num_faces", _vp),
                 ("world_to_view", _vp), ("proj", _vp), ("V", C.c_int64), ("F", C.c_int64), ("N", C.c_int32),
                 ("face_verts", _vp), ("grad_face_verts", _vp), ("grad_verts", _vp), ("flags", C.c_int32),
-                ("vert_corner_start", _vp), ("vert_corners", _vp)]
+                ("vert_corner_start", _vp), ("vert_corners", _vp), ("seed_advance", _vp),
+                ("seed_advance_n", C.c_int32)]
 
 
 class PRSO3Args(C.Structure):
@@ -160,7 +161,7 @@ EXPORTS = {
     "pr_vert_normals_fwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
     "pr_vert_normals_bwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
 }
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _lib = None
 

@@ -86,6 +86,15 @@ PR_DEV U4 philox_block(uint64_t seed, uint32_t pixel, uint32_t slot, uint32_t gr
 // k-th index of [0, n) in centre-out order (n/2, n/2-1, n/2+1, ...): workgroups over
 // image rows are dispatched from the middle outwards, so the rows of a centred object
 // (the expensive ones) start first and the cheap border rows fill the tail.
+PR_DEV uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// pr_seed_advance's update of a device key base (DeviceSeed.advance)
+PR_DEV uint64_t seed_next(uint64_t s) { return mix64(s + 0x9E3779B97F4A7C15ull); }
+
 PR_DEV int centre_out(int k, int n) { return (k & 1) ? n / 2 - 1 - (k >> 1) : n / 2 + (k >> 1); }
 
 // --------------------------------------------------------------------- math

@@ -1727,6 +1727,12 @@ __global__ void project_fwd_kernel(PRProjectArgs a) {
 __global__ void project_prep_kernel(PRProjectArgs a, float blur, int cull_backfaces, FaceRec* recs, uint2* bbox,
                                     float* zero_fv, float* zero_v, BinGrid bins) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (a.seed_advance && blockIdx.x == 0 && threadIdx.x == 0) {  // the caller's deferred key advances
+    const unsigned i = threadIdx.x;  // (lane-indexed: a vector store)
+    uint64_t s = a.seed_advance[i];
+    for (int k = 0; k < a.seed_advance_n; ++k) s = seed_next(s);
+    a.seed_advance[i] = s;
+  }
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.F; f += stride) {
     const int n = mesh_of(a.mesh_first_face, a.mesh_num_faces, a.N, f);
     float fv[9];
@@ -2062,7 +2068,7 @@ extern "C" int pr_interp_bwd(const PRInterpArgs* args, void* stream) {
 
 static int project_check(const PRProjectArgs* a) {
   if (!a || !a->verts || !a->faces || !a->mesh_first_face || !a->mesh_num_faces || !a->world_to_view || !a->proj ||
-      a->N <= 0 || a->V < 0 || a->F < 0)
+      a->N <= 0 || a->V < 0 || a->F < 0 || a->seed_advance_n < 0 || (a->seed_advance_n > 0 && !a->seed_advance))
     return set_error(PR_ERR_ARG, "project: bad args");
   return PR_OK;
 }
@@ -2112,8 +2118,8 @@ extern "C" int pr_project_rast_fwd(const PRProjectArgs* pa, const PRRastArgs* ra
   if (int e = bins_begin(a, bins, st)) return e;
   const int64_t work = std::max<int64_t>(std::max<int64_t>(a.F, a.grad_face_verts ? a.F * 9 : 0),
                                          pa->grad_verts ? pa->V * 3 : 0);
-  if (work > 0) {
-    const int nb = (int)std::min<int64_t>((work + kThreads - 1) / kThreads, 1024);
+  if (work > 0 || (pa->seed_advance && pa->seed_advance_n > 0)) {
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((work + kThreads - 1) / kThreads, 1024));
     project_prep_kernel<<<nb, kThreads, 0, st>>>(*pa, a.blur_radius, a.cull_backfaces, fr, fbox, a.grad_face_verts,
                                                  pa->grad_verts, bins);
     if (int e = check_launch("project_prep")) return e;

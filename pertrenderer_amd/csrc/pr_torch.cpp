@@ -471,7 +471,7 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
   static variable_list forward(AutogradContext* ctx, Tensor verts, Tensor faces, Tensor first, Tensor nfaces,
                                Tensor w2v, Tensor proj, c10::optional<Tensor> csr_start,
                                c10::optional<Tensor> csr_corners, std::vector<int64_t> cfg, double blur,
-                               bool need) {
+                               bool need, c10::optional<Tensor> seed_adv, int64_t seed_n) {
     if (cfg.size() != 8) throw std::invalid_argument("project_rasterize: cfg must have 8 entries");
     Tensor cs = csr_start.has_value() ? *csr_start : Tensor(), cc = csr_corners.has_value() ? *csr_corners : Tensor();
     on_device({&verts, &faces, &first, &nfaces, &w2v, &proj, &cs, &cc});
@@ -487,6 +487,12 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
     project_common(pa, v, f, first, nfaces, m1, m2);
     pa.face_verts = ptr<float>(fv);
     pa.grad_verts = ptr<float>(gv);
+    const Tensor sa = val(seed_adv);  // the caller's deferred noise-key advances (DeviceSeed)
+    if (sa.defined() && seed_n > 0) {
+      on_device({&sa});
+      pa.seed_advance = static_cast<uint64_t*>(sa.data_ptr());
+      pa.seed_advance_n = static_cast<int32_t>(seed_n);
+    }
     PRRastArgs a{};
     rast_common(a, fv, first, nfaces, cfg, blur);
     auto p2f = empty({N, H, W, K}, at::kLong, v);
@@ -577,11 +583,13 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
 
 variable_list project_rasterize(const Tensor& verts, const Tensor& faces, const Tensor& first, const Tensor& nfaces,
                                 const Tensor& w2v, const Tensor& proj, c10::optional<Tensor> csr_start,
-                                c10::optional<Tensor> csr_corners, std::vector<int64_t> cfg, double blur) {
+                                c10::optional<Tensor> csr_corners, std::vector<int64_t> cfg, double blur,
+                                c10::optional<Tensor> seed_adv, int64_t seed_n) {
   // the forward's gradient accumulators are sized when d verts will be wanted (Python's
   // ctx.needs_input_grad[0]; the C++ context has no edges to ask before the node is executable)
   const bool need = at::GradMode::is_enabled() && verts.requires_grad();
-  return ProjectRasterizeFn::apply(verts, faces, first, nfaces, w2v, proj, csr_start, csr_corners, cfg, blur, need);
+  return ProjectRasterizeFn::apply(verts, faces, first, nfaces, w2v, proj, csr_start, csr_corners, cfg, blur, need,
+                                   seed_adv, seed_n);
 }
 
 // ------------------------------------------------------------------ fused perturbed blend

@@ -78,26 +78,61 @@ class Noise:
 class DeviceSeed:
     """Graph-capturable Philox keys.
 
-    A device-resident 64-bit base is advanced in place by ``advance()``
-    (pr_seed_advance, a stream-ordered kernel that a captured graph replays);
-    every operator call in between gets a distinct stream id, and the kernels
-    key Philox with mix64(base ^ id).  Inside a captured step the ids are baked
-    into the graph while the base changes per replay, so every replay draws
-    fresh noise without any host work."""
+    A device-resident 64-bit base is advanced in place by ``advance()``; every operator call in
+    between gets a distinct stream id, and the kernels key Philox with mix64(base ^ id).  Inside a
+    captured step the ids are baked into the graph while the base changes per replay, so every
+    replay draws fresh noise without any host work.
+
+    The advance is deferred (round 5): ``advance()`` only counts it, and the next native face pass
+    (``MeshRasterizer`` -> pr_project_rast_fwd, PRProjectArgs.seed_advance) applies it in its first
+    thread, so a pose-optimisation step spends no launch of its own on it; any draw from this seed
+    before such a pass (``stream_id``) flushes the pending advances with pr_seed_advance first, so
+    the keys every operator sees are those of the eager update."""
 
     def __init__(self, device, seed=None):
         self.tensor = torch.tensor([draw_key() if seed is None else int(seed)], dtype=torch.int64,
                                    device=device)
         self._next = 1
+        self._pending = 0
 
     def stream_id(self):
+        self.flush()
         i = self._next
         self._next += 1
         return i
 
     def advance(self):
-        nat.call("pr_seed_advance", "pr_seed_advance", self.tensor, nat.ptr(self.tensor), 1)
+        self._pending += 1
         self._next = 1
+
+    def flush(self):
+        """Apply the pending advances now (pr_seed_advance on the current stream)."""
+        while self._pending:
+            nat.call("pr_seed_advance", "pr_seed_advance", self.tensor, nat.ptr(self.tensor), 1)
+            self._pending -= 1
+
+    def take_pending(self, device):
+        """(tensor, n) of the pending advances for a native face pass on `device` to apply (n = 0:
+        none); the caller owns them from here (give_back on failure)."""
+        if not self._pending or self.tensor.device != device:
+            return None, 0
+        n, self._pending = self._pending, 0
+        return self.tensor, n
+
+    def give_back(self, n):
+        self._pending += n
+
+
+def take_pending_advance(device):
+    """The active DeviceSeed's deferred advances for a face pass on `device`: (tensor, n)."""
+    if _DEVICE_SEED is None:
+        return None, 0
+    return _DEVICE_SEED.take_pending(device)
+
+
+def give_back_advance(n):
+    if n and _DEVICE_SEED is not None:
+        _DEVICE_SEED.give_back(n)
 
 
 _DEVICE_SEED = None

@@ -15,6 +15,7 @@ import torch
 
 from .. import _native as nat
 from .. import host_layer
+from .. import noise as noise_mod
 from .. import timing as _timing
 from .mesh import gather_faces
 from .project import project_faces
@@ -170,7 +171,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, verts, faces, first, nfaces, w2v, proj, H, W, K, blur, persp, clip, cull, bins=(0, 0),
-                csr_start=None, csr_corners=None):
+                csr_start=None, csr_corners=None, seed_adv=None, seed_n=0):
         from .project import _per_mesh
         nat.require_device(verts, faces, first, nfaces, w2v, proj)
         lib = nat.load()
@@ -187,6 +188,8 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         pa.world_to_view, pa.proj = nat.ptr(m1), nat.ptr(m2)
         pa.V, pa.F, pa.N = v.shape[0], F, N
         pa.face_verts, pa.grad_verts = nat.ptr(fv), nat.ptr(gv)
+        if seed_adv is not None and seed_n > 0:  # the caller's deferred noise-key advances (DeviceSeed)
+            pa.seed_advance, pa.seed_advance_n = nat.ptr(seed_adv), int(seed_n)
         a = nat.PRRastArgs()
         a.face_verts, a.mesh_first_face, a.mesh_num_faces = nat.ptr(fv), nat.ptr(first), nat.ptr(nfaces)
         a.F, a.N, a.H, a.W, a.K = F, N, H, W, K
@@ -221,7 +224,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
     def backward(ctx, gp2f, gzbuf, gbary, gdists, gcounts):
         v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv = ctx.saved_tensors
         if gfv is None:
-            return (None,) * 16
+            return (None,) * 18
         H, W, K, blur, persp, clip, cull = ctx.cfg
         # a second backward (retain_graph) finds the accumulators used: zero them again
         flags = nat.PR_GRAD_PREZEROED if ctx.prezeroed else 0
@@ -254,7 +257,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         pa.grad_face_verts, pa.grad_verts, pa.flags = nat.ptr(gfv), nat.ptr(gv), flags
         pa.vert_corner_start, pa.vert_corners = nat.ptr(ctx.csr[0]), nat.ptr(ctx.csr[1])
         nat.call("pr_project_bwd", "pr_project_bwd", gv, pa)
-        return (gv,) + (None,) * 15
+        return (gv,) + (None,) * 17
 
 
 def rasterize_meshes(meshes, image_size=256, blur_radius=0.0, faces_per_pixel=8, bin_size=None,
@@ -315,18 +318,25 @@ class MeshRasterizer(torch.nn.Module):
             faces = meshes_world.faces_packed()
             bins = bin_params(rs.bin_size, rs.max_faces_per_bin, H, W, faces.shape[0], first.shape[0])
             ext = host_layer.get()
-            if ext is not None:  # the C++ autograd layer (host_layer.py): same kernels and arguments
-                p2f, zbuf, bary, dists, counts = ext.project_rasterize(
-                    meshes_world.verts_packed(), faces, first, nfaces, cameras.world_to_view_matrix(),
-                    cameras.projection_matrix(), *meshes_world.corner_csr("gather"),
-                    [H, W, int(rs.faces_per_pixel), int(bool(rs.perspective_correct)), int(bool(clip)),
-                     int(bool(rs.cull_backfaces)), bins[0], bins[1]], float(rs.blur_radius))
-            else:
-                p2f, zbuf, bary, dists, counts = _ProjectRasterizeFn.apply(
-                    meshes_world.verts_packed(), faces, first, nfaces,
-                    cameras.world_to_view_matrix(), cameras.projection_matrix(), H, W, int(rs.faces_per_pixel),
-                    float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces),
-                    bins, *meshes_world.corner_csr("gather"))
+            verts = meshes_world.verts_packed()
+            # the active DeviceSeed's deferred advance rides on this face pass (noise.DeviceSeed)
+            seed_adv, seed_n = noise_mod.take_pending_advance(verts.device)
+            try:
+                if ext is not None:  # the C++ autograd layer (host_layer.py): same kernels and arguments
+                    p2f, zbuf, bary, dists, counts = ext.project_rasterize(
+                        verts, faces, first, nfaces, cameras.world_to_view_matrix(),
+                        cameras.projection_matrix(), *meshes_world.corner_csr("gather"),
+                        [H, W, int(rs.faces_per_pixel), int(bool(rs.perspective_correct)), int(bool(clip)),
+                         int(bool(rs.cull_backfaces)), bins[0], bins[1]], float(rs.blur_radius), seed_adv, seed_n)
+                else:
+                    p2f, zbuf, bary, dists, counts = _ProjectRasterizeFn.apply(
+                        verts, faces, first, nfaces,
+                        cameras.world_to_view_matrix(), cameras.projection_matrix(), H, W, int(rs.faces_per_pixel),
+                        float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces),
+                        bins, *meshes_world.corner_csr("gather"), seed_adv, seed_n)
+            except BaseException:
+                noise_mod.give_back_advance(seed_n)
+                raise
             return Fragments(pix_to_face=attach_valid_counts(p2f, counts), zbuf=zbuf, bary_coords=bary, dists=dists)
         meshes_screen = self.transform(meshes_world, **kwargs)
         p2f, zbuf, bary, dists = rasterize_meshes(

@@ -20,13 +20,18 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shard", ["frames", "samples"])
-def test_bench_two_ranks_gloo(shard):
+@pytest.mark.parametrize("shard,extra", [("frames", ["--image-size", "128"]), ("samples", ["--image-size", "128"]),
+                                         (None, ["--config", "cfg4", "--batch", "2", "--image-size", "256"])],
+                         ids=["frames", "samples", "default-cfg4-reduced"])
+def test_bench_two_ranks_gloo(shard, extra):
+    """None: bench.py's N > 1 default (--shard samples) on a reduced cfg 4 shape (2 x 256^2 per rank,
+    K = 150, 64 samples split 32 / 32)."""
     env = dict(os.environ, PR_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--steps", "3", "--warmup", "2", "--shard", shard, "--image-size", "128", "--no-cpu-baseline",
-           "--no-dense"]
+           "--steps", "3", "--warmup", "2", "--no-cpu-baseline", "--no-dense"] + extra
+    if shard is not None:
+        cmd += ["--shard", shard]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -34,4 +39,8 @@ def test_bench_two_ranks_gloo(shard):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0 and d["ms_per_step"] > 0
     assert d["scaling"] == ("weak" if shard == "frames" else "strong")
+    if shard != "frames":
+        ss = d["strong_scaling"]
+        assert ss["replicated_ms_per_rank"] > 0 and ss["sharded_ms_per_rank"] > 0 and ss["speedup_bound_vs_1gpu"] > 1
+        assert "sample-parallel x2" in d["config"]["parallelism"]
     assert d["config"]["execution"] == "graph"  # the captured multi-rank step, not the eager fallback

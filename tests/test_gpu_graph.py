@@ -114,3 +114,58 @@ def test_fixed_noise_ignores_device_seed(device):
                 assert not torch.equal(imgs[0], imgs[1])
     finally:
         use_device_seed(None)
+
+
+def _seed_next(s):
+    """pr_seed_advance's update (pr_common.h seed_next) on the host."""
+    m = (1 << 64) - 1
+    z = (s + 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & m
+    z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & m
+    return z ^ (z >> 31)
+
+
+def test_deferred_seed_advance_rides_on_the_face_pass(device):
+    """DeviceSeed.advance() is applied by the next native face pass (MeshRasterizer ->
+    pr_project_rast_fwd, PRProjectArgs.seed_advance), or flushed by a draw before one: either way
+    the keys are those of the eager update, advanced once per call, in graph replays too."""
+    import bench
+    wl = bench.Workload(device, image_size=32, K=8, samples=4)
+    ds = DeviceSeed(device, seed=4321)
+    use_device_seed(ds)
+    try:
+        u = lambda t: int(t.item()) & ((1 << 64) - 1)
+        b0 = u(ds.tensor)
+        ds.advance()
+        ds.advance()  # two pending advances, one face pass
+        assert u(ds.tensor) == b0  # deferred
+        wl.forward()
+        torch.cuda.synchronize()
+        assert ds._pending == 0 and u(ds.tensor) == _seed_next(_seed_next(b0))
+        # a draw with no face pass before it flushes
+        b1 = u(ds.tensor)
+        ds.advance()
+        fr = _frags(device, seed=4)
+        perturbed_blend(fr[3], fr[0], fr[1], fr[2], torch.tensor(1e-3), torch.tensor(1e-2), torch.tensor(1.0), 4, 4)
+        torch.cuda.synchronize()
+        assert ds._pending == 0 and u(ds.tensor) == _seed_next(b1)
+        # captured: every replay advances once, through the face pass
+        wl.device_scalars()
+        graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ds.advance()
+            wl.forward().backward()
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.cuda.graph(graph):
+            ds.advance()
+            wl.forward().backward()
+        assert ds._pending == 0
+        b2 = u(ds.tensor)
+        graph.replay()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert u(ds.tensor) == _seed_next(_seed_next(b2))
+    finally:
+        use_device_seed(None)

@@ -3,9 +3,9 @@ the consecutive blocks) against the consecutive layout.
 
 Every pixel is computed from its own fragments with Philox counters keyed by its physical index,
 so the forward image must be bitwise equal in both layouts, and so must the backward's per-slot
-gradients: B6 splits a slot's sample groups over nch lanes (nch chosen from the pass's entry
-count, which differs between the layouts), but sums them in one canonical order (a pairwise tree
-over the group index) whatever the split.  The smoothing scalars' gradients are per-block partial
+gradients: B6 sums each entry's samples in order on one lane, whatever block holds the pixel
+(rounds 1-4 split light passes' sample groups over several lanes, so the two layouts summed
+some pixels differently).  The smoothing scalars' gradients are per-block partial
 sums reduced in another grouping, and the vertex-colour gradient is a float-atomic scatter: those
 two compare at conftest.assert_close (1e-5 elementwise relative).  Cases: the bench frame
 at 128^2 (vertex colours, Gaussian pair with and without variance reduction), a batch of two
