@@ -77,6 +77,11 @@ extern "C" {
  * reference's backward has no uniform branch and fails (smoothagg.py:64-70), so
  * pr_blend_bwd rejects the flag with PR_ERR_ARG */
 #define PR_BLEND_AGG_UNIFORM 256
+/* Forward only (ABI 16): `winners` (P,Sa) is an INPUT -- the per-sample argmax indices of all Sa
+ * samples, gathered from sample shards (pertrenderer_amd.multidevice) -- instead of the Monte-Carlo
+ * argmax: the same win counts and the same colour mix, so the image is the one-device image bit
+ * for bit.  With !RAST (prob input); no agg noise is read. */
+#define PR_BLEND_WINNERS_IN 512
 
 typedef struct PRBlendParams {
   int32_t N, H, W, K;        /* fragment shape */

@@ -365,22 +365,29 @@ class _FusedBlendFn(torch.autograd.Function):
         zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
         noise = cfg["noise"].to(dev)
         sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
+        prob_in = bool(cfg.get("prob_in"))  # `dists` holds the probabilities (multidevice sample shards)
         p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf,
-                    nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | cfg["vflags"])
+                    (0 if prob_in else nat.PR_BLEND_RAST) | nat.PR_BLEND_COLOR | cfg["vflags"])
         image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
         # per-slot (prob, rast score) kept for the backward instead of regenerating rast noise
         soft = bool(cfg["vflags"] & nat.PR_BLEND_SOFT)
         cache = (torch.empty((N, H, W, K, 2), dtype=F32, device=dev)
-                 if RAST_CACHE and not soft and any(ctx.needs_input_grad[:7]) else None)
+                 if RAST_CACHE and not soft and not prob_in and any(ctx.needs_input_grad[:7]) else None)
         plan = None if soft else _plan(nat.load(), p, cfg["counts"], dev)
         sync = None if soft else _sync(dev)
         a = nat.PRBlendFwdArgs()
         a.p = p
-        a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
+        a.pix_to_face, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(z_c), nat.ptr(c_c)
+        if prob_in:
+            a.prob = nat.ptr(d_c)
+        else:
+            a.dists = nat.ptr(d_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
         a.pix_count, a.plan, a.sync = nat.ptr(cfg["counts"]), nat.ptr(plan), nat.ptr(sync)
         _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
+        if cfg.get("winners_sink") is not None:
+            cfg["winners_sink"].append(winners)
         ctx.save_for_backward(p2f_c, d_c, z_c, c_c, zn, zf, winners, cache, plan, sync)
         ctx.p = p  # the backward's parameter block is the forward's
         ctx.sc_dev = sc_dev
@@ -404,9 +411,13 @@ class _FusedBlendFn(torch.autograd.Function):
         gsc = torch.empty(3, dtype=F32, device=dev)
         a = nat.PRBlendBwdArgs()
         a.p = p
-        a.pix_to_face, a.dists, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c), nat.ptr(c_c)
+        a.pix_to_face, a.zbuf, a.colors = nat.ptr(p2f_c), nat.ptr(z_c), nat.ptr(c_c)
         a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
-        a.grad_dists, a.grad_zbuf, a.grad_colors, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gc), nat.ptr(gsc)
+        a.grad_zbuf, a.grad_colors, a.grad_scalars = nat.ptr(gz), nat.ptr(gc), nat.ptr(gsc)
+        if cfg.get("prob_in"):
+            a.prob, a.grad_prob = nat.ptr(d_c), nat.ptr(gd)
+        else:
+            a.dists, a.grad_dists = nat.ptr(d_c), nat.ptr(gd)
         a.pix_count, a.plan, a.sync = nat.ptr(cfg["counts"]), nat.ptr(plan), nat.ptr(sync)
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
@@ -433,20 +444,28 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
         noise = cfg["noise"].to(dev)
         sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
-        flags = nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | nat.PR_BLEND_VERTEX | cfg["vflags"]
+        prob_in = bool(cfg.get("prob_in"))  # `dists` holds the probabilities (multidevice sample shards)
+        flags = (0 if prob_in else nat.PR_BLEND_RAST) | nat.PR_BLEND_COLOR | nat.PR_BLEND_VERTEX | cfg["vflags"]
         p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf, flags)
         image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
         need = ctx.needs_input_grad
-        cache = torch.empty((N, H, W, K, 2), dtype=F32, device=dev) if RAST_CACHE and any(need[:8]) else None
+        cache = (torch.empty((N, H, W, K, 2), dtype=F32, device=dev)
+                 if RAST_CACHE and not prob_in and any(need[:8]) else None)
         a = nat.PRBlendFwdArgs()
         a.p = p
-        a.pix_to_face, a.dists, a.zbuf = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c)
+        a.pix_to_face, a.zbuf = nat.ptr(p2f_c), nat.ptr(z_c)
+        if prob_in:
+            a.prob = nat.ptr(d_c)
+        else:
+            a.dists = nat.ptr(d_c)
         a.bary, a.faces, a.vert_colors = nat.ptr(b_c), nat.ptr(f_c), nat.ptr(v_c)
         a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
         plan, sync = _plan(nat.load(), p, cfg["counts"], dev), _sync(dev)
         a.pix_count, a.plan, a.sync = nat.ptr(cfg["counts"]), nat.ptr(plan), nat.ptr(sync)
         _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
+        if cfg.get("winners_sink") is not None:
+            cfg["winners_sink"].append(winners)
         ctx.save_for_backward(p2f_c, d_c, z_c, b_c, v_c, f_c, zn, zf, winners, cache, plan, sync)
         ctx.p = p  # the backward's parameter block is the forward's
         ctx.sc_dev = sc_dev
@@ -472,10 +491,14 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         gsc = torch.empty(3, dtype=F32, device=dev)
         a = nat.PRBlendBwdArgs()
         a.p = p
-        a.pix_to_face, a.dists, a.zbuf = nat.ptr(p2f_c), nat.ptr(d_c), nat.ptr(z_c)
+        a.pix_to_face, a.zbuf = nat.ptr(p2f_c), nat.ptr(z_c)
         a.bary, a.faces, a.vert_colors = nat.ptr(b_c), nat.ptr(f_c), nat.ptr(v_c)
         a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
-        a.grad_dists, a.grad_zbuf, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gsc)
+        a.grad_zbuf, a.grad_scalars = nat.ptr(gz), nat.ptr(gsc)
+        if cfg.get("prob_in"):
+            a.prob, a.grad_prob = nat.ptr(d_c), nat.ptr(gd)
+        else:
+            a.dists, a.grad_dists = nat.ptr(d_c), nat.ptr(gd)
         a.grad_bary, a.grad_vert_colors = nat.ptr(gb), nat.ptr(gv)
         a.pix_count, a.plan, a.sync = nat.ptr(cfg["counts"]), nat.ptr(plan), nat.ptr(sync)
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
@@ -484,6 +507,37 @@ class _FusedVertexBlendFn(torch.autograd.Function):
         s_g, g_g, a_g = _scalar_grads(gsc, need[4:7], ctx.refs)
         return (gd if need[0] else None, gz if need[1] else None, gb if need[2] else None, gv,
                 s_g, g_g, a_g, _link_grad(gsc, need[7]), None, None, None, None, None)
+
+
+def image_from_winners(prob, zbuf, colors, p2f, winners, gamma, alpha, eps=1e-10, background=(1.0, 1.0, 1.0),
+                       znear=1.0, zfar=100.0, vert_colors=None, faces=None):
+    """The fused blend's image from given per-sample winners (P, Sa) (PR_BLEND_WINNERS_IN): the win
+    counts and colour mix of the one-device kernel, so a sample-sharded blend whose shards' winners
+    are gathered here gives the one-device image bit for bit.  `colors` are texels (N,H,W,K,3), or
+    with vert_colors / faces the barycentrics (N,H,W,K,3) of the fused TexturesVertex sampling.
+    Forward only (multidevice.sharded_blend routes the gradients through the shards)."""
+    N, H, W, K = p2f.shape
+    dev = p2f.device
+    Sa = winners.shape[1]
+    vertex = vert_colors is not None
+    p2f_c = nat.dense(p2f, torch.int64)
+    pr_c, z_c, c_c, w_c = _contig(prob), _contig(zbuf), _contig(colors), nat.dense(winners, torch.uint8)
+    zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
+    sc, sc_dev = _scalars((1.0, gamma, alpha), dev)
+    flags = nat.PR_BLEND_COLOR | nat.PR_BLEND_WINNERS_IN | (nat.PR_BLEND_VERTEX if vertex else 0)
+    p = _params((N, H, W, K), 1, Sa, sc, sc_dev, float(eps), _background(background), Noise.philox(), zn, zf, flags)
+    image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
+    a = nat.PRBlendFwdArgs()
+    a.p = p
+    a.pix_to_face, a.prob, a.zbuf = nat.ptr(p2f_c), nat.ptr(pr_c), nat.ptr(z_c)
+    if vertex:
+        f_c, v_c = nat.dense(faces, torch.int64), _contig(vert_colors)
+        a.bary, a.faces, a.vert_colors = nat.ptr(c_c), nat.ptr(f_c), nat.ptr(v_c)
+    else:
+        a.colors = nat.ptr(c_c)
+    a.image, a.winners, a.pix_count = nat.ptr(image), nat.ptr(w_c), nat.ptr(_counts_for(p2f))
+    nat.call("pr_blend_fwd", "pr_blend_fwd", image, a)
+    return image
 
 
 def _fused(vertex, dists, zbuf, colors, vert_colors, sigma, gamma, alpha, link, p2f, faces, znear, zfar, cfg):

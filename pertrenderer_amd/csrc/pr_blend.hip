@@ -589,7 +589,7 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
   //      argmax is the background, W_bg = Sa / Sa = 1, alpha = 1 - (empty product) = 0; the
   //      same values the phases below would produce, without them
   if (pcnt && g.empty && uni(EA[bnpix]) == bnpix) {
-    for (int i = tid; i < bnpix * p.Sa; i += kThreads) {
+    for (int i = tid; i < ((p.flags & PR_BLEND_WINNERS_IN) ? 0 : bnpix * p.Sa); i += kThreads) {
       const int pl = i / p.Sa;
       a.winners[(int64_t)GPX[pl] * p.Sa + (i - pl * p.Sa)] = (uint8_t)K;
     }
@@ -785,8 +785,14 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
   __syncthreads();
   PR_BSTAMP(3);
 
-  // ---- 3: Monte-Carlo argmax: thread = (pixel, 4-sample group, candidate stripe c::NC)
-  {
+  // ---- 3: Monte-Carlo argmax: thread = (pixel, 4-sample group, candidate stripe c::NC);
+  //         PR_BLEND_WINNERS_IN: the given winners of every sample counted instead
+  if (p.flags & PR_BLEND_WINNERS_IN) {
+    PR_FOR_SLOTS(p.Sa, g.qS, g.rS, npix * p.Sa) {
+      const int w = a.winners[(int64_t)gpx[pl] * p.Sa + k];
+      atomicAdd(&CNT[ea[pl] - eb + (w == K ? cl[pl] : w)], 1);
+    }
+  } else {
     const int ng = agg_num_groups(p), g0 = agg_first_group(p);
     const int npairs = npix * ng * NC;
     for (int base = 0; base < npairs; base += kThreads) {
@@ -2021,6 +2027,8 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
   if (int e = check_params(a.p, rast)) return e;
   if (!a.pix_to_face && !a.mask) return set_error(PR_ERR_ARG, "blend_fwd: need pix_to_face or mask");
   const int cm = color_mode(a.p.flags);
+  if ((a.p.flags & PR_BLEND_WINNERS_IN) && rast)
+    return set_error(PR_ERR_ARG, "blend_fwd: PR_BLEND_WINNERS_IN takes probabilities (no PR_BLEND_RAST)");
   if (!a.zbuf || !a.winners || (rast && !a.dists) || (!rast && !a.prob) ||
       (cm == 1 && (!a.colors || !a.image)) || (!color && !a.weights) ||
       (cm == 2 && (!a.image || !a.bary || !a.faces || !a.vert_colors || !a.pix_to_face)))

@@ -535,7 +535,7 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    variable_list out(11);
+    variable_list out(13);  // one per forward argument
     const Saved sv(ctx);
     auto gfv = sv("gfv"), gv = sv("gv");
     if (!gfv.defined()) return out;

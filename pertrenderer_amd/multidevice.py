@@ -7,23 +7,28 @@ backend", §8(e) exact mode) for callers that stay one process, as eval.py does 
     # or, with eval.py's source unchanged:  PR_SAMPLE_DEVICES=all python experiments/eval.py
 
 Every ``smooth_rgb_blend`` of a native Monte-Carlo pair (GaussianRast / ArctanRast /
-*_wovr x GaussianAgg / CauchyAgg / *_wovr) then splits its Sr rast and Sa agg samples over
-the devices (``parallel.sample_shard``: global sample indices, one Philox key per operator as
-on one device) and assembles the full-S estimator with in-process collectives:
+*_wovr x GaussianAgg / CauchyAgg / *_wovr), and RandomSimpleShader's fused TexturesVertex blend,
+then splits its Sr rast and Sa agg samples over the devices (``parallel.sample_shard``: global
+sample indices, one Philox key per operator as on one device, host keys or a graph-mode
+``DeviceSeed``) and assembles the full-S estimator with in-process collectives:
 
-  forward : fragments broadcast to the devices; each device's perturbed Heaviside counts
-            over its rast shard are sum-reduced to the primary (P = sum_i n_i/Sr * P_i) and
-            P is broadcast back; each device's perturbed argmax counts over its agg shard are
-            sum-reduced (W); the colour mix and alpha on the primary (random_rasterizer.py:47-54);
-  backward: the adjoints of the same collectives (broadcast <-> sum-reduce), so d dists,
-            d zbuf and the smoothing scalars' gradients are the full-S ones.
+  forward : fragments broadcast to the devices; each device's perturbed Heaviside counts over
+            its rast shard are summed on the primary as integers (P = sum_i C_i / Sr, the
+            one-device P bit for bit) and P is broadcast back; each device runs the fused blend
+            kernel on P (prob input, PR_BLEND_RAST off) over its agg shard -- texel or vertex
+            colours -- and its per-sample winners are gathered on the primary, whose
+            PR_BLEND_WINNERS_IN launch forms the image from all Sa winners: the one-device
+            fused image bit for bit (same win counts, same colour mix);
+  backward: the image is sum_i (n_i / Sa) rgb_i (+ alpha, which every shard computes alike), so
+            shard i's fused backward takes (n_i / Sa) g_rgb (and g_alpha on the primary only);
+            the adjoints of the broadcasts / count sum carry d P to the Heaviside shards:
+            d dists, d zbuf, d colours / d bary / d vertex colours and the smoothing scalars'
+            gradients are the full-S ones up to the summation order of the shards' partials.
 
-P and W are exact counts, so the image is the one-device image bit for bit; gradients differ
-only by the summation order of the shards' partials.  The collectives are
-``torch.cuda.comm`` broadcast / reduce_add, i.e. RCCL (ncclCommInitAll) over xGMI when the
-devices are distinct GPUs; logical shards on one device (tests, one-GPU boxes) copy instead.
-This is the north star's sample partition without torchrun; the torchrun paths
-(``parallel.py``, bench.py) remain the measured multi-GPU configuration.
+The collectives are ``torch.cuda.comm`` broadcast / reduce_add, i.e. RCCL (ncclCommInitAll)
+over xGMI when the devices are distinct GPUs; logical shards on one device (tests, one-GPU
+boxes) copy instead.  This is the north star's sample partition without torchrun; the torchrun
+paths (``parallel.py``, bench.py) remain the measured multi-GPU configuration.
 """
 import os
 import warnings
@@ -146,47 +151,125 @@ class _WeightedReduce(torch.autograd.Function):
         return (None, None) + tuple(gi * w for gi, w in zip(gs, ctx.weights))
 
 
+class _CountReduce(torch.autograd.Function):
+    """(P_i on device i, P_i = C_i / n_i) -> (sum_i C_i) / Sr on dst with the integer counts
+    C_i = round(n_i P_i) summed exactly (the one-device P bit for bit); backward: the adjoint of
+    sum_i (n_i / Sr) P_i, i.e. (n_i / Sr) g broadcast to device i."""
+
+    @staticmethod
+    def forward(ctx, dst, ns, Sr, *ps):
+        ctx.devs, ctx.weights = [x.device for x in ps], [n / Sr for n in ns]
+        counts = [torch.round(x.detach() * float(n)) for x, n in zip(ps, ns)]
+        return _reduce_add(counts, dst) / float(Sr)
+
+    @staticmethod
+    def backward(ctx, g):
+        gs = _broadcast(g.detach(), ctx.devs)
+        return (None, None, None) + tuple(gi * w for gi, w in zip(gs, ctx.weights))
+
+
+class _ShardImages(torch.autograd.Function):
+    """image (the primary's PR_BLEND_WINNERS_IN image) standing for sum_i w_i rgb_i (+ alpha): the
+    forward returns `image`; the backward hands shard i the gradient of w_i rgb_i, and the alpha
+    gradient to shard 0 only (every shard's alpha is the same function of P)."""
+
+    @staticmethod
+    def forward(ctx, image, weights, *shard_images):
+        ctx.devs, ctx.weights = [x.device for x in shard_images], weights
+        return image
+
+    @staticmethod
+    def backward(ctx, g):
+        out = []
+        for i, (d, w) in enumerate(zip(ctx.devs, ctx.weights)):
+            gi = g.detach().to(d, copy=True)
+            gi[..., :3] *= w
+            if i:
+                gi[..., 3] = 0.0
+            out.append(gi)
+        return (None, None) + tuple(out)
+
+
+def _seeds_on(noise, devices):
+    """The DeviceSeed base of `noise` on every device (the tensor itself on its own device)."""
+    s = noise.seeds
+    if s is None:
+        return [None] * len(devices)
+    return [s if d == s.device else s.to(d) for d in devices]
+
+
 def sharded_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_samples_rast, nb_samples_agg,
                   devices=None, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0, zfar=100.0, fixed_noise=False,
-                  rast_kind="gaussian", rast_vr=True, agg_kind="gaussian", agg_vr=True):
+                  rast_kind="gaussian", rast_vr=True, agg_kind="gaussian", agg_vr=True, vert_colors=None, faces=None):
     """smooth_rgb_blend (random_rasterizer.py:34-56) of a native Monte-Carlo pair with its samples
-    split over `devices` (default: set_sample_devices) -- see the module docstring."""
-    from .blend import perturbed_aggregate, perturbed_heaviside
-    from .random_rasterizer import _background_tensor
-    from .variants import prod_last
+    split over `devices` (default: set_sample_devices) -- see the module docstring.  With
+    vert_colors / faces, `colors` are the fragments' barycentrics and the slot colours are the
+    fused TexturesVertex sampling's (RandomSimpleShader, random_rasterizer.py:164-177)."""
+    from .blend import (_FusedBlendFn, _FusedVertexBlendFn, _background, _counts_for, image_from_winners,
+                        perturbed_heaviside, variant_flags)
+    from .renderer.rasterizer import attach_valid_counts
     devices = [torch.device(d) for d in (devices or _DEVICES or [pix_to_face.device])]
     primary = pix_to_face.device
     if devices[0] != primary:
         raise ValueError(f"the first sample device ({devices[0]}) must hold the fragments ({primary})")
+    vertex = vert_colors is not None
     shape = tuple(pix_to_face.shape)
     N, H, W, K = shape
     # one key per operator, drawn as the one-device path draws them (rast, then agg)
     nr = noise_mod.draw_rast(shape, nb_samples_rast, primary, rast_kind)
     na = noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, primary, fixed_noise, agg_kind)
-    if nr.mode != nat.PR_NOISE_PHILOX or na.mode != nat.PR_NOISE_PHILOX or nr.seeds is not None \
-            or na.seeds is not None:
-        raise NotImplementedError("sample sharding over devices needs host-keyed Philox noise (not the "
-                                  "'torch' noise source or a graph-mode DeviceSeed)")
+    if nr.mode != nat.PR_NOISE_PHILOX or na.mode != nat.PR_NOISE_PHILOX:
+        raise NotImplementedError("sample sharding over devices needs Philox noise (not the 'torch' noise source)")
     n = len(devices)
     sh_r = [sample_shard(nb_samples_rast, i, n) for i in range(n)]
     sh_a = [sample_shard(nb_samples_agg, i, n) for i in range(n)]
     if any(c == 0 for _, c in sh_r + sh_a):
         raise ValueError(f"{n} sample devices need >= {n} rast and agg samples "
                          f"(Sr={nb_samples_rast}, Sa={nb_samples_agg})")
-    mask = pix_to_face >= 0
-    m_b = _broadcast(mask, devices)
+    counts = _counts_for(pix_to_face)
+    p2f_b = _broadcast(pix_to_face, devices)
+    if counts is not None:  # the valid-prefix counts travel with the fragments
+        for p2f_i, c_i in zip(p2f_b, _broadcast(counts, devices)):
+            attach_valid_counts(p2f_i, c_i)
+    mask_b = [p >= 0 for p in p2f_b]
     d_b = _Broadcast.apply(devices, dists)
     z_b = _Broadcast.apply(devices, zbuf)
-    P_i = [perturbed_heaviside(d_b[i], sigma, sh_r[i][1],
-                               noise=Noise.philox(seed_r=nr.seed_r, offset_r=nr.offset_r + sh_r[i][0]),
-                               kind=rast_kind, variance_reduction=rast_vr) * m_b[i] for i in range(n)]
-    P = _WeightedReduce.apply(primary, [c / nb_samples_rast for _, c in sh_r], *P_i)
+    c_b = _Broadcast.apply(devices, colors)
+    v_b = _Broadcast.apply(devices, vert_colors) if vertex else [None] * n
+    f_b = _broadcast(faces, devices) if vertex else [None] * n
+    sr_b, sa_b = _seeds_on(nr, devices), _seeds_on(na, devices)
+    # ---- rast shards -> P: exact integer counts summed on the primary
+    # device smoothing scalars are read by pointer: each shard's from its own device (a
+    # differentiable copy); CPU leaves and floats go by value
+    on = lambda x, d: x.to(d) if torch.is_tensor(x) and x.is_cuda and x.device != d else x
+    P_i = [perturbed_heaviside(d_b[i], on(sigma, devices[i]), sh_r[i][1],
+                               noise=Noise.philox(seed_r=nr.seed_r, offset_r=nr.offset_r + sh_r[i][0], seeds=sr_b[i]),
+                               kind=rast_kind, variance_reduction=rast_vr) * mask_b[i] for i in range(n)]
+    P = _CountReduce.apply(primary, [c for _, c in sh_r], nb_samples_rast, *P_i)
     P_b = _Broadcast.apply(devices, P)
-    W_i = [perturbed_aggregate(z_b[i], zfar, znear, P_b[i], m_b[i], gamma, alpha, sh_a[i][1], eps=eps,
-                               noise=Noise.philox(seed_a=na.seed_a, offset_a=na.offset_a + sh_a[i][0]),
-                               kind=agg_kind, variance_reduction=agg_vr) for i in range(n)]
-    Wt = _WeightedReduce.apply(primary, [c / nb_samples_agg for _, c in sh_a], *W_i)
-    bg = _background_tensor(background, primary)
-    rgb = (Wt[..., :K, None] * colors).sum(dim=-2) + Wt[..., K:K + 1] * bg  # random_rasterizer.py:50-53
-    a = 1.0 - prod_last(1.0 - P)  # :48, :54
-    return torch.cat([rgb, a[..., None]], dim=-1)
+    # ---- agg shards: the fused blend on P (prob input) over each shard's samples
+    vflags = variant_flags(rast_kind, rast_vr, agg_kind, agg_vr)
+    bg = _background(background)
+    sink = []
+    images = []
+    for i, d in enumerate(devices):
+        cfg = dict(Sr=nb_samples_rast, Sa=sh_a[i][1], eps=float(eps), bg=bg, vflags=vflags,
+                   counts=_counts_for(p2f_b[i]), prob_in=True, winners_sink=sink,
+                   noise=Noise.philox(seed_a=na.seed_a, offset_a=na.offset_a + sh_a[i][0], seeds=sa_b[i]))
+        zn = znear.to(d) if torch.is_tensor(znear) else znear
+        zf = zfar.to(d) if torch.is_tensor(zfar) else zfar
+        sc = [on(x, d) for x in (sigma, gamma, alpha)]
+        if vertex:
+            images.append(_FusedVertexBlendFn.apply(P_b[i], z_b[i], c_b[i], v_b[i], *sc, None, p2f_b[i], f_b[i], zn,
+                                                    zf, cfg))
+        else:
+            images.append(_FusedBlendFn.apply(P_b[i], z_b[i], c_b[i], *sc, None, p2f_b[i], zn, zf, cfg))
+    # ---- the image from every sample's winner on the primary (the one-device image bit for bit)
+    winners = torch.cat([w.to(primary) for w in sink], dim=1)
+    with torch.no_grad():
+        image = image_from_winners(P.detach(), zbuf.detach(), colors.detach(), pix_to_face, winners,
+                                   gamma.detach() if torch.is_tensor(gamma) else gamma,
+                                   alpha.detach() if torch.is_tensor(alpha) else alpha, eps=eps,
+                                   background=bg, znear=znear, zfar=zfar,
+                                   vert_colors=vert_colors.detach() if vertex else None, faces=faces)
+    return _ShardImages.apply(image, [c / nb_samples_agg for _, c in sh_a], *images)

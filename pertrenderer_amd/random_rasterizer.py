@@ -189,10 +189,16 @@ class RandomSimpleShader(_RandomShaderBase):
         blend_params = kwargs.get("blend_params", self.blend_params)
         znear, zfar = _planes_from(cameras, kwargs)
         vc = _vertex_colors(meshes)
-        if vc is not None and _is_fusable(self.smoothrast, self.smoothagg, fragments) \
-                and _multidevice.sample_devices() is None:
+        if vc is not None and _is_fusable(self.smoothrast, self.smoothagg, fragments):
             # TexturesVertex sampling fused into the blend (no (N,H,W,K,3) texel tensor)
             sr, sa = self.smoothrast, self.smoothagg
+            if _multidevice.sample_devices() is not None and _noise.get_noise_source() == "philox":
+                # samples split over the devices of set_sample_devices (in-process RCCL collectives)
+                return _multidevice.sharded_blend(
+                    fragments.bary_coords, fragments.pix_to_face, fragments.dists, fragments.zbuf, sr.sigma,
+                    sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,
+                    background=blend_params.background_color, znear=znear, zfar=zfar, fixed_noise=sa.fixed_noise,
+                    vert_colors=vc, faces=meshes.faces_packed(), **_variant_kw(sr, sa))
             return _blend.perturbed_blend_vertex(
                 vc, meshes.faces_packed(), fragments.pix_to_face, fragments.bary_coords, fragments.dists,
                 fragments.zbuf, sr.sigma, sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,

@@ -47,3 +47,32 @@ def test_set_sample_devices_needs_rocm_devices():
         md.set_sample_devices(["cpu", "cpu"])
     md.set_sample_devices(None)
     assert md.sample_devices() is None
+
+
+def test_count_reduce_is_exact_and_its_adjoint_is_the_weighted_broadcast():
+    """P = (sum_i round(n_i P_i)) / Sr: the one-device count / Sr bit for bit even when n_i does not
+    divide Sr (6 / 5 / 5 of 16), and the gradient that of sum_i (n_i / Sr) P_i."""
+    cpu = torch.device("cpu")
+    g = torch.Generator().manual_seed(0)
+    ns, Sr = [6, 5, 5], 16
+    cnt = [torch.randint(0, n + 1, (7, 9), generator=g) for n in ns]
+    ps = [(c.float() / n).requires_grad_(True) for c, n in zip(cnt, ns)]
+    P = md._CountReduce.apply(cpu, ns, Sr, *ps)
+    assert torch.equal(P, sum(c for c in cnt).float() / Sr)
+    w = torch.randn(7, 9, generator=g)
+    (P * w).sum().backward()
+    for p, n in zip(ps, ns):
+        torch.testing.assert_close(p.grad, w * (n / Sr))
+
+
+def test_shard_images_route_rgb_by_weight_and_alpha_to_the_primary():
+    cpu = torch.device("cpu")
+    image = torch.rand(1, 2, 3, 4)
+    shards = [torch.rand(1, 2, 3, 4, requires_grad=True) for _ in range(3)]
+    out = md._ShardImages.apply(image, [0.5, 0.25, 0.25], *shards)
+    assert torch.equal(out, image)
+    g = torch.randn(1, 2, 3, 4)
+    out.backward(g)
+    for i, (s, w) in enumerate(zip(shards, [0.5, 0.25, 0.25])):
+        torch.testing.assert_close(s.grad[..., :3], g[..., :3] * w)
+        torch.testing.assert_close(s.grad[..., 3], g[..., 3] if i == 0 else torch.zeros_like(g[..., 3]))
