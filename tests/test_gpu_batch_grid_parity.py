@@ -11,7 +11,7 @@ random_rasterizer.py:34-56):
 * image, d dists, d zbuf, d colours (texel variant) / d bary (vertex-colour variant) at
   conftest.assert_close (1e-5 elementwise relative), the smoothing scalars at 2e-5;
 * the per-slot gradients of the default layout bitwise equal to the consecutive layout's
-  (PR_BLEND_INTERLEAVE=0): B6 sums a pixel's d z in sample order on one lane in either layout;
+  (PR_BLEND_INTERLEAVE=0): B6's lane split depends on the launch, not on the block's entries;
 * the fused scalar reduction bitwise equal to the finalize kernel (PR_BLEND_SYNC=0 semantics via
   the module switch) and to its acq_rel-ordered form (PR_BLEND_SYNC_ORDER=release), on this grid.
 """
@@ -156,7 +156,7 @@ def test_batch_grid_default_layout_matches_oracle(case, device):
 
 
 def test_batch_grid_layouts_bitwise(case, device):
-    """Per-slot gradients do not depend on the pixel-block layout (B6: one lane, sample order)."""
+    """Per-slot gradients do not depend on the pixel-block layout (B6's split is per launch)."""
     vertex, f, _, _ = case
     a = _env({"PR_BLEND_INTERLEAVE": None}, lambda: _gpu(f, vertex, device))
     b = _env({"PR_BLEND_INTERLEAVE": "0"}, lambda: _gpu(f, vertex, device))

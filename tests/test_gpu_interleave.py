@@ -3,9 +3,10 @@ the consecutive blocks) against the consecutive layout.
 
 Every pixel is computed from its own fragments with Philox counters keyed by its physical index,
 so the forward image must be bitwise equal in both layouts, and so must the backward's per-slot
-gradients: B6 sums each entry's samples in order on one lane, whatever block holds the pixel
-(rounds 1-4 split light passes' sample groups over several lanes, so the two layouts summed
-some pixels differently).  The smoothing scalars' gradients are per-block partial
+gradients: B6's lane split per entry depends on the launch only (the agg sample count), never
+on the pass's entry count, so a pixel's d z is summed in the same order whatever block holds it
+(rounds 1-4 split light passes' sample groups over more lanes, so the two layouts summed some
+pixels differently).  The smoothing scalars' gradients are per-block partial
 sums reduced in another grouping, and the vertex-colour gradient is a float-atomic scatter: those
 two compare at conftest.assert_close (1e-5 elementwise relative).  Cases: the bench frame
 at 128^2 (vertex colours, Gaussian pair with and without variance reduction), a batch of two
@@ -133,8 +134,10 @@ def test_interleaved_blocks_aggregate(device):
     _compare(a, b, ("weights", "d prob", "d zbuf", "d gamma", "d alpha"), loose=("d gamma", "d alpha"))
 
 
-def test_default_layout_on_a_batch_grid(device):
-    """The default on a batch grid (5 x 256^2, backward grid > 8192 blocks): consecutive forward,
+@pytest.mark.parametrize("Sa", [8, 64])
+def test_default_layout_on_a_batch_grid(device, Sa):
+    """The default on a batch grid (5 x 256^2, backward grid > 8192 blocks; Sa = 64: B6 splits each
+    entry's 16 sample groups over 4 lanes in both layouts): consecutive forward,
     interleaved backward -- the forward's winners and rast cache are read by physical pixel / slot,
     so the mixed pair equals the consecutive one (image and per-slot gradients bitwise, the
     smoothing scalars to the per-block partials' grouping)."""
@@ -143,7 +146,7 @@ def test_default_layout_on_a_batch_grid(device):
     def run():
         dists, zbuf, colors = (t.clone().requires_grad_(True) for t in (d0, z0, c0))
         sig, gam, alp = (torch.tensor(v, device=device, requires_grad=True) for v in (1e-3, 1e-2, 1.0))
-        img = pa.perturbed_blend(colors, p2f, dists, zbuf, sig, gam, alp, 8, 8, background=(0.1, 0.2, 0.3),
+        img = pa.perturbed_blend(colors, p2f, dists, zbuf, sig, gam, alp, 8, Sa, background=(0.1, 0.2, 0.3),
                                  noise=Noise.philox(seed_r=3, seed_a=4))
         g = torch.randn(img.shape, device=device, generator=torch.Generator(device).manual_seed(5))
         img.backward(g)
