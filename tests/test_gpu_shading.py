@@ -255,3 +255,78 @@ def test_native_shading_matches_float32_composition(kind, device):
             assert_close(x, y, name=name)
     finally:
         torch.use_deterministic_algorithms(old)
+
+
+@pytest.mark.parametrize("counts", [True, False])
+def test_tiny_frames_shade_as_one_frame(device, counts):
+    """Frames of a few slots: a 2048-slot chunk of the shading kernels then spans more images than
+    its LDS table of per-image padded terms holds (pr_shade.hip pad_table), so padded slots take
+    the direct path.  The 48x48 frame cut into 576 frames of 2x2 pixels (the same light, camera and
+    materials on every row) shades bit for bit as the one frame, forward and backward, with the
+    valid-prefix counts attached or not."""
+    from pertrenderer_amd.renderer.rasterizer import Fragments, valid_counts
+    mesh, frag, lights, cams, mats, verts, loc, extra = _scene(device, "vertex")
+    N, H, W, K = frag.pix_to_face.shape
+    b = frag.bary_coords.detach().clone().requires_grad_(True)
+    one = Fragments(frag.pix_to_face, frag.zbuf.detach(), b, frag.dists.detach())
+    assert valid_counts(one.pix_to_face) is not None
+    out1 = sh.textured_phong_shading(mesh, one, lights, cams, mats)
+    n = H * W // 4
+    p2f = frag.pix_to_face.reshape(n, 2, 2, K).clone()
+    if counts:
+        c = valid_counts(frag.pix_to_face).reshape(n, 2, 2)
+        p2f._pr_valid_counts = (p2f._version, c)
+    bt = b.reshape(n, 2, 2, K, 3)
+    tiny = Fragments(p2f, frag.zbuf.detach().reshape(n, 2, 2, K), bt, frag.dists.detach().reshape(n, 2, 2, K))
+    assert (valid_counts(tiny.pix_to_face) is not None) == counts
+    outn = sh.textured_phong_shading(mesh, tiny, lights, cams, mats)
+    assert torch.equal(outn.reshape(out1.shape), out1)
+    G = torch.randn(out1.shape, device=device, generator=torch.Generator(device).manual_seed(9))
+    g1 = torch.autograd.grad((out1 * G).sum(), [b, extra], retain_graph=True)
+    gn = torch.autograd.grad((outn * G.reshape(outn.shape)).sum(), [b, extra])
+    assert torch.equal(g1[0], gn[0])
+    # float atomics: the per-vertex sums' order differs (entries that cancel keep an absolute error)
+    torch.testing.assert_close(g1[1], gn[1], rtol=1e-5, atol=1e-6 * float(g1[1].abs().max()))
+
+
+@pytest.mark.parametrize("kind", ["vertex", "uv"])
+def test_pixel_block_kernels_match_the_slot_kernels(kind, device, monkeypatch):
+    """With the valid-prefix counts attached the shading forward runs as pixel blocks (padded slots
+    written as 16-byte stores of the image's colour pattern, live slots enumerated from the counts'
+    prefix, pr_shade.hip shade_fwd_pix_kernel); PR_SHADE_PIX=0 forces the per-wave chunk kernel.
+    Colours bit for bit (and the backward, one kernel for both, on them); on a batch of 3 frames
+    whose pixel blocks straddle image boundaries (48^2 pixels = 36 blocks of 64)."""
+    from pertrenderer_amd.renderer.rasterizer import Fragments, valid_counts
+    mesh, frag, lights, cams, mats, verts, loc, extra = _scene(device, kind)
+    assert valid_counts(frag.pix_to_face) is not None
+    N = 3
+    p2f = frag.pix_to_face.expand(N, -1, -1, -1).contiguous()
+    p2f._pr_valid_counts = (p2f._version, valid_counts(frag.pix_to_face).expand(N, -1, -1).contiguous())
+    b = frag.bary_coords.detach().expand(N, -1, -1, -1, -1).contiguous().requires_grad_(True)
+    fr = Fragments(p2f, frag.zbuf.detach().expand(N, -1, -1, -1), b, frag.dists.detach().expand(N, -1, -1, -1))
+    if kind == "uv":
+        tex = mesh.textures
+        maps = tex.maps_padded().expand(N, -1, -1, -1).contiguous().detach().requires_grad_(True)
+        m = Meshes([verts] * N, [mesh.faces_packed()] * N,
+                   TexturesUV(maps, tex.faces_uvs_list() * N, tex.verts_uvs_list() * N))
+        leaf = maps
+    else:
+        m = Meshes([verts] * N, [mesh.faces_packed()] * N, TexturesVertex([extra] * N))
+        leaf = extra
+    F = mesh.faces_packed().shape[0]
+    # frame i's faces are the i-th copy in the packed mesh
+    fr = Fragments(p2f.where(p2f < 0, p2f + F * torch.arange(N, device=device).view(N, 1, 1, 1)), fr.zbuf, b,
+                   fr.dists)
+    fr.pix_to_face._pr_valid_counts = (fr.pix_to_face._version, p2f._pr_valid_counts[1])
+    G = torch.randn((N,) + tuple(frag.pix_to_face.shape[1:]) + (3,), device=device,
+                    generator=torch.Generator(device).manual_seed(2))
+    runs = []
+    for pix in ("1", "0"):
+        monkeypatch.setenv("PR_SHADE_PIX", pix)
+        out = sh.textured_phong_shading(m, fr, lights, cams, mats)
+        runs.append((out,) + tuple(torch.autograd.grad((out * G).sum(), [b, verts, leaf])))
+    (o1, gb1, gv1, gt1), (o0, gb0, gv0, gt0) = runs
+    assert torch.equal(o1, o0)
+    assert torch.equal(gb1, gb0)
+    for x, y in ((gv1, gv0), (gt1, gt0)):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6 * float(y.abs().max()))

@@ -7,7 +7,10 @@
 #                                   (libname: a variant built with build_native --out, default the product)
 #   rprof TAG [ENV=V ...]...        rast_fwd per-tile timeline (-DPR_RAST_PROFILE variant), one per env set
 #   pmc TAG [kprof.py args]         PMC counter passes, each its own rocprofv3 run (kernel trace only)
+#   pmcbench TAG [bench.py args]    PMC passes (as pmc) over one bench.py command
 #   prof TAG [bench.py args]        rocprofv3 --kernel-trace --stats of one bench command
+#   kvar TAG REGEX ENVS... -- ARGS  average times of the kernels matching REGEX, one rocprofv3 run of
+#                                   bench.py ARGS per env set
 #   final TAG                       round-end measurement: tests, smoke, bench lines (graph + CPU
 #                                   baseline, eager, eager under HIP_LAUNCH_BLOCKING=1, eval, cfg3,
 #                                   cfg4, eager eval), cfg5 (pose_opt 100 x 800), rocprof stats, PMC
@@ -80,6 +83,21 @@ prof() {
   python tools/rocprof_summary.py "$f" "$OUT/rocprof_kernels_$tag.json" "rocprofv3 --kernel-trace --stats -- python bench.py $*"
 }
 
+pmcbench() {  # PMC passes over a bench.py run: pmcbench TAG [bench.py args]
+  local tag="$1"; shift
+  (cd /tmp && export TMPDIR=/tmp
+   local i=0
+   for C in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" \
+            "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+     i=$((i+1))
+     timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$OUT/${tag}_p$i" -o p -- \
+       python "$R/bench.py" "$@" > "$OUT/${tag}_p$i.log" 2>&1 || { echo "pmc pass $i failed"; tail -5 "$OUT/${tag}_p$i.log"; exit 1; }
+     find "$OUT/${tag}_p$i" -name "*kernel_trace.csv" -delete
+   done) || return 1
+  python tools/pmc_summary.py "$OUT"/${tag}_p* > "$OUT/pmc_summary_$tag.txt" 2>&1
+  tail -20 "$OUT/pmc_summary_$tag.txt"
+}
+
 dense() {  # SURVEY §8(d) dense-fragment blend microbench: rocprofv3 stats + PMC passes
   local tag="$1"
   (cd /tmp && export TMPDIR=/tmp
@@ -98,6 +116,27 @@ sel() {  # selected GPU test files: sel TAG FILE...
   local rc=$?; grep -E "^(FAILED|ERROR)|passed|failed" "$OUT/tests_$tag.log" | tail -15; return $rc
 }
 
+kvar() {  # kernel times per env variant: kvar TAG REGEX "ENV=V ..." ... -- bench.py args
+  local tag="$1" pat="$2"; shift 2
+  local vars=()
+  while [ $# -gt 0 ] && [ "$1" != "--" ]; do vars+=("$1"); shift; done
+  shift || true
+  for envs in "${vars[@]}"; do
+    local d="$OUT/kvar_${tag}_${envs// /_}"
+    (cd /tmp && export TMPDIR=/tmp && export $envs
+     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o k -- \
+       python "$R/bench.py" "$@" > "$d.json" 2> "$d.err") || { echo "FAIL $envs"; tail -5 "$d.err"; return 1; }
+    local f; f=$(find "$d" -name "*kernel_stats.csv" | sort | sed -n 1p)
+    find "$d" -name "*kernel_trace.csv" -delete
+    python - "$f" "$pat" "$envs" "$d.json" <<'PY'
+import csv, json, re, sys
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if re.search(sys.argv[2], r["Name"])]
+v = json.load(open(sys.argv[4]))["value"]
+print(sys.argv[3], "value", v, {r["Name"].split("(")[0][-40:]: round(float(r["AverageNs"]) / 1e3, 2) for r in rows})
+PY
+  done
+}
+
 kernels() {  # per-step kernel list with the issuing call (tools/step_kernels.py)
   local tag="$1"; shift
   timeout -k 10 300 python tools/step_kernels.py --json "$OUT/step_kernels_$tag.json" "$@" > "$OUT/step_kernels_$tag.txt" 2>&1 \
@@ -109,6 +148,8 @@ case "$CMD" in
   dense) dense "${1:-d}" ;;
   sel) sel "$@" ;;
   kernels) kernels "$@" ;;
+  kvar) kvar "$@" ;;
+  pmcbench) pmcbench "$@" ;;
   tests) tests "${1:-t}" ;;
   quick) tests "${1:-q}" && bench "${1:-q}" --no-cpu-baseline ;;
   bench) bench "$@" ;;

@@ -73,7 +73,7 @@ if __name__ == "__main__":
         del args[i:i + 2]
     res = load(args)
     for k in sorted(res, key=lambda x: -res[x].get("SQ_WAVE_CYCLES", 0)):
-        if any(s in k for s in ("blend", "rast", "interp", "project", "heaviside")):
+        if any(s in k for s in ("blend", "rast", "interp", "project", "heaviside", "shade")):
             print(k, json.dumps({c: round(v) for c, v in sorted(res[k].items())}))
     if out:
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
