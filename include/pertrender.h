@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 16
+#define PR_ABI_VERSION 17
 
 /* error codes */
 #define PR_OK 0
@@ -285,6 +285,9 @@ typedef struct PRShadeArgs {
   const float* verts;          /* (V,3) world positions */
   int32_t flags;               /* PR_DETERMINISTIC: the backward's per-vertex / per-texel / per-batch */
                                /* sums in slot order (pr_shade_bwd_workspace_size bytes of workspace) */
+                               /* PR_GRAD_PREZEROED (backward): grad_verts / grad_normals / */
+                               /* grad_vert_colors / grad_light / grad_camera were zeroed by the */
+                               /* forward (below); grad_maps is still zeroed by the call */
   void* workspace;
   size_t workspace_bytes;
   const float* normals;        /* (V,3) vertex normals */
@@ -305,7 +308,9 @@ typedef struct PRShadeArgs {
   const float* shininess;      /* (N,) */
   const float* camera;         /* (N,3) camera centres */
   float* colors;               /* fwd out (N,H,W,K,3) */
-  /* backward: every non-null output is overwritten (accumulators are zeroed by the call) */
+  /* backward: every non-null output is overwritten (accumulators are zeroed by the call, or by */
+  /* the forward: pr_shade_fwd zeroes the non-null grad_verts, grad_normals, grad_vert_colors */
+  /* (PR_TEX_VERTEX), grad_light and grad_camera it is given, for a PR_GRAD_PREZEROED backward) */
   const float* grad_colors;    /* (N,H,W,K,3) */
   float* grad_bary;            /* (N,H,W,K,3) */
   float* grad_verts;           /* (V,3) */

@@ -162,7 +162,7 @@ EXPORTS = {
     "pr_vert_normals_fwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
     "pr_vert_normals_bwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
 }
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _lib = None
 

@@ -247,6 +247,20 @@ PR_DEV int wave_compact(const bool (&live)[R], int* list) {
   return off;
 }
 
+// The backward's small accumulators (d verts, d normals, d vertex colours, d light, d camera), when
+// given to the forward: zeroed by its grid, for a PR_GRAD_PREZEROED pr_shade_bwd (no memsets)
+PR_DEV void zero_accumulators(const PRShadeArgs& a) {
+  const int64_t t0 = (int64_t)blockIdx.x * kThreads + threadIdx.x, st = (int64_t)gridDim.x * kThreads;
+  float* vbuf[3] = {a.grad_verts, a.grad_normals, a.texture == PR_TEX_VERTEX ? a.grad_vert_colors : nullptr};
+  float* bbuf[2] = {a.grad_light, a.grad_camera};
+  for (int j = 0; j < 3; ++j)
+    if (vbuf[j])
+      for (int64_t i = t0; i < a.V * 3; i += st) vbuf[j][i] = 0.f;
+  for (int j = 0; j < 2; ++j)
+    if (bbuf[j])
+      for (int64_t i = t0; i < (int64_t)a.N * 3; i += st) bbuf[j][i] = 0.f;
+}
+
 // the per-image padded terms (lit, spec, tex: 9 floats per image) of all N images into LDS, once
 // per workgroup; false when N exceeds the table (padded slots then shade directly)
 // (threads t0.. compute it: the pixel-block kernels leave wave 0 to the counts)
@@ -287,6 +301,7 @@ template <int R>
 __global__ void __launch_bounds__(kThreads) shade_fwd_kernel(PRShadeArgs a, int64_t PK, int64_t HW, int idx32) {
   __shared__ int lists[kWaves][64 * R];
   __shared__ float pad[kPadImgs * 9];
+  zero_accumulators(a);
   const bool i32 = idx32 != 0;
   const int lane = threadIdx.x & 63;
   int* list = lists[threadIdx.x >> 6];
@@ -669,6 +684,7 @@ __global__ void __launch_bounds__(kThreads) shade_fwd_pix_kernel(PRShadeArgs a, 
                                                                   uint32_t kmag) {
   __shared__ PixBlock pb;
   __shared__ float4 pat[kPadImgs * 3];
+  zero_accumulators(a);
   pad_patterns(a, pat, 64);
   PR_PIX_BLOCKS(P, p0, npix) {
     pix_block_load(a, p0, (int)npix, HW, pb);
@@ -859,11 +875,13 @@ extern "C" int pr_shade_bwd(const PRShadeArgs* args, void* stream) {
   if (!a.grad_colors) return set_error(PR_ERR_ARG, "shade_bwd: grad_colors missing");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (a.flags & PR_DETERMINISTIC) return shade_bwd_deterministic(a, st);
+  // (PR_GRAD_PREZEROED: the forward zeroed the small accumulators; the map gradient is zeroed here)
+  const bool pre = a.flags & PR_GRAD_PREZEROED;
   struct Z { float* p; size_t n; } zs[] = {
-      {a.grad_verts, (size_t)a.V * 3}, {a.grad_normals, (size_t)a.V * 3},
-      {a.texture == PR_TEX_VERTEX ? a.grad_vert_colors : nullptr, (size_t)a.V * 3},
+      {pre ? nullptr : a.grad_verts, (size_t)a.V * 3}, {pre ? nullptr : a.grad_normals, (size_t)a.V * 3},
+      {a.texture == PR_TEX_VERTEX && !pre ? a.grad_vert_colors : nullptr, (size_t)a.V * 3},
       {a.texture == PR_TEX_UV ? a.grad_maps : nullptr, (size_t)a.N * a.Hm * a.Wm * 3},
-      {a.grad_light, (size_t)a.N * 3}, {a.grad_camera, (size_t)a.N * 3}};
+      {pre ? nullptr : a.grad_light, (size_t)a.N * 3}, {pre ? nullptr : a.grad_camera, (size_t)a.N * 3}};
   for (const Z& z : zs)
     if (z.p && z.n && hipMemsetAsync(z.p, 0, z.n * sizeof(float), st) != hipSuccess)
       return set_error(PR_ERR_HIP, "shade_bwd: memset failed");

@@ -790,10 +790,15 @@ void shade_common(PRShadeArgs& a, const Tensor& p2f, const Tensor& counts, const
 const char* kShadeKeys[6] = {"bary", "verts", "normals", "tex", "light", "camera"};
 const char* kShadeRows[6] = {"ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular", "shininess"};
 
+// the small gradient accumulators (d verts, d normals, d vertex colours, d light, d camera) that
+// pr_shade_fwd zeroes for a PR_GRAD_PREZEROED backward: inputs 1, 2, 3 (vertex colours), 4, 5
+bool prezeroable(int i, int64_t mode) { return i == 1 || i == 2 || i == 4 || i == 5 || (i == 3 && mode == PR_TEX_VERTEX); }
+
 struct ShadeFn : public torch::autograd::Function<ShadeFn> {
+  // pz: bit i set = input i will want a gradient (sized and zeroed by the forward's kernel)
   static Tensor forward(AutogradContext* ctx, Tensor bary, Tensor verts, Tensor normals, Tensor tex, Tensor light,
                         Tensor camera, Tensor p2f, Opt counts_o, Tensor faces, Opt face_uvs_o, std::vector<Tensor> rows,
-                        int64_t mode, bool directional) {
+                        int64_t mode, bool directional, int64_t pz) {
     const Tensor counts = val(counts_o), face_uvs = val(face_uvs_o);
     if (rows.size() != 6) throw std::invalid_argument("shade: 6 parameter rows expected");
     on_device({&bary, &verts, &normals, &tex, &light, &camera, &p2f, &counts, &faces, &face_uvs});
@@ -806,10 +811,21 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
     PRShadeArgs a{};
     shade_common(a, p2f_c, counts, faces, face_uvs, t, rows.data(), mode, directional);
     a.colors = ptr<float>(colors);
+    Tensor acc[6];
+    for (int i = 1; i < 6; ++i)
+      if ((pz >> i) & 1 && prezeroable(i, mode)) acc[i] = at::empty_like(t[i]);
+    a.grad_verts = ptr<float>(acc[1]);
+    a.grad_normals = ptr<float>(acc[2]);
+    a.grad_vert_colors = ptr<float>(acc[3]);
+    a.grad_light = ptr<float>(acc[4]);
+    a.grad_camera = ptr<float>(acc[5]);
     at::DeviceGuard dg(colors.device());
     check(api().shade_fwd(&a, stream_of(colors)), "pr_shade_fwd");
     Keep k(ctx);
     for (int i = 0; i < 6; ++i) k(kShadeKeys[i], t[i]);
+    const char* kAcc[6] = {"", "acc1", "acc2", "acc3", "acc4", "acc5"};
+    for (int i = 1; i < 6; ++i) k(kAcc[i], acc[i]);
+    ctx->saved_data["prezeroed"] = true;
     for (int i = 0; i < 6; ++i) k(kShadeRows[i], rows[i]);
     k("p2f", p2f_c);
     k("counts", counts);
@@ -822,7 +838,7 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    variable_list out(13);
+    variable_list out(14);  // one per forward argument
     if (!grads[0].defined()) return out;
     const Saved sv(ctx);
     Tensor t[6], rows[6];
@@ -834,7 +850,17 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
     shade_common(a, sv("p2f"), sv("counts"), sv("faces"), sv("face_uvs"), t, rows,
                  mode, ctx->saved_data["directional"].toBool());
     a.grad_colors = ptr<float>(g);
-    for (int i = 0; i < 6; ++i) out[i] = ctx->needs_input_grad(i) ? at::empty_like(t[i]) : Tensor();
+    // the forward's zeroed accumulators, once: a second backward (retain_graph) sizes and zeroes
+    // its own; an accumulator the forward did not size sends the whole call down the zeroing path
+    const char* kAcc[6] = {"", "acc1", "acc2", "acc3", "acc4", "acc5"};
+    bool pre = ctx->saved_data["prezeroed"].toBool();
+    ctx->saved_data["prezeroed"] = false;
+    for (int i = 0; i < 6; ++i) {
+      if (!ctx->needs_input_grad(i)) continue;
+      const Tensor z = i > 0 && pre ? sv(kAcc[i]) : Tensor();
+      out[i] = z.defined() ? z : at::empty_like(t[i]);
+      if (i > 0 && prezeroable(i, mode) && !z.defined()) pre = false;
+    }
     a.grad_bary = ptr<float>(out[0]);
     a.grad_verts = ptr<float>(out[1]);
     a.grad_normals = ptr<float>(out[2]);
@@ -846,11 +872,12 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
     at::DeviceGuard dg(g.device());
     Tensor ws;
     if (at::globalContext().deterministicAlgorithms()) {  // in-order sums, no float atomics
-      a.flags = PR_DETERMINISTIC;
+      a.flags = PR_DETERMINISTIC;  // (overwrites its outputs: the pre-zeroing is moot)
       ws = workspace(api().shade_bwd_workspace_size(&a), g);
       a.workspace = ws.data_ptr();
       a.workspace_bytes = static_cast<size_t>(ws.numel());
     }
+    if (pre && !(a.flags & PR_DETERMINISTIC)) a.flags |= PR_GRAD_PREZEROED;
     check(api().shade_bwd(&a, stream_of(g)), "pr_shade_bwd");
     return once(grads, out);
   }
@@ -859,8 +886,14 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
 Tensor shade(const Tensor& bary, const Tensor& verts, const Tensor& normals, const Tensor& tex, const Tensor& light,
              const Tensor& camera, const Tensor& p2f, Opt counts, const Tensor& faces, Opt face_uvs,
              std::vector<Tensor> rows, int64_t mode, bool directional) {
+  // which inputs will want a gradient (as project_rasterize: the C++ context cannot ask yet)
+  int64_t pz = 0;
+  if (at::GradMode::is_enabled()) {
+    const Tensor* in[6] = {&bary, &verts, &normals, &tex, &light, &camera};
+    for (int i = 0; i < 6; ++i) pz |= in[i]->requires_grad() ? (int64_t(1) << i) : 0;
+  }
   return ShadeFn::apply(bary, verts, normals, tex, light, camera, p2f, counts, faces, face_uvs, rows, mode,
-                        directional);
+                        directional, pz);
 }
 
 struct VertNormalsFn : public torch::autograd::Function<VertNormalsFn> {

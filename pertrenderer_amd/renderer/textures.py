@@ -36,6 +36,8 @@ class TexturesUV:
         self.padding_mode, self.align_corners = padding_mode, align_corners
 
     def maps_padded(self):
+        if len(self._maps) == 1:  # a view: no copy of the map per render (gradients flow through it)
+            return self._maps[0].unsqueeze(0)
         return torch.stack(self._maps, 0)
 
     def faces_uvs_list(self):
@@ -45,7 +47,19 @@ class TexturesUV:
         return self._verts_uvs
 
     def faces_verts_uvs_packed(self):
-        return torch.cat([vu[fu] for vu, fu in zip(self._verts_uvs, self._faces_uvs)], 0)   # (F,3,2)
+        """(F,3,2) per-face-corner UVs.  Without gradients on the UVs the gather is kept on the
+        object, keyed by the UV tensors' identities and versions (an in-place edit misses): a
+        render per step then launches no gather / concatenation kernels for constant UVs.  The
+        returned tensor is shared between calls: treat it as read-only."""
+        srcs = self._verts_uvs + self._faces_uvs
+        if any(t.requires_grad for t in srcs):
+            return torch.cat([vu[fu] for vu, fu in zip(self._verts_uvs, self._faces_uvs)], 0)
+        key = tuple((id(t), t._version) for t in srcs)
+        hit = getattr(self, "_fvu_cache", None)
+        if hit is None or hit[0] != key:
+            out = torch.cat([vu[fu] for vu, fu in zip(self._verts_uvs, self._faces_uvs)], 0)
+            self._fvu_cache = hit = (key, out, srcs)  # (srcs held: their ids are not reused)
+        return hit[1]
 
     def fusable(self):
         """The native shading kernel samples these maps itself: bilinear, align_corners, border

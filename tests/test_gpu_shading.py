@@ -330,3 +330,28 @@ def test_pixel_block_kernels_match_the_slot_kernels(kind, device, monkeypatch):
     assert torch.equal(gb1, gb0)
     for x, y in ((gv1, gv0), (gt1, gt0)):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6 * float(y.abs().max()))
+
+
+def test_forward_zeroed_accumulators_once(device):
+    """The C++ layer's shading forward zeroes the backward's small accumulators (d verts, d normals,
+    d vertex colours, d light; pr_shade_fwd + PR_GRAD_PREZEROED, no memsets in the backward): a
+    second backward of the same graph (retain_graph) zeroes its own and gives the same gradients,
+    and both agree with the Python layer's (zeroed by the backward call)."""
+    from pertrenderer_amd import host_layer
+    assert host_layer.get() is not None, host_layer.error()
+    mesh, frag, lights, cams, mats, verts, loc, extra = _scene(device, "vertex")
+    out = sh.textured_phong_shading(mesh, frag, lights, cams, mats)
+    G = torch.randn(out.shape, device=device, generator=torch.Generator(device).manual_seed(4))
+    leaves = [verts, loc, extra]
+    g1 = torch.autograd.grad((out * G).sum(), leaves, retain_graph=True)
+    g2 = torch.autograd.grad((out * G).sum(), leaves)
+    with host_layer.disabled():
+        mesh2, frag2, lights2, cams2, mats2, verts2, loc2, extra2 = _scene(device, "vertex")
+        out2 = sh.textured_phong_shading(mesh2, frag2, lights2, cams2, mats2)
+        g3 = torch.autograd.grad((out2 * G).sum(), [verts2, loc2, extra2])
+    assert torch.equal(out, out2)
+    for a, b, c in zip(g1, g2, g3):
+        assert float(a.abs().sum()) > 0
+        tol = dict(rtol=1e-5, atol=1e-6 * float(c.abs().max()))  # float atomics: order differs
+        torch.testing.assert_close(a, b, **tol)
+        torch.testing.assert_close(a, c, **tol)
