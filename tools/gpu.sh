@@ -15,6 +15,8 @@
 #                                   baseline, eager, eager under HIP_LAUNCH_BLOCKING=1, eval, cfg3,
 #                                   cfg4, eager eval), cfg5 (pose_opt 100 x 800), rocprof stats, PMC
 #                                   passes and their summary
+#   final2 TAG                      eager / HIP_LAUNCH_BLOCKING=1 rows of the eval renderer and cfg5
+#                                   (20 problems), then the dense microbench records
 #
 # Every GPU step runs under its own timeout and the chain stops at the first failure.
 set -u
@@ -177,6 +179,18 @@ case "$CMD" in
     tail -3 "$OUT/cfg5_$T.log"
     prof "$T" --steps 200 --warmup 20 --no-cpu-baseline --no-dense || exit 1
     pmc "pmc_$T" || exit 1
+    ;;
+  final2)  # the eager / host-synchronous rows of eval.py's own mode + the dense records
+    T="${1:-fin}"
+    HIP_LAUNCH_BLOCKING=1 bench "eager_blocking_eval_$T" --config eval --mode eager --no-cpu-baseline --no-dense || exit 1
+    # cfg5 at 20 of the 100 problems (the per-problem time is what compares): eager, then host-synchronous
+    timeout -k 10 300 python -m pertrenderer_amd.pose_opt -np 20 -ni 800 --mode eager --out "$OUT/cfg5_eager_$T" \
+      > "$OUT/cfg5_eager_$T.log" 2>&1 || { tail -5 "$OUT/cfg5_eager_$T.log"; exit 1; }
+    tail -2 "$OUT/cfg5_eager_$T.log"
+    HIP_LAUNCH_BLOCKING=1 timeout -k 10 400 python -m pertrenderer_amd.pose_opt -np 20 -ni 800 --mode eager \
+      --out "$OUT/cfg5_eager_blocking_$T" > "$OUT/cfg5_eager_blocking_$T.log" 2>&1 || { tail -5 "$OUT/cfg5_eager_blocking_$T.log"; exit 1; }
+    tail -2 "$OUT/cfg5_eager_blocking_$T.log"
+    dense "$T" || exit 1
     ;;
   *) echo "unknown command $CMD"; exit 2 ;;
 esac
