@@ -94,9 +94,10 @@ __global__ void __launch_bounds__(kThreads) rotate_fwd_kernel(PRRotateArgs a) {
 }
 
 // One workgroup per R (per batch if R_batched, else one for all): d R = sum_p p^T g,
-// reduced in a fixed order; d points = g @ R^T alongside.
+// reduced in a fixed order (per lane, then a wave butterfly, then the waves in order);
+// d points = g @ R^T alongside.
 __global__ void __launch_bounds__(kThreads) rotate_bwd_kernel(PRRotateArgs a) {
-  __shared__ float red[kThreads * 9];
+  __shared__ float red[kThreads / 64][9];
   const int tid = threadIdx.x;
   const int r = blockIdx.x;
   const int n0 = a.R_batched ? r : 0, n1 = a.R_batched ? r + 1 : a.N;
@@ -118,16 +119,18 @@ __global__ void __launch_bounds__(kThreads) rotate_bwd_kernel(PRRotateArgs a) {
   }
   if (!a.grad_R) return;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) red[i * kThreads + tid] = acc[i];
-  __syncthreads();
-  for (int s = kThreads / 2; s > 0; s >>= 1) {
-    if (tid < s) {
+  for (int i = 0; i < 9; ++i)
 #pragma unroll
-      for (int i = 0; i < 9; ++i) red[i * kThreads + tid] += red[i * kThreads + tid + s];
-    }
-    __syncthreads();
+    for (int m = 32; m > 0; m >>= 1) acc[i] += __shfl_xor(acc[i], m);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) red[tid >> 6][i] = acc[i];
+  __syncthreads();
+  if (tid < 9) {
+    float v = red[0][tid];
+    for (int w = 1; w < kThreads / 64; ++w) v += red[w][tid];
+    a.grad_R[r * 9 + tid] = v;
   }
-  if (tid < 9) a.grad_R[r * 9 + tid] = red[tid * kThreads];
 }
 
 }  // namespace
