@@ -16,6 +16,7 @@
 #include "../../include/pertrender.h"
 
 #define PR_DEV __device__ __forceinline__
+#define PR_HD __host__ __device__ __forceinline__
 
 namespace pr {
 

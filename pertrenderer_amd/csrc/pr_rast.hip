@@ -523,15 +523,22 @@ PR_DEV void wave_sort_lds(float* lkey, int* lidx, int lane) {
 
 PR_DEV bool ekey_less(float2 x, float2 y) { return key_less(x.x, __float_as_int(x.y), y.x, __float_as_int(y.y)); }
 
+// one wave's LDS region of rast_fwd_kernel (16-byte multiple: the next wave's chunk records)
 template <int SL>
-size_t rast_fwd_lds_sl(int K) {
+PR_HD size_t rast_fwd_wave_bytes(int K) {
   using C = RastCfg<SL>;
-  return C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL + rast_qpad<SL>()) * 8 + (size_t)C::CAP * 12 + 64 * 4 + C::CH * 12 + 16;
+  const size_t b = C::CH * sizeof(FaceRec) + (size_t)K * (64 / SL + rast_qpad<SL>()) * 8 + 64 * 4 + C::CH * 12;
+  return (b + 15) / 16 * 16;
 }
 
-size_t rast_fwd_lds(int K, int SL) {
-  return SL == 8 ? rast_fwd_lds_sl<8>(K)
-                 : SL == 4 ? rast_fwd_lds_sl<4>(K) : (SL == 2 ? rast_fwd_lds_sl<2>(K) : rast_fwd_lds_sl<1>(K));
+template <int SL>
+size_t rast_fwd_lds_sl(int K, int NW) {
+  return NW * rast_fwd_wave_bytes<SL>(K) + (size_t)RastCfg<SL>::CAP * 12 + 16;
+}
+
+size_t rast_fwd_lds(int K, int SL, int NW = 1) {
+  return SL == 8 ? rast_fwd_lds_sl<8>(K, 1)
+                 : SL == 4 ? rast_fwd_lds_sl<4>(K, NW) : (SL == 2 ? rast_fwd_lds_sl<2>(K, 1) : rast_fwd_lds_sl<1>(K, 1));
 }
 
 // v from the lane of the same pixel that holds slice s (lane = pixel * SL + slice):
@@ -608,25 +615,42 @@ PR_DEV void ring_tile(int b, int m, int& tx, int& ty) {
 #ifndef PR_RAST_WPE  // sweeps: 4 waves/SIMD (with PR_RAST_CH4=16: 128 VGPRs, 2 spills) measured equal
 #define PR_RAST_WPE 1
 #endif
-template <int SL, bool PERSP, bool CLIP, bool FRAG>
-__global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces,
-                                                      const uint2* __restrict__ fbox, int ring, BinGrid bins) {
+#ifndef PR_RAST_DUO_WPE  // two-wave tiles: waves per SIMD the register budget must allow
+#define PR_RAST_DUO_WPE 1
+#endif
+// NW = 2 (PR_RAST_DUO, SL = 4): two waves per tile.  Wave 0 culls and sorts the tile's face
+// list; the waves then walk alternate chunks of it, each into its own per-pixel K-queue, so a
+// heavy tile's test loop -- its critical path -- is split in two; the output pass reads the
+// k-th smallest key of the two queues by a merge-path search and is split over both waves.
+// The queues end as the K smallest keys of their halves, so the merged K smallest are the
+// one-wave kernel's: the same fragments bit for bit.
+template <int SL, bool PERSP, bool CLIP, bool FRAG, int NW>
+__global__ void __launch_bounds__(64 * NW, NW == 2 ? PR_RAST_DUO_WPE : PR_RAST_WPE)
+    rast_fwd_kernel(PRRastArgs a, const FaceRec* __restrict__ faces, const uint2* __restrict__ fbox, int ring,
+                    BinGrid bins) {
   constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW, TP = TW * TH;
   constexpr int kCap = RastCfg<SL>::CAP, kGroup = RastCfg<SL>::G, CH = RastCfg<SL>::CH;
   constexpr int QS = TP + rast_qpad<SL>();  // queue row stride (entries): padding spreads a pixel's rows over banks
+  constexpr int NT = 64 * NW;               // threads per tile
   extern __shared__ float smem[];
   const int K = a.K;
-  const int lane = threadIdx.x, pix = lane / SL, slice = lane % SL;
-  FaceRec* lrec = reinterpret_cast<FaceRec*>(smem);                // [CH] staged chunk
+  const int tid = threadIdx.x, lane = tid & 63, wv = NW == 2 ? tid >> 6 : 0;
+  const int pix = lane / SL, slice = lane % SL;
+  // per-wave regions [staged chunk | queues | queue sizes | chunk ids | suffix mins | margins],
+  // then the tile's shared face list (rast_fwd_lds_sl)
+  const size_t wbytes = rast_fwd_wave_bytes<SL>(K);
+  char* wbase = reinterpret_cast<char*>(smem) + wv * wbytes;
+  FaceRec* lrec = reinterpret_cast<FaceRec*>(wbase);                // [CH] staged chunk
   float2* q = reinterpret_cast<float2*>(lrec + CH);                 // [K][QS] per-pixel queues
-  int* lfid = reinterpret_cast<int*>(q + (size_t)K * QS);           // [kCap] tile face list (cull order)
-  float* lkey = reinterpret_cast<float*>(lfid + kCap);              // [kCap] sort key, then
-  float* lsuf = lkey;                                               //   suffix min of z_min
-  int* lidx = reinterpret_cast<int*>(lkey + kCap);                  // [kCap] sorted -> cull order
-  int* qsz = lidx + kCap;                                           // [64] queue sizes (per pixel)
+  int* qsz = reinterpret_cast<int*>(q + (size_t)K * QS);            // [64] queue sizes (per pixel)
   int* lcf = qsz + 64;                                              // [CH] staged chunk face ids
   float* lcs = reinterpret_cast<float*>(lcf + CH);                  // [CH] staged chunk suffix mins
   float* lmg = lcs + CH;                                            // [CH] staged faces' distance margins
+  int* lfid = reinterpret_cast<int*>(reinterpret_cast<char*>(smem) + NW * wbytes);  // [kCap] tile face list
+  float* lkey = reinterpret_cast<float*>(lfid + kCap);              // [kCap] sort key, then
+  float* lsuf = lkey;                                               //   suffix min of z_min
+  int* lidx = reinterpret_cast<int*>(lkey + kCap);                  // [kCap] sorted -> cull order
+  int64_t* lctl = reinterpret_cast<int64_t*>(lidx + kCap);          // [2] round: next cull position, list size
   const int n = blockIdx.z;
   const int H = a.H, W = a.W;
   int tile_x = blockIdx.x, tile_y = blockIdx.y;
@@ -673,9 +697,9 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
   while (base < fe) {
     // ---- gather this round's culled faces (expanded bbox overlaps the tile): kCullU
     //      chunks' boxes in flight at once, appended in face order without atomics; a
-    //      chunk that would overflow the round's list starts the next round
+    //      chunk that would overflow the round's list starts the next round (wave 0)
     int nl = 0;
-    while (base < fe && nl <= kCap - 64) {
+    while (wv == 0 && base < fe && nl <= kCap - 64) {
       uint2 pb[kCullU];  // packed fp16 boxes: half the registers of unpacked ones
       int fi[kCullU];
 #pragma unroll
@@ -703,6 +727,12 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
       }
       base = next < fe ? next : fe;
     }
+    if constexpr (NW > 1) {  // the round's list size and next cull position to the other wave
+      if (tid == 0) { lctl[0] = base; lctl[1] = nl; }
+      __syncthreads();
+      base = lctl[0];
+      nl = (int)lctl[1];
+    }
     __syncthreads();
     PR_STAMP(0);
 #ifdef PR_RAST_PROFILE
@@ -721,7 +751,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     //      appends).  Exactness does not depend on it; the early exit uses z_min.
     int n2 = 64;
     while (n2 < nl) n2 <<= 1;
-    for (int i = lane; i < n2; i += 64) {
+    for (int i = tid; i < n2; i += NT) {
       float key = __builtin_inff();
       if (i < nl) {
         const FaceRec& r = faces[lfid[i]];
@@ -743,17 +773,19 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     }
     __syncthreads();
     PR_STAMP(1);
-    if (n2 == 64) wave_sort_lds<1>(lkey, lidx, lane);
-    else if (kCap >= 128 && n2 == 128) wave_sort_lds<2>(lkey, lidx, lane);
-    else if (kCap >= 256 && n2 == 256) wave_sort_lds<4>(lkey, lidx, lane);
-    else if constexpr (kCap >= 512) wave_sort_lds<8>(lkey, lidx, lane);
+    if (wv == 0) {
+      if (n2 == 64) wave_sort_lds<1>(lkey, lidx, lane);
+      else if (kCap >= 128 && n2 == 128) wave_sort_lds<2>(lkey, lidx, lane);
+      else if (kCap >= 256 && n2 == 256) wave_sort_lds<4>(lkey, lidx, lane);
+      else if constexpr (kCap >= 512) wave_sort_lds<8>(lkey, lidx, lane);
+    }
     __syncthreads();
     PR_STAMP(2);
     // suffix minimum of z_min along the sorted order (faces after position i cannot
     // produce pz below lsuf[i] when barycentrics are clipped)
     {
-      const int per = (nl + 63) / 64;  // contiguous run of sorted positions per lane
-      const int i0 = lane * per, i1 = min(nl, i0 + per);
+      const int per = (nl + 63) / 64;  // contiguous run of sorted positions per lane (wave 0)
+      const int i0 = lane * per, i1 = wv == 0 ? min(nl, i0 + per) : i0;
       float zl[8];  // z_min of this lane's run (per <= kCap / 64)
 #pragma unroll
       for (int u = 0; u < 8; ++u) zl[u] = i0 + u < i1 ? faces[lfid[lidx[i0 + u]]].f.w : __builtin_inff();
@@ -785,13 +817,13 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     int nfid = 0;
     float nsuf = 0.f;
     if (lane < CH) {
-      const int sp = min(lane, nl - 1);
+      const int sp = min(wv * CH + lane, nl - 1);
       nfid = lfid[lidx[sp]];
       nsuf = lsuf[sp];
       const FaceRec* fp = faces + nfid;
       nra = fp->a; nrb = fp->b; nrc = fp->c; nrd = fp->d; nre = fp->e; nrf = fp->f;
     }
-    for (int c0 = 0; c0 < nl && __ballot(!done) != 0; c0 += CH) {
+    for (int c0 = wv * CH; c0 < nl && __ballot(!done) != 0; c0 += NW * CH) {
       const int cnt = min(CH, nl - c0);
       __builtin_amdgcn_wave_barrier();
       if (lane < cnt) {
@@ -803,8 +835,8 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      if (c0 + CH < nl && lane < CH) {
-        const int sp = c0 + CH + min(lane, nl - c0 - CH - 1);
+      if (c0 + NW * CH < nl && lane < CH) {
+        const int sp = c0 + NW * CH + min(lane, nl - c0 - NW * CH - 1);
         nfid = lfid[lidx[sp]];
         nsuf = lsuf[sp];
         const FaceRec* fp = faces + nfid;
@@ -1017,11 +1049,41 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     __syncthreads();
     PR_STAMP(4);
   }
-  if (slice == 0) {
-    qsz[pix] = inimg ? qs : 0;
-    if (inimg && a.pix_count) a.pix_count[((int64_t)n * H + row) * W + col] = qs;
+  if (slice == 0) qsz[pix] = inimg ? qs : 0;
+  if constexpr (NW == 1) {
+    if (slice == 0 && inimg && a.pix_count) a.pix_count[((int64_t)n * H + row) * W + col] = qs;
   }
   __syncthreads();
+  // NW = 2: the tile's two queues (each sorted, disjoint faces) and their merged sizes
+  const float2* qa = reinterpret_cast<const float2*>(reinterpret_cast<const char*>(lrec) - wv * wbytes + CH * sizeof(FaceRec));
+  const float2* qb = reinterpret_cast<const float2*>(reinterpret_cast<const char*>(qa) + wbytes);
+  const int* qsa = reinterpret_cast<const int*>(qa + (size_t)K * QS);
+  const int* qsb = reinterpret_cast<const int*>(qb + (size_t)K * QS);
+  if constexpr (NW == 2) {
+    if (wv == 0 && slice == 0 && inimg && a.pix_count)
+      a.pix_count[((int64_t)n * H + row) * W + col] = min(K, qsa[pix] + qsb[pix]);
+  }
+  // the merged queue's size at tile pixel t, and its k-th smallest key (merge path: i of A's
+  // entries are among the k smallest when A[i-1] < B[k-i] and B[k-i-1] < A[i])
+  auto msize = [&](int t) { return NW == 2 ? min(K, qsa[t] + qsb[t]) : qsz[t]; };
+  auto kth = [&](int t, int k) -> float2 {
+    if constexpr (NW == 1) {
+      return q[k * QS + t];
+    } else {
+      const int na = qsa[t], nb = qsb[t];
+      int lo = max(0, k - nb), hi = min(k, na);
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ekey_less(qa[mid * QS + t], qb[(k - 1 - mid) * QS + t])) lo = mid + 1;
+        else hi = mid;
+      }
+      const int j = k - lo;
+      if (lo >= na) return qb[j * QS + t];
+      if (j >= nb) return qa[lo * QS + t];
+      const float2 x = qa[lo * QS + t], y = qb[j * QS + t];
+      return ekey_less(x, y) ? x : y;
+    }
+  };
   // ---- coalesced output: each tile row's pixels own a contiguous ncols*K slot range;
   //      the wave walks the tile's rows as one flat index (4 slots per lane in flight)
   {
@@ -1037,24 +1099,25 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     // valid slot per lane (a pixel's valid slots are its queue prefix), so no face evaluation
     // runs for a lane group that holds padding -- on a heavy tile half or more of its slots
     constexpr bool kCompact = FRAG && TP <= 16 && PR_RAST_FRAGC;
-    for (int base = 0; base < total; base += 64 * U) {
+    for (int base = 0; base < total; base += NT * U) {
       float2 e[U];
       int sz[U], kk[U], cc[U], rr[U];
       int64_t o[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int i = min(base + u * 64 + lane, total - 1);
+        const int i = min(base + u * NT + tid, total - 1);
         int rem;
         rr[u] = divmod_small(i, per_row, inv_row, rem);
         cc[u] = divmod_small(rem, K, inv_k, kk[u]);
         const int tl = rr[u] * TW + cc[u];
         o[u] = (((int64_t)n * H + row0 + rr[u]) * W + col0) * K + rem;
-        e[u] = q[kk[u] * QS + tl];  // read with the size (stale beyond it, unused)
-        sz[u] = qsz[tl];
+        sz[u] = msize(tl);
+        if constexpr (NW == 1) e[u] = q[kk[u] * QS + tl];  // read with the size (stale beyond it, unused)
+        else e[u] = kk[u] < sz[u] ? kth(tl, kk[u]) : make_float2(0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (base + u * 64 + lane >= total) break;
+        if (base + u * NT + tid >= total) break;
         const bool valid = kk[u] < sz[u];
         const int fid = __float_as_int(e[u].y);
         a.pix_to_face[o[u]] = valid ? (int64_t)fid : (int64_t)-1;
@@ -1086,7 +1149,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
     if constexpr (kCompact) {
       // valid slot v belongs to the pixel t with ex[t] <= v < ex[t] + qsz[t] (ex: exclusive
       // prefix of the queue sizes over the tile's pixels, wave-uniform), at queue position v - ex[t]
-      const int mysz = lane < TP ? qsz[lane] : 0;
+      const int mysz = lane < TP ? msize(lane) : 0;
       int incl = mysz;
 #pragma unroll
       for (int o = 1; o < TP; o <<= 1) {
@@ -1098,12 +1161,12 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
 #pragma unroll
       for (int t = 0; t < TP; ++t) ex[t] = __builtin_amdgcn_readlane(excl, t);
       const int nvalid = __builtin_amdgcn_readlane(incl, TP - 1);
-      for (int vb = 0; vb < nvalid; vb += 64 * U) {
+      for (int vb = 0; vb < nvalid; vb += NT * U) {
         float2 e[U];
         int tl[U], kk[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int v = min(vb + u * 64 + lane, nvalid - 1);
+          const int v = min(vb + u * NT + tid, nvalid - 1);
           int t = 0, e0 = 0;
 #pragma unroll
           for (int s = 1; s < TP; ++s) {
@@ -1113,11 +1176,11 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
           }
           tl[u] = t;
           kk[u] = v - e0;
-          e[u] = q[kk[u] * QS + t];
+          e[u] = kth(t, kk[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if (vb + u * 64 + lane >= nvalid) break;
+          if (vb + u * NT + tid >= nvalid) break;
           const int fid = __float_as_int(e[u].y);
           const int rr = tl[u] / TW, cc = tl[u] % TW;
           const int64_t o = (((int64_t)n * H + row0 + rr) * W + col0 + cc) * K + kk[u];
@@ -1139,7 +1202,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
   PR_STAMP(5);
   int n_app_tot = n_app, n_ins_tot = n_ins;
   for (int o = 32; o > 0; o >>= 1) { n_app_tot += __shfl_xor(n_app_tot, o); n_ins_tot += __shfl_xor(n_ins_tot, o); }
-  if (lane == 0) {
+  if (tid == 0) {
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -1160,7 +1223,7 @@ __global__ void __launch_bounds__(64, PR_RAST_WPE) rast_fwd_kernel(PRRastArgs a,
 
 template <int SL, bool PERSP, bool CLIP>
 void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, bool frag, size_t lds,
-                        const BinGrid& bins, hipStream_t st) {
+                        const BinGrid& bins, hipStream_t st, int nw) {
   constexpr int TW = SL >= 4 ? 4 : 8, TH = 64 / SL / TW;
   dim3 grid((a.W + TW - 1) / TW, (a.H + TH - 1) / TH, a.N);
   // centre-out tile order on square grids of even side (PR_RAST_ORDER bit 0; 0: row-major)
@@ -1171,27 +1234,35 @@ void launch_rast_fwd_sl(const PRRastArgs& a, const FaceRec* fr, const uint2* fb,
   const bool sq = grid.x % 2 == 0 && (grid.y == grid.x || grid.y == 2 * grid.x);
   const int ring = (ring_env && sq ? 1 : 0) | (prio_env ? 2 : 0) | (prio_t << 8);
   ktimer_mark(0, "rast_fwd_kernel", st);
-  if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true><<<grid, 64, lds, st>>>(a, fr, fb, ring, bins);
-  else rast_fwd_kernel<SL, PERSP, CLIP, false><<<grid, 64, lds, st>>>(a, fr, fb, ring, bins);
+  if constexpr (SL == 4) {
+    if (nw == 2) {
+      if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true, 2><<<grid, 128, lds, st>>>(a, fr, fb, ring, bins);
+      else rast_fwd_kernel<SL, PERSP, CLIP, false, 2><<<grid, 128, lds, st>>>(a, fr, fb, ring, bins);
+      ktimer_mark(1, "rast_fwd_kernel", st);
+      return;
+    }
+  }
+  if (frag) rast_fwd_kernel<SL, PERSP, CLIP, true, 1><<<grid, 64, lds, st>>>(a, fr, fb, ring, bins);
+  else rast_fwd_kernel<SL, PERSP, CLIP, false, 1><<<grid, 64, lds, st>>>(a, fr, fb, ring, bins);
   ktimer_mark(1, "rast_fwd_kernel", st);
 }
 
 template <bool PERSP, bool CLIP>
 void launch_rast_fwd_pc(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, int sl, bool frag, size_t lds,
-                        const BinGrid& bins, hipStream_t st) {
-  if (sl == 8) launch_rast_fwd_sl<8, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st);
-  else if (sl == 4) launch_rast_fwd_sl<4, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st);
-  else if (sl == 2) launch_rast_fwd_sl<2, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st);
-  else launch_rast_fwd_sl<1, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st);
+                        const BinGrid& bins, hipStream_t st, int nw) {
+  if (sl == 8) launch_rast_fwd_sl<8, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st, 1);
+  else if (sl == 4) launch_rast_fwd_sl<4, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st, nw);
+  else if (sl == 2) launch_rast_fwd_sl<2, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st, 1);
+  else launch_rast_fwd_sl<1, PERSP, CLIP>(a, fr, fb, frag, lds, bins, st, 1);
 }
 
 void launch_rast_fwd(const PRRastArgs& a, const FaceRec* fr, const uint2* fb, int sl, bool frag, size_t lds,
-                     const BinGrid& bins, hipStream_t st) {
+                     const BinGrid& bins, hipStream_t st, int nw) {
   const bool persp = a.perspective_correct != 0, clip = a.clip_barycentric_coords != 0;
-  if (persp && clip) launch_rast_fwd_pc<true, true>(a, fr, fb, sl, frag, lds, bins, st);
-  else if (persp) launch_rast_fwd_pc<true, false>(a, fr, fb, sl, frag, lds, bins, st);
-  else if (clip) launch_rast_fwd_pc<false, true>(a, fr, fb, sl, frag, lds, bins, st);
-  else launch_rast_fwd_pc<false, false>(a, fr, fb, sl, frag, lds, bins, st);
+  if (persp && clip) launch_rast_fwd_pc<true, true>(a, fr, fb, sl, frag, lds, bins, st, nw);
+  else if (persp) launch_rast_fwd_pc<true, false>(a, fr, fb, sl, frag, lds, bins, st, nw);
+  else if (clip) launch_rast_fwd_pc<false, true>(a, fr, fb, sl, frag, lds, bins, st, nw);
+  else launch_rast_fwd_pc<false, false>(a, fr, fb, sl, frag, lds, bins, st, nw);
 }
 
 // Forward, pass 2: barycentrics (perspective-corrected, clipped) and signed squared
@@ -1964,9 +2035,12 @@ static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2
   }
   bool frag = true;
   if (const char* e = getenv("PR_RAST_FRAG")) frag = atoi(e) != 0;
-  const size_t lds = rast_fwd_lds(a.K, sl);
+  // two waves per 4x4 tile (rast_fwd_kernel NW = 2; PR_RAST_DUO=1, read per call)
+  const char* duo = getenv("PR_RAST_DUO");
+  const int nw = sl == 4 && duo && duo[0] == '1' ? 2 : 1;
+  const size_t lds = rast_fwd_lds(a.K, sl, nw);
   if (lds > 160 * 1024) return set_error(PR_ERR_ARG, "rast_fwd: faces_per_pixel too large for the LDS queue (max 300)");
-  launch_rast_fwd(a, fr, fbox, sl, frag, lds, bins, st);
+  launch_rast_fwd(a, fr, fbox, sl, frag, lds, bins, st, nw);
   if (int e = check_launch("rast_fwd")) return e;
   if (frag) return PR_OK;
   const int64_t total = (int64_t)a.N * a.H * a.W * a.K;

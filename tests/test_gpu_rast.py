@@ -231,6 +231,29 @@ def test_mesh_rasterizer_sphere_matches_oracle(size, K, dist_cam, device):
     assert (rp >= 0).sum(-1).max() == min(K, 56)  # the blur radius fills all K slots somewhere (<= 56 here)
 
 
+@pytest.mark.parametrize("size,K", [(256, 50), (24, 16), (64, 100)])
+def test_two_wave_tiles_match_one_wave_bitwise(size, K, device, monkeypatch):
+    """PR_RAST_DUO=1 (rast_fwd_kernel NW = 2: two waves per 4x4 tile, each walking alternate
+    chunks of the sorted face list into its own K-queue, the output pass merging them) gives the
+    one-wave kernel's fragments and valid counts bit for bit -- the cfg 2 frame, small images whose
+    lists take several rounds, and K = 100 (cfg 3)."""
+    from pertrenderer_amd.renderer.rasterizer import valid_counts
+    verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
+    mesh = Meshes([verts.to(device)], [faces.verts_idx.to(device)])
+    R, T = look_at_view_transform(2.7, 30.0, 120.0, device=device)
+    cams = FoVPerspectiveCameras(R=R, T=T, device=device)
+    rs = RasterizationSettings(image_size=size, blur_radius=np.log(1.0 / 1e-4 - 1.0) * 1e-3, faces_per_pixel=K,
+                               perspective_correct=False)
+    out = []
+    for duo in ("0", "1"):
+        monkeypatch.setenv("PR_RAST_DUO", duo)
+        f = MeshRasterizer(cameras=cams, raster_settings=rs)(mesh)
+        out.append((f.pix_to_face, f.zbuf, f.bary_coords, f.dists, valid_counts(f.pix_to_face)))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
+    assert (out[0][0] >= 0).sum() > 0
+
+
 def test_mesh_batch_with_one_camera_matches_single_meshes(device):
     """One camera broadcast over a batch of different meshes (PyTorch3D semantics): each image of
     the batch equals the single-mesh render, with pix_to_face offset by the mesh's first face."""

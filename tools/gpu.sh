@@ -124,7 +124,7 @@ kvar() {  # kernel times per env variant: kvar TAG REGEX "ENV=V ..." ... -- benc
   while [ $# -gt 0 ] && [ "$1" != "--" ]; do vars+=("$1"); shift; done
   shift || true
   for envs in "${vars[@]}"; do
-    local d="$OUT/kvar_${tag}_${envs// /_}"
+    local d="$OUT/kvar_${tag}_$(echo "$envs" | tr ' /' '__')"
     (cd /tmp && export TMPDIR=/tmp && export $envs
      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o k -- \
        python "$R/bench.py" "$@" > "$d.json" 2> "$d.err") || { echo "FAIL $envs"; tail -5 "$d.err"; return 1; }
