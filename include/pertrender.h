@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 17
+#define PR_ABI_VERSION 18
 
 /* error codes */
 #define PR_OK 0
@@ -213,6 +213,10 @@ typedef struct PRRastArgs {
   /* fragments never depend on either knob.  bin_size <= 0: every tile culls the whole mesh.      */
   int32_t bin_size;
   int32_t max_faces_per_bin;
+  /* nullable: the forward reads the blur threshold from this device float instead of          */
+  /* blur_radius (ABI 18), so a captured graph replays with a blur the caller changes in place   */
+  /* (eval.py's adaptive schedule lowers it every 50 iterations, eval.py:389-391)               */
+  const float* blur_radius_dev;
 } PRRastArgs;
 
 typedef struct PRInterpArgs {

@@ -78,7 +78,7 @@ class PRRastArgs(C.Structure):
                 ("grad_zbuf", _vp), ("grad_bary", _vp), ("grad_dists", _vp),
                 ("grad_face_verts", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
                 ("pix_count", _vp), ("flags", C.c_int32), ("bin_size", C.c_int32),
-                ("max_faces_per_bin", C.c_int32)]
+                ("max_faces_per_bin", C.c_int32), ("blur_radius_dev", _vp)]
 
 
 class PRInterpArgs(C.Structure):
@@ -162,7 +162,7 @@ EXPORTS = {
     "pr_vert_normals_fwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
     "pr_vert_normals_bwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
 }
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _lib = None
 

@@ -231,8 +231,9 @@ PR_DEV int mesh_of_sorted(const int64_t* first, int N, int64_t f) {
   return lo;
 }
 
-__global__ void face_prep_kernel(const float* fv, int64_t F, float blur, int cull_backfaces, FaceRec* out,
-                                 uint2* bbox, BinGrid bins, const int64_t* mesh_first, int N) {
+__global__ void face_prep_kernel(const float* fv, int64_t F, float blur_v, const float* blur_dev, int cull_backfaces,
+                                 FaceRec* out, uint2* bbox, BinGrid bins, const int64_t* mesh_first, int N) {
+  const float blur = blur_dev ? *blur_dev : blur_v;
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < F; f += (int64_t)gridDim.x * blockDim.x) {
     float v[9];
 #pragma unroll
@@ -683,7 +684,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 2 ? PR_RAST_DUO_WPE : PR_RAST_W
     if (c <= bins.cap) { ids = bins.list + (int64_t)b * bins.cap; fe = c; }
   }
   constexpr bool clip = CLIP;
-  const float blur = a.blur_radius, sqrt_blur = sqrtf(blur);
+  const float blur = a.blur_radius_dev ? *a.blur_radius_dev : a.blur_radius, sqrt_blur = sqrtf(blur);
   // the pixel's queue state, replicated in its SL lanes
   int qs = 0;
   float qlast_z = __builtin_inff();
@@ -1795,9 +1796,10 @@ __global__ void project_fwd_kernel(PRProjectArgs a) {
 // MeshRasterizer's projection and the rasterizer's face preparation in one pass (one
 // thread per face, project_fwd_kernel's operations per corner), plus the zeroing of the
 // backward's accumulators (grad_face_verts, grad_verts) so the backward needs no memset.
-__global__ void project_prep_kernel(PRProjectArgs a, float blur, int cull_backfaces, FaceRec* recs, uint2* bbox,
-                                    float* zero_fv, float* zero_v, BinGrid bins) {
+__global__ void project_prep_kernel(PRProjectArgs a, float blur_v, const float* blur_dev, int cull_backfaces,
+                                    FaceRec* recs, uint2* bbox, float* zero_fv, float* zero_v, BinGrid bins) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const float blur = blur_dev ? *blur_dev : blur_v;
   if (a.seed_advance && blockIdx.x == 0 && threadIdx.x == 0) {  // the caller's deferred key advances
     const unsigned i = threadIdx.x;  // (lane-indexed: a vector store)
     uint64_t s = a.seed_advance[i];
@@ -2012,8 +2014,8 @@ extern "C" int pr_rast_fwd(const PRRastArgs* args, void* stream) {
   if (int e = bins_begin(a, bins, st)) return e;
   if (a.F > 0) {
     const int nb = (int)std::min<int64_t>((a.F + kThreads - 1) / kThreads, 1024);
-    face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.cull_backfaces, fr, fbox, bins,
-                                              a.mesh_first_face, a.N);
+    face_prep_kernel<<<nb, kThreads, 0, st>>>(a.face_verts, a.F, a.blur_radius, a.blur_radius_dev, a.cull_backfaces, fr,
+                                              fbox, bins, a.mesh_first_face, a.N);
     if (int e = check_launch("rast_face_prep")) return e;
   }
   return rast_fwd_prepared(a, fr, fbox, bins, st);
@@ -2194,8 +2196,8 @@ extern "C" int pr_project_rast_fwd(const PRProjectArgs* pa, const PRRastArgs* ra
                                          pa->grad_verts ? pa->V * 3 : 0);
   if (work > 0 || (pa->seed_advance && pa->seed_advance_n > 0)) {
     const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((work + kThreads - 1) / kThreads, 1024));
-    project_prep_kernel<<<nb, kThreads, 0, st>>>(*pa, a.blur_radius, a.cull_backfaces, fr, fbox, a.grad_face_verts,
-                                                 pa->grad_verts, bins);
+    project_prep_kernel<<<nb, kThreads, 0, st>>>(*pa, a.blur_radius, a.blur_radius_dev, a.cull_backfaces, fr, fbox,
+                                                 a.grad_face_verts, pa->grad_verts, bins);
     if (int e = check_launch("project_prep")) return e;
   }
   return rast_fwd_prepared(a, fr, fbox, bins, st);

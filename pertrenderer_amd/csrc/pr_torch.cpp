@@ -471,7 +471,8 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
   static variable_list forward(AutogradContext* ctx, Tensor verts, Tensor faces, Tensor first, Tensor nfaces,
                                Tensor w2v, Tensor proj, c10::optional<Tensor> csr_start,
                                c10::optional<Tensor> csr_corners, std::vector<int64_t> cfg, double blur,
-                               bool need, c10::optional<Tensor> seed_adv, int64_t seed_n) {
+                               c10::optional<Tensor> blur_dev, bool need, c10::optional<Tensor> seed_adv,
+                               int64_t seed_n) {
     if (cfg.size() != 8) throw std::invalid_argument("project_rasterize: cfg must have 8 entries");
     Tensor cs = csr_start.has_value() ? *csr_start : Tensor(), cc = csr_corners.has_value() ? *csr_corners : Tensor();
     on_device({&verts, &faces, &first, &nfaces, &w2v, &proj, &cs, &cc});
@@ -495,6 +496,13 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
     }
     PRRastArgs a{};
     rast_common(a, fv, first, nfaces, cfg, blur);
+    const Tensor bd = val(blur_dev);  // a device blur threshold (graph replays with a changing blur)
+    if (bd.defined()) {
+      on_device({&bd});
+      if (bd.scalar_type() != at::kFloat || bd.numel() != 1)
+        throw std::invalid_argument("project_rasterize: a device blur_radius must be one float32");
+      a.blur_radius_dev = bd.data_ptr<float>();
+    }
     auto p2f = empty({N, H, W, K}, at::kLong, v);
     auto zbuf = empty({N, H, W, K}, at::kFloat, v);
     auto bary = empty({N, H, W, K, 3}, at::kFloat, v);
@@ -535,7 +543,7 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    variable_list out(13);  // one per forward argument
+    variable_list out(14);  // one per forward argument
     const Saved sv(ctx);
     auto gfv = sv("gfv"), gv = sv("gv");
     if (!gfv.defined()) return out;
@@ -584,12 +592,12 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
 variable_list project_rasterize(const Tensor& verts, const Tensor& faces, const Tensor& first, const Tensor& nfaces,
                                 const Tensor& w2v, const Tensor& proj, c10::optional<Tensor> csr_start,
                                 c10::optional<Tensor> csr_corners, std::vector<int64_t> cfg, double blur,
-                                c10::optional<Tensor> seed_adv, int64_t seed_n) {
+                                c10::optional<Tensor> blur_dev, c10::optional<Tensor> seed_adv, int64_t seed_n) {
   // the forward's gradient accumulators are sized when d verts will be wanted (Python's
   // ctx.needs_input_grad[0]; the C++ context has no edges to ask before the node is executable)
   const bool need = at::GradMode::is_enabled() && verts.requires_grad();
-  return ProjectRasterizeFn::apply(verts, faces, first, nfaces, w2v, proj, csr_start, csr_corners, cfg, blur, need,
-                                   seed_adv, seed_n);
+  return ProjectRasterizeFn::apply(verts, faces, first, nfaces, w2v, proj, csr_start, csr_corners, cfg, blur,
+                                   blur_dev, need, seed_adv, seed_n);
 }
 
 // ------------------------------------------------------------------ fused perturbed blend

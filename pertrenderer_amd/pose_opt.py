@@ -207,12 +207,22 @@ def _device_leaves(shader, device):
 
 
 def _fresh_adam(log_rot, lr):
-    """torch.optim.Adam([log_rot], lr) with its state initialised up front (capturable, fused):
-    the same state a new optimizer starts from (eval.py:337, :394)."""
-    opt = torch.optim.Adam([log_rot], lr=lr, capturable=True, fused=True)
+    """torch.optim.Adam([log_rot], lr) with its state initialised up front (capturable, fused, the
+    learning rate a device tensor): the same state a new optimizer starts from (eval.py:337)."""
+    lr_t = torch.tensor(float(lr), dtype=torch.float32, device=log_rot.device)
+    opt = torch.optim.Adam([log_rot], lr=lr_t, capturable=True, fused=True)
     opt.state[log_rot] = {"step": torch.zeros((), dtype=torch.float32, device=log_rot.device),
                           "exp_avg": torch.zeros_like(log_rot), "exp_avg_sq": torch.zeros_like(log_rot)}
     return opt
+
+
+def _renew_adam(opt, log_rot, lr):
+    """eval.py:394's new torch.optim.Adam(lr) in place: the state zeroed and the device learning
+    rate rewritten, so a captured step keeps addressing the same tensors."""
+    with torch.no_grad():
+        for t in opt.state[log_rot].values():
+            t.zero_()
+        opt.param_groups[0]["lr"].fill_(float(lr))
 
 
 class _CapturedIteration:
@@ -282,8 +292,11 @@ class _CapturedIteration:
 def optimize_pose_graph(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Niter=800, adapt_reg=True,
                         adapt_params=(1.1, 1.1)):
     """optimize_pose (eval.py:320-409) with every iteration a graph replay.  The host only acts at
-    the schedule's decision points (i > 100 with (i+1) % 50 == 0, eval.py:389): it reads v_gamma,
-    applies the smoothing / nb_samples / lr update and re-captures.  Returns (best_log_rot, info)."""
+    the schedule's decision points (i > 100 with (i+1) % 50 == 0, eval.py:389): it reads v_gamma
+    and applies the smoothing / blur / lr update in place -- the smoothing leaves, the blur radius
+    (a device float the rasterizer reads, PRRastArgs.blur_radius_dev) and Adam's learning rate
+    and state are device tensors the captured step addresses -- so it captures again only when
+    nb_samples changes (the kernels' sample counts are launch arguments).  Returns (best_log_rot, info)."""
     from . import noise
     dev = scene.device
     sh = renderer.shader
@@ -298,6 +311,9 @@ def optimize_pose_graph(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Ni
     target = target_rgb[0]
     lr = lr_init
     opt = _fresh_adam(log_rot, lr)
+    rs = renderer.rasterizer.raster_settings
+    blur0 = rs.blur_radius
+    rs.blur_radius = torch.tensor(float(blur0), dtype=torch.float32, device=dev)
     pool = torch.cuda.graph_pool_handle()
     step, step_post = None, None
     i = 0
@@ -323,18 +339,20 @@ def optimize_pose_graph(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Ni
                     sigma, gamma, _ = sh.get_smoothing()
                     s = max(float(sigma.detach()) / adapt_params[0], 5e-5)
                     g = max(float(gamma.detach()) / adapt_params[1], 5e-4)
-                    renderer.rasterizer.raster_settings.blur_radius = BLUR_FACTOR * s
+                    nb = sh.get_nb_samples()
                     with torch.no_grad():
+                        rs.blur_radius.fill_(BLUR_FACTOR * s)
                         sh.smoothrast.sigma.fill_(s)
                         sh.smoothagg.gamma.fill_(g)
                         sh.smoothagg.alpha.fill_(1.0)
-                    sh.update_nb_samples(nb_samples=min(2 * sh.get_nb_samples(), 128))
+                    sh.update_nb_samples(nb_samples=min(2 * nb, 128))
                     lr = max(lr / 1.5, 1e-4)
-                    opt = _fresh_adam(log_rot, lr)
-                    step_post = None  # S, blur and the optimizer changed: capture again
-                    torch.cuda.synchronize()
+                    _renew_adam(opt, log_rot, lr)
+                    if sh.get_nb_samples() != nb:
+                        step_post = None  # the sample counts changed: capture again
     finally:
         noise.use_device_seed(None)
+        rs.blur_radius = float(rs.blur_radius)  # back to PyTorch3D's float (one host read, at the end)
     torch.cuda.synchronize()
     info = dict(loss_values=st["losses"].cpu().tolist(), gradient_values=st["gnorms"].cpu().tolist(),
                 nb_samples=sh.get_nb_samples())

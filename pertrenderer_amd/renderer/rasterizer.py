@@ -87,6 +87,18 @@ def valid_counts(pix_to_face):
     return e[1] if e is not None and e[0] == pix_to_face._version else None
 
 
+def _blur_arg(blur, device):
+    """(by-value threshold, device threshold or None) for PRRastArgs: RasterizationSettings.blur_radius
+    may be a one-element float32 tensor on the mesh's device (an extension of PyTorch3D's float),
+    which the kernels read in place -- a captured graph then replays with the value the caller
+    last wrote (pose_opt's graph mode, eval.py's adaptive blur)."""
+    if torch.is_tensor(blur):
+        if blur.device != device or blur.dtype != F32 or blur.numel() != 1:
+            raise ValueError("a tensor blur_radius must be one float32 on the mesh's device")
+        return 0.0, blur
+    return float(blur), None
+
+
 def _bwd_workspace(lib, a, device):
     """Deterministic mode (torch.use_deterministic_algorithms): PR_DETERMINISTIC and its sort
     workspace on the rasterizer backward's args; None otherwise."""
@@ -193,7 +205,8 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         a = nat.PRRastArgs()
         a.face_verts, a.mesh_first_face, a.mesh_num_faces = nat.ptr(fv), nat.ptr(first), nat.ptr(nfaces)
         a.F, a.N, a.H, a.W, a.K = F, N, H, W, K
-        a.blur_radius, a.perspective_correct = float(blur), int(persp)
+        blur_v, blur_dev = _blur_arg(blur, dev)
+        a.blur_radius, a.blur_radius_dev, a.perspective_correct = blur_v, nat.ptr(blur_dev), int(persp)
         a.clip_barycentric_coords, a.cull_backfaces = int(clip), int(cull)
         a.bin_size, a.max_faces_per_bin = bins
         p2f = torch.empty((N, H, W, K), dtype=torch.int64, device=dev)
@@ -212,7 +225,7 @@ class _ProjectRasterizeFn(torch.autograd.Function):
         if timing is not None:
             timing.stop("rast_fwd")
         ctx.save_for_backward(v, f, first, nfaces, m1, m2, fv, p2f, counts, gfv, gv)
-        ctx.cfg = (H, W, K, float(blur), int(persp), int(clip), int(cull))
+        ctx.cfg = (H, W, K, blur_v, int(persp), int(clip), int(cull))
         ctx.csr = (csr_start, csr_corners)
         ctx.prezeroed = True
         ctx.mark_non_differentiable(p2f, counts)
@@ -305,8 +318,8 @@ class MeshRasterizer(torch.nn.Module):
     def forward(self, meshes_world, **kwargs) -> Fragments:
         rs = kwargs.get("raster_settings", self.raster_settings)
         clip = rs.clip_barycentric_coords
-        if clip is None:
-            clip = rs.blur_radius > 0.0
+        if clip is None:  # (a device blur_radius is taken as > 0: reading it would synchronise)
+            clip = True if torch.is_tensor(rs.blur_radius) else rs.blur_radius > 0.0
         cameras = kwargs.get("cameras", self.cameras)
         overrides = any(k in kwargs for k in ("R", "T", "znear", "zfar", "fov", "aspect_ratio", "degrees"))
         if (hasattr(cameras, "world_to_view_matrix") and not overrides and not cameras.matrices_need_grad()
@@ -327,20 +340,22 @@ class MeshRasterizer(torch.nn.Module):
                         verts, faces, first, nfaces, cameras.world_to_view_matrix(),
                         cameras.projection_matrix(), *meshes_world.corner_csr("gather"),
                         [H, W, int(rs.faces_per_pixel), int(bool(rs.perspective_correct)), int(bool(clip)),
-                         int(bool(rs.cull_backfaces)), bins[0], bins[1]], float(rs.blur_radius), seed_adv, seed_n)
+                         int(bool(rs.cull_backfaces)), bins[0], bins[1]], *_blur_arg(rs.blur_radius, verts.device),
+                        seed_adv, seed_n)
                 else:
                     p2f, zbuf, bary, dists, counts = _ProjectRasterizeFn.apply(
                         verts, faces, first, nfaces,
                         cameras.world_to_view_matrix(), cameras.projection_matrix(), H, W, int(rs.faces_per_pixel),
-                        float(rs.blur_radius), bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces),
+                        rs.blur_radius, bool(rs.perspective_correct), bool(clip), bool(rs.cull_backfaces),
                         bins, *meshes_world.corner_csr("gather"), seed_adv, seed_n)
             except BaseException:
                 noise_mod.give_back_advance(seed_n)
                 raise
             return Fragments(pix_to_face=attach_valid_counts(p2f, counts), zbuf=zbuf, bary_coords=bary, dists=dists)
         meshes_screen = self.transform(meshes_world, **kwargs)
+        blur = float(rs.blur_radius)  # (the torch-transform path takes the value: one host read)
         p2f, zbuf, bary, dists = rasterize_meshes(
-            meshes_screen, image_size=rs.image_size, blur_radius=rs.blur_radius,
+            meshes_screen, image_size=rs.image_size, blur_radius=blur,
             faces_per_pixel=rs.faces_per_pixel, bin_size=rs.bin_size, max_faces_per_bin=rs.max_faces_per_bin,
             perspective_correct=rs.perspective_correct, clip_barycentric_coords=clip,
             cull_backfaces=rs.cull_backfaces)

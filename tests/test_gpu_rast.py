@@ -4,6 +4,7 @@ Forward outputs are compared bit-exactly (same fp32 operation order on both side
 default backward computes each slot with the oracle's operations but sums faces with float
 atomics in arbitrary order, so it is compared at the 1e-5 bar (conftest.assert_close); its
 deterministic mode is the oracle bit for bit (tests/test_gpu_deterministic.py)."""
+import contextlib
 import os
 
 import numpy as np
@@ -337,3 +338,43 @@ def test_rasterizer_large_mesh_bins_match_oracle(bin_size, mfpb, device):
     np.testing.assert_array_equal(frag.zbuf.cpu().numpy(), rz)
     np.testing.assert_array_equal(frag.dists.cpu().numpy(), rd)
     np.testing.assert_array_equal(frag.bary_coords.cpu().numpy(), rb)
+
+
+@pytest.mark.parametrize("layer", ["c++", "python"])
+def test_device_blur_radius_matches_float_and_replays(layer, device):
+    """RasterizationSettings.blur_radius as a one-element float32 device tensor
+    (PRRastArgs.blur_radius_dev, ABI 18): fragments equal the float threshold's bit for bit; a
+    captured forward replays with the value last written into the tensor (pose_opt's graph mode
+    lowers the blur in place instead of capturing again)."""
+    from pertrenderer_amd import host_layer
+    verts, faces, _ = load_obj(os.path.join(ROOT, "tests", "golden", "sphere_642.obj"))
+    mesh = Meshes([verts.to(device)], [faces.verts_idx.to(device)])
+    R, T = look_at_view_transform(2.7, 30.0, 120.0, device=device)
+    cams = FoVPerspectiveCameras(R=R, T=T, device=device)
+    b1, b2 = 9.2e-3, 2.1e-3
+
+    def run(blur):
+        rs = RasterizationSettings(image_size=64, blur_radius=blur, faces_per_pixel=20, perspective_correct=False)
+        return MeshRasterizer(cameras=cams, raster_settings=rs)(mesh)
+
+    ctx = host_layer.disabled() if layer == "python" else contextlib.nullcontext()
+    with ctx:
+        ref1, ref2 = run(b1), run(b2)
+        bt = torch.tensor(b1, dtype=torch.float32, device=device)
+        got = run(bt)
+        for x, y in zip(got, ref1):
+            assert torch.equal(x, y)
+        assert not torch.equal(ref1.pix_to_face, ref2.pix_to_face)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            run(bt)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = run(bt)
+        bt.fill_(b2)
+        g.replay()
+        torch.cuda.synchronize()
+        for x, y in zip(out, ref2):
+            assert torch.equal(x, y)

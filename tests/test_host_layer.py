@@ -39,7 +39,7 @@ def test_host_tensors_are_refused():
         ext.project_rasterize(torch.zeros(3, 3), torch.zeros(1, 3, dtype=torch.int64),
                               torch.zeros(1, dtype=torch.int64), torch.ones(1, dtype=torch.int64),
                               torch.eye(4)[None], torch.eye(4)[None], None, None, [8, 8, 2, 0, 0, 0, 0, 0], 0.0,
-                              None, 0)
+                              None, None, 0)
     p = nat.PRBlendParams()
     z = torch.zeros(1, 2, 2, 3)
     with pytest.raises(ValueError, match="ROCm devices only"):
