@@ -289,33 +289,104 @@ class _CapturedIteration:
             self.graph.replay()
 
 
+def _nb(sh):
+    """(Sr, Sa) of a perturbed shader: the launch-time sample counts a captured step bakes in."""
+    return (getattr(sh.smoothrast, "nb_samples", None), getattr(sh.smoothagg, "nb_samples", None))
+
+
+class GraphSession:
+    """The captured iterations of optimize_pose_graph kept across the problems of one benchmark
+    run (compare_pose_opt / compare_runtime: one session per renderer configuration).  The first
+    call adopts its renderer and sizes every tensor a captured step addresses (the pose and its
+    gradient, the target, the loss records, Adam's state and learning rate, the noise key, the
+    blur radius, the smoothing leaves); later calls reset those in place to their problem's start
+    and replay the graphs already captured for each (phase, Sr, Sa) -- a problem then captures only
+    at sample counts no earlier problem reached.  The later calls' own renderers must be configured
+    as the adopted one (init_renderers with the same arguments); only their starting values are
+    taken from the call."""
+
+    def __init__(self):
+        self.renderer = None
+        self.graphs = {}
+
+    def bind(self, scene, init_pose, renderer, target_rgb, lr_init, Niter):
+        from . import noise
+        dev = scene.device
+        if self.renderer is None:
+            sh = renderer.shader
+            self.renderer, self.scene, self.Niter = renderer, scene, Niter
+            sr, sa = sh.smoothrast, sh.smoothagg
+            f = lambda t: float(t.detach()) if torch.is_tensor(t) else float(t)
+            self.start = dict(sigma=f(sr.sigma), gamma=f(sa.gamma), alpha=f(sa.alpha), nb=_nb(sh),
+                              blur=float(renderer.rasterizer.raster_settings.blur_radius))
+            _device_leaves(sh, dev)
+            self.seed = noise.DeviceSeed(dev)
+            self.log_rot = init_pose.clone().detach().to(dev).requires_grad_(True)
+            self.log_rot.grad = torch.zeros_like(self.log_rot)
+            self.target = target_rgb[0].clone()
+            self.st = dict(it=torch.zeros((), dtype=torch.int64, device=dev), losses=torch.zeros(Niter, device=dev),
+                           gnorms=torch.zeros(Niter, device=dev), best_loss=torch.full((), float("inf"), device=dev),
+                           best=self.log_rot.detach().clone(), v=torch.zeros(3, device=dev))
+            self.opt = _fresh_adam(self.log_rot, lr_init)
+            self.blur = torch.tensor(self.start["blur"], dtype=torch.float32, device=dev)
+            self.pool = torch.cuda.graph_pool_handle()
+        else:
+            if scene is not self.scene or Niter != self.Niter or type(renderer.shader) is not type(self.renderer.shader):
+                raise ValueError("GraphSession: a call with another scene, iteration count or shader")
+            sh = self.renderer.shader
+            z = self.start
+            with torch.no_grad():
+                for t, v in ((sh.smoothrast.sigma, z["sigma"]), (sh.smoothagg.gamma, z["gamma"]),
+                             (sh.smoothagg.alpha, z["alpha"])):
+                    if torch.is_tensor(t):
+                        t.fill_(v)
+                        t.grad.zero_()
+                if z["nb"][0] is not None:
+                    sh.smoothrast.nb_samples = z["nb"][0]
+                if z["nb"][1] is not None:
+                    sh.smoothagg.nb_samples = z["nb"][1]
+                self.blur.fill_(z["blur"])
+                self.log_rot.copy_(init_pose.to(dev))
+                self.log_rot.grad.zero_()
+                self.target.copy_(target_rgb[0])
+                st = self.st
+                st["it"].zero_()
+                st["losses"].zero_()
+                st["gnorms"].zero_()
+                st["best_loss"].fill_(float("inf"))
+                st["best"].copy_(self.log_rot)
+                st["v"].zero_()
+                self.seed.tensor.fill_(noise.draw_key())  # a new problem's key, as a new DeviceSeed draws
+                self.seed._next, self.seed._pending = 1, 0
+            _renew_adam(self.opt, self.log_rot, lr_init)
+        self.renderer.rasterizer.raster_settings.blur_radius = self.blur
+        noise.use_device_seed(self.seed)
+
+    def step(self, post):
+        """The captured iteration for the current phase and sample counts (captured on first use)."""
+        key = (post,) + _nb(self.renderer.shader)
+        cur = self.graphs.get(key)
+        if cur is None:
+            cur = _CapturedIteration(self.scene, self.renderer, self.target, self.log_rot, self.st, self.opt, post,
+                                     self.seed, self.pool)
+            self.graphs[key] = cur
+        return cur
+
+
 def optimize_pose_graph(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Niter=800, adapt_reg=True,
-                        adapt_params=(1.1, 1.1)):
+                        adapt_params=(1.1, 1.1), session=None):
     """optimize_pose (eval.py:320-409) with every iteration a graph replay.  The host only acts at
     the schedule's decision points (i > 100 with (i+1) % 50 == 0, eval.py:389): it reads v_gamma
     and applies the smoothing / blur / lr update in place -- the smoothing leaves, the blur radius
     (a device float the rasterizer reads, PRRastArgs.blur_radius_dev) and Adam's learning rate
     and state are device tensors the captured step addresses -- so it captures again only when
-    nb_samples changes (the kernels' sample counts are launch arguments).  Returns (best_log_rot, info)."""
+    the sample counts change (launch arguments).  `session` (GraphSession) keeps the captured
+    iterations for the next problem.  Returns (best_log_rot, info)."""
     from . import noise
-    dev = scene.device
-    sh = renderer.shader
-    _device_leaves(sh, dev)
-    seed = noise.DeviceSeed(dev)
-    noise.use_device_seed(seed)
-    log_rot = init_pose.clone().detach().to(dev).requires_grad_(True)
-    log_rot.grad = torch.zeros_like(log_rot)
-    st = dict(it=torch.zeros((), dtype=torch.int64, device=dev), losses=torch.zeros(Niter, device=dev),
-              gnorms=torch.zeros(Niter, device=dev), best_loss=torch.full((), float("inf"), device=dev),
-              best=log_rot.detach().clone(), v=torch.zeros(3, device=dev))
-    target = target_rgb[0]
+    ses = GraphSession() if session is None else session
+    ses.bind(scene, init_pose, renderer, target_rgb, lr_init, Niter)
+    sh, st, rs = ses.renderer.shader, ses.st, ses.renderer.rasterizer.raster_settings
     lr = lr_init
-    opt = _fresh_adam(log_rot, lr)
-    rs = renderer.rasterizer.raster_settings
-    blur0 = rs.blur_radius
-    rs.blur_radius = torch.tensor(float(blur0), dtype=torch.float32, device=dev)
-    pool = torch.cuda.graph_pool_handle()
-    step, step_post = None, None
     i = 0
     try:
         while i < Niter:
@@ -324,14 +395,7 @@ def optimize_pose_graph(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Ni
                 end = min(Niter, i + (49 - i % 50) + 1)  # through the next i with (i+1) % 50 == 0
             else:
                 end = min(Niter, 101) if adapt_reg else Niter
-            cur = step_post if post else step
-            if cur is None:
-                cur = _CapturedIteration(scene, renderer, target, log_rot, st, opt, post, seed, pool)
-                if post:
-                    step_post = cur
-                else:
-                    step = cur
-            cur.replay(end - i)
+            ses.step(post).replay(end - i)
             i = end
             if post and i % 50 == 0:  # the last replayed iteration had (i+1) % 50 == 0
                 v_gamma = float(st["v"][1])
@@ -339,20 +403,17 @@ def optimize_pose_graph(scene, init_pose, renderer, target_rgb, lr_init=5e-2, Ni
                     sigma, gamma, _ = sh.get_smoothing()
                     s = max(float(sigma.detach()) / adapt_params[0], 5e-5)
                     g = max(float(gamma.detach()) / adapt_params[1], 5e-4)
-                    nb = sh.get_nb_samples()
                     with torch.no_grad():
-                        rs.blur_radius.fill_(BLUR_FACTOR * s)
+                        ses.blur.fill_(BLUR_FACTOR * s)
                         sh.smoothrast.sigma.fill_(s)
                         sh.smoothagg.gamma.fill_(g)
                         sh.smoothagg.alpha.fill_(1.0)
-                    sh.update_nb_samples(nb_samples=min(2 * nb, 128))
+                    sh.update_nb_samples(nb_samples=min(2 * sh.get_nb_samples(), 128))
                     lr = max(lr / 1.5, 1e-4)
-                    _renew_adam(opt, log_rot, lr)
-                    if sh.get_nb_samples() != nb:
-                        step_post = None  # the sample counts changed: capture again
+                    _renew_adam(ses.opt, ses.log_rot, lr)
     finally:
         noise.use_device_seed(None)
-        rs.blur_radius = float(rs.blur_radius)  # back to PyTorch3D's float (one host read, at the end)
+        rs.blur_radius = float(ses.blur)  # back to PyTorch3D's float (one host read, at the end)
     torch.cuda.synchronize()
     info = dict(loss_values=st["losses"].cpu().tolist(), gradient_values=st["gnorms"].cpu().tolist(),
                 nb_samples=sh.get_nb_samples())
@@ -374,7 +435,11 @@ def make_problems(scene, num_prob, noise_type, pert):
     return problems
 
 
-def run_problem(scene, problem, noise_type, sigma, gamma, nb_mc, pert, niter, adapt_reg, adapt_params, mode):
+def run_problem(scene, problem, noise_type, sigma, gamma, nb_mc, pert, niter, adapt_reg, adapt_params, mode,
+                sessions=None):
+    """One compare_pose_opt problem for every noise type.  `sessions` (a dict kept by the caller
+    across problems; graph mode): one GraphSession per noise type, so the captured iterations of
+    earlier problems are replayed instead of captured again."""
     target_rgb, R_true, log_rot_init = problem
     _, renderers = init_renderers(scene, R_true, pert_init_intensity=pert, sigma=sigma, gamma=gamma,
                                   nb_samples=nb_mc, noise_type=noise_type)
@@ -383,8 +448,9 @@ def run_problem(scene, problem, noise_type, sigma, gamma, nb_mc, pert, niter, ad
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if mode == "graph":
+            ses = None if sessions is None else sessions.setdefault(nt, GraphSession())
             log_rot, info = optimize_pose_graph(scene, log_rot_init, renderer, target_rgb, Niter=niter,
-                                                adapt_reg=adapt_reg, adapt_params=adapt_params)
+                                                adapt_reg=adapt_reg, adapt_params=adapt_params, session=ses)
         else:
             log_rot, info = optimize_pose(scene, log_rot_init, renderer, target_rgb, Niter=niter, adapt_reg=adapt_reg,
                                           adapt_params=adapt_params)
@@ -504,10 +570,11 @@ def main(argv=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     results = {}
+    sessions = {}  # graph mode: the captured iterations, kept across this rank's problems
     for i in mine:
         results[i] = run_problem(scene, problems[i], noise_type, sigma, gamma, args.mc_samples,
                                  args.initial_perturbation, args.num_iterations, bool(args.adaptive_regularization),
-                                 adapt_params, args.mode)
+                                 adapt_params, args.mode, sessions=sessions)
         if rank == 0:
             print(json.dumps({"problem": i, **{nt: {k: round(v, 4) if isinstance(v, float) else v
                                                     for k, v in r.items()} for nt, r in results[i].items()}}),

@@ -99,3 +99,30 @@ def test_cfg5_full_size_graph_runs(device):
     json.dumps(tab)
     assert set(tab["mean_solved"]["gaussian"]) == set(pose_opt.THRESHOLDS)
     assert set(tab["mean_errors"]) == set(NOISE)
+
+
+def test_graph_session_replays_captured_iterations(device, monkeypatch):
+    """compare_pose_opt's driver keeps one GraphSession per noise type: the second problem resets
+    the session's tensors to its own start and replays the iterations the first one captured (no
+    capture at a sample count already seen), and still optimises its pose."""
+    torch.manual_seed(3)
+    scene = pose_opt.Scene(device, 64)
+    probs = pose_opt.make_problems(scene, 2, ["gaussian"], 20.0)
+    count = []
+    init0 = pose_opt._CapturedIteration.__init__
+
+    def counting(self, *a, **k):
+        count.append(1)
+        init0(self, *a, **k)
+
+    monkeypatch.setattr(pose_opt._CapturedIteration, "__init__", counting)
+    sessions = {}
+    per = []
+    for p in probs:
+        before = len(count)
+        per.append((pose_opt.run_problem(scene, p, ["gaussian"], 1e-3, 1e-2, 8, 20.0, 300, True, (1.1, 1.1), "graph",
+                                         sessions=sessions), len(count) - before))
+    (r1, c1), (r2, c2) = per
+    assert c1 >= 2 and c2 < c1, (c1, c2)
+    for r in (r1, r2):
+        assert np.isfinite(r["gaussian"]["final_error"]) and r["gaussian"]["final_error"] < r["gaussian"]["init_error"]

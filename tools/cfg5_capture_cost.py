@@ -1,6 +1,6 @@
 """Where a cfg 5 problem's time goes in graph mode: graph (re)captures against replays.
 
-    python tools/cfg5_capture_cost.py [problems]
+    python tools/cfg5_capture_cost.py [problems] [--sessions]
 
 Wraps pose_opt._CapturedIteration (construction = warm-up pass + capture) and its replay with
 device synchronisations, runs compare_pose_opt's problems through optimize_pose_graph and prints
@@ -16,7 +16,8 @@ from pertrenderer_amd import pose_opt as po  # noqa: E402
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    n = int(args[0]) if args else 3
     dev = torch.device("cuda:0")
     torch.manual_seed(1)
     scene = po.Scene(dev, 256)
@@ -41,6 +42,7 @@ def main():
         acc["replays"] += m
 
     Cap.__init__, Cap.replay = init, replay
+    sessions = {} if "--sessions" in sys.argv else None
     for noise_type in ("gaussian", "softras"):
         for p in range(n):
             target, R_true = scene.target()
@@ -48,12 +50,14 @@ def main():
             for k in acc:
                 acc[k] = 0 if isinstance(acc[k], int) else 0.0
             t = time.perf_counter()
-            po.optimize_pose_graph(scene, log_rot0, renderer, target, Niter=800)
+            ses = None if sessions is None else sessions.setdefault(noise_type, po.GraphSession())
+            po.optimize_pose_graph(scene, log_rot0, renderer, target, Niter=800, session=ses)
             torch.cuda.synchronize()
             tot = time.perf_counter() - t
             print(f"{noise_type} problem {p}: {tot:.3f} s; captures {acc['captures']} in {acc['capture']:.3f} s, "
                   f"replays {acc['replays']} in {acc['replay']:.3f} s ({1e3 * acc['replay'] / max(acc['replays'], 1):.3f} "
-                  f"ms each), other {tot - acc['capture'] - acc['replay']:.3f} s; final S {renderer.shader.get_nb_samples()}",
+                  f"ms each), other {tot - acc['capture'] - acc['replay']:.3f} s; final S "
+                  f"{(ses.renderer if ses is not None else renderer).shader.get_nb_samples()}",
                   flush=True)
 
 
