@@ -329,7 +329,6 @@ class GraphSession:
                            best=self.log_rot.detach().clone(), v=torch.zeros(3, device=dev))
             self.opt = _fresh_adam(self.log_rot, lr_init)
             self.blur = torch.tensor(self.start["blur"], dtype=torch.float32, device=dev)
-            self.pool = torch.cuda.graph_pool_handle()
         else:
             if scene is not self.scene or Niter != self.Niter or type(renderer.shader) is not type(self.renderer.shader):
                 raise ValueError("GraphSession: a call with another scene, iteration count or shader")
@@ -367,8 +366,10 @@ class GraphSession:
         key = (post,) + _nb(self.renderer.shader)
         cur = self.graphs.get(key)
         if cur is None:
+            # each graph its own memory pool: graphs sharing a pool may only replay in capture order,
+            # and a session replays its first-phase graph again after the later ones were captured
             cur = _CapturedIteration(self.scene, self.renderer, self.target, self.log_rot, self.st, self.opt, post,
-                                     self.seed, self.pool)
+                                     self.seed, torch.cuda.graph_pool_handle())
             self.graphs[key] = cur
         return cur
 
@@ -534,6 +535,9 @@ def main(argv=None):
     ap.add_argument("-ar", "--adaptive-regularization", type=int, default=1)
     ap.add_argument("-s", "--seed", type=int, default=1)
     ap.add_argument("--mode", choices=["eager", "graph"], default="eager")
+    ap.add_argument("--graph-reuse", action="store_true",
+                    help="graph mode: keep the captured iterations across problems (GraphSession; opt-in: "
+                         "its 100-problem gaussian run solved fewer problems, profiles/r5/cfg5_graph_reuse.md)")
     ap.add_argument("--out", default=None, help="directory for eval.py's tables + summary.json")
     ap.add_argument("--runtime", action="store_true",
                     help="eval.py compare_runtime instead: runtimes.txt / memory.txt per MC setting")
@@ -570,7 +574,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     results = {}
-    sessions = {}  # graph mode: the captured iterations, kept across this rank's problems
+    sessions = {} if args.graph_reuse else None  # graph mode: captured iterations kept across problems
     for i in mine:
         results[i] = run_problem(scene, problems[i], noise_type, sigma, gamma, args.mc_samples,
                                  args.initial_perturbation, args.num_iterations, bool(args.adaptive_regularization),
