@@ -2040,7 +2040,8 @@ static int rast_fwd_prepared(const PRRastArgs& a, const FaceRec* fr, const uint2
   // two waves per 4x4 tile (rast_fwd_kernel NW = 2; PR_RAST_DUO=1, read per call)
   const char* duo = getenv("PR_RAST_DUO");
   const int nw = sl == 4 && duo && duo[0] == '1' ? 2 : 1;
-  const size_t lds = rast_fwd_lds(a.K, sl, nw);
+  size_t lds = rast_fwd_lds(a.K, sl, nw);
+  if (const char* e = getenv("PR_RAST_LDS_MIN")) lds = std::max(lds, (size_t)atol(e));  // occupancy sweeps
   if (lds > 160 * 1024) return set_error(PR_ERR_ARG, "rast_fwd: faces_per_pixel too large for the LDS queue (max 300)");
   launch_rast_fwd(a, fr, fbox, sl, frag, lds, bins, st, nw);
   if (int e = check_launch("rast_fwd")) return e;
