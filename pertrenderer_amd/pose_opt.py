@@ -22,7 +22,10 @@ Execution modes (``--mode``):
                 gradient norm, best-loss test).  This is what ``python eval.py`` does.
   * ``graph``:  the same iteration as a captured HIP graph (fwd + bwd + guard + Adam + best-loss
                 tracking + the smoothing-gradient EMA, all on the device); the host only decides the
-                adaptive schedule every 50 iterations and re-captures when it changes S or blur.
+                adaptive schedule every 50 iterations, applies it in place (device smoothing leaves,
+                blur radius, learning rate) and captures again only when it changes the sample
+                counts.  compare_pose_opt keeps the captured iterations across its problems (one
+                GraphSession per noise type; ``--no-graph-reuse`` captures per problem).
                 Numerically the same algorithm (same Philox noise stream per iteration).
 
 Multi-GPU (``torchrun --nproc-per-node G -m pertrenderer_amd.pose_opt``): the independent problems
@@ -258,7 +261,14 @@ class _CapturedIteration:
         R = so3_exponential_map(self.log_rot)
         predicted = mesh.update_padded(Rotate(R).transform_points(mesh.verts_padded()))
         images = self.renderer(predicted, cameras=self.scene.cameras[0], lights=self.scene.lights)
-        return ((images[..., :3] - self.target) ** 2).mean()
+        d = (images[..., :3] - self.target) ** 2
+        # eval.py's .mean() in two single-workgroup stages (rows, then their sum).  torch's one-pass
+        # mean of a whole frame reduces across workgroups through scratch memory, and on this
+        # PyTorch-ROCm build an eager BLAS call (init_renderers' bmm, angle_deg) between the
+        # replays of a kept graph leaves that reduction wrong: GraphSession's reused graphs recorded
+        # stale losses and tracked the wrong best pose (tools/scratch/graph_mean_repro.py,
+        # profiles/r5/cfg5_graph_reuse.md).  Same gradient: 1/numel per element.
+        return d.reshape(d.shape[0] * d.shape[1], -1).sum(1).sum() / d.numel()
 
     def _body(self):
         st, log_rot = self.st, self.log_rot
@@ -535,9 +545,9 @@ def main(argv=None):
     ap.add_argument("-ar", "--adaptive-regularization", type=int, default=1)
     ap.add_argument("-s", "--seed", type=int, default=1)
     ap.add_argument("--mode", choices=["eager", "graph"], default="eager")
-    ap.add_argument("--graph-reuse", action="store_true",
-                    help="graph mode: keep the captured iterations across problems (GraphSession; opt-in: "
-                         "its 100-problem gaussian run solved fewer problems, profiles/r5/cfg5_graph_reuse.md)")
+    ap.add_argument("--no-graph-reuse", action="store_true",
+                    help="graph mode: capture every problem's iterations anew instead of keeping them across "
+                         "problems (GraphSession; profiles/r5/cfg5_graph_reuse.md)")
     ap.add_argument("--out", default=None, help="directory for eval.py's tables + summary.json")
     ap.add_argument("--runtime", action="store_true",
                     help="eval.py compare_runtime instead: runtimes.txt / memory.txt per MC setting")
@@ -574,7 +584,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     results = {}
-    sessions = {} if args.graph_reuse else None  # graph mode: captured iterations kept across problems
+    sessions = None if args.no_graph_reuse else {}  # graph mode: captured iterations kept across problems
     for i in mine:
         results[i] = run_problem(scene, problems[i], noise_type, sigma, gamma, args.mc_samples,
                                  args.initial_perturbation, args.num_iterations, bool(args.adaptive_regularization),

@@ -126,3 +126,29 @@ def test_graph_session_replays_captured_iterations(device, monkeypatch):
     assert c1 >= 2 and c2 < c1, (c1, c2)
     for r in (r1, r2):
         assert np.isfinite(r["gaussian"]["final_error"]) and r["gaussian"]["final_error"] < r["gaussian"]["init_error"]
+
+
+def test_kept_graphs_record_each_problems_losses(device):
+    """A kept (GraphSession) softras graph replayed for a later problem -- after the eager work
+    between compare_pose_opt's problems (init_renderers' bmm, angle_deg) and host synchronisations
+    -- records that problem's own losses: the same trace as a fresh capture of it.  (With torch's
+    one-pass frame mean in the captured step, the reused graphs recorded the first problem's last
+    loss at every iteration: pose_opt._CapturedIteration._forward.)"""
+    torch.manual_seed(1)
+    scene = pose_opt.Scene(device, 256)  # a whole 256^2 frame: torch's mean reduces it across workgroups
+    probs = pose_opt.make_problems(scene, 2, ["softras", "gaussian"], 20.0)
+    traces = {}
+    for use in (False, True):
+        sessions = {} if use else None
+        for i, (target_rgb, R_true, log_rot_init) in enumerate(probs):
+            _, rs = pose_opt.init_renderers(scene, R_true, noise_type=["softras"])
+            torch.cuda.synchronize()
+            ses = None if sessions is None else sessions.setdefault("softras", pose_opt.GraphSession())
+            best, info = pose_opt.optimize_pose_graph(scene, log_rot_init, rs[0], target_rgb, Niter=800, session=ses)
+            torch.cuda.synchronize()
+            pose_opt.angle_deg(best, R_true)
+            traces[(use, i)] = np.asarray(info["loss_values"])
+    fresh, kept = traces[(False, 1)], traces[(True, 1)]
+    assert len(np.unique(kept[:100].round(9))) > 10, kept[:5]
+    np.testing.assert_allclose(kept[:20], fresh[:20], rtol=1e-4)
+    assert abs(kept[:100].mean() - fresh[:100].mean()) < 1e-3 * fresh[:100].mean()
