@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 18
+#define PR_ABI_VERSION 19
 
 /* error codes */
 #define PR_OK 0
@@ -402,6 +402,32 @@ int pr_so3_exp_fwd(const PRSO3Args* args, void* stream);
 int pr_so3_exp_bwd(const PRSO3Args* args, void* stream);
 int pr_rotate_fwd(const PRRotateArgs* args, void* stream);
 int pr_rotate_bwd(const PRRotateArgs* args, void* stream);
+
+/* One optimize_pose iteration's bookkeeping after loss.backward() and before optimizer.step()
+ * (experiments/eval.py:356-358, 372-379, 382-385), as one single-thread kernel for a captured
+ * graph (ABI 19).  With t = *it:
+ *   losses[t] = *loss; if (*loss < *best_loss) { *best_loss = *loss; best = log_rot }
+ *   gnorms[t] = |grad|; if (|grad| > 1000) grad = 1e-5 * N(0, 1) (Philox keyed by *seed and t)
+ *   post: v[i] = 0.9 v[i] + 0.1 *leaf_grad[i]; *leaf_grad[i] = 0   (i < 3, null leaves skipped)
+ *   *it = t + 1                                                       (t < niter checked)   */
+typedef struct PRPoseStepArgs {
+  const float* loss;           /* 0-d */
+  const float* log_rot;        /* [n] */
+  float* grad;                 /* [n] log_rot's gradient (the guard rewrites it) */
+  int64_t* it;                 /* iteration counter */
+  float* losses;               /* [niter] */
+  float* gnorms;               /* [niter] */
+  float* best_loss;            /* 0-d */
+  float* best;                 /* [n] */
+  float* v;                    /* [3] EMA of the smoothing gradients (post) */
+  float* leaf_grad[3];         /* sigma / gamma / alpha gradients (post), nullable */
+  const uint64_t* seed;        /* guard noise key, nullable (then key 0) */
+  int64_t niter;
+  int32_t n;                   /* log_rot's numel (<= 64) */
+  int32_t post;                /* eval.py's adapt_reg and i > 100 */
+} PRPoseStepArgs;
+
+int pr_pose_step(const PRPoseStepArgs* args, void* stream);
 
 int pr_abi_version(void);
 const char* pr_last_error(void);

@@ -105,6 +105,12 @@ class PRRotateArgs(C.Structure):
                 ("out", _vp), ("grad_out", _vp), ("grad_points", _vp), ("grad_R", _vp)]
 
 
+class PRPoseStepArgs(C.Structure):
+    _fields_ = [("loss", _vp), ("log_rot", _vp), ("grad", _vp), ("it", _vp), ("losses", _vp), ("gnorms", _vp),
+                ("best_loss", _vp), ("best", _vp), ("v", _vp), ("leaf_grad", _vp * 3), ("seed", _vp),
+                ("niter", C.c_int64), ("n", C.c_int32), ("post", C.c_int32)]
+
+
 PR_TEX_GIVEN = 0
 PR_TEX_UV = 1
 PR_TEX_VERTEX = 2
@@ -151,6 +157,7 @@ EXPORTS = {
     "pr_project_fwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
     "pr_project_bwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
     "pr_project_rast_fwd": (C.c_int, [C.POINTER(PRProjectArgs), C.POINTER(PRRastArgs), _vp]),
+    "pr_pose_step": (C.c_int, [C.POINTER(PRPoseStepArgs), _vp]),
     "pr_so3_exp_fwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
     "pr_so3_exp_bwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
@@ -162,7 +169,7 @@ EXPORTS = {
     "pr_vert_normals_fwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
     "pr_vert_normals_bwd": (C.c_int, [C.POINTER(PRNormalsArgs), _vp]),
 }
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 _lib = None
 

@@ -133,10 +133,56 @@ __global__ void __launch_bounds__(kThreads) rotate_bwd_kernel(PRRotateArgs a) {
   }
 }
 
+// One optimize_pose iteration's bookkeeping (pr_pose_step, PRPoseStepArgs): the loss and
+// gradient-norm records, the best-loss pose, eval.py's grad-norm guard, the post-phase EMA of the
+// smoothing gradients and their zeroing, the iteration counter.  A captured step otherwise spends
+// ~20 one-element torch kernels on it (index_copy, where, norm, randn, mul, add, fill, copy).
+__global__ void pose_step_kernel(PRPoseStepArgs a) {
+  if (threadIdx.x != 0) return;
+  const int64_t t = *a.it;
+  if (t < 0 || t >= a.niter) return;  // past the records (the host sizes them): nothing written
+  const float loss = *a.loss;
+  a.losses[t] = loss;
+  if (loss < *a.best_loss) {  // eval.py:372-374 (the pose that produced this loss, before the step)
+    *a.best_loss = loss;
+    for (int i = 0; i < a.n; ++i) a.best[i] = a.log_rot[i];
+  }
+  float ss = 0.f;
+  for (int i = 0; i < a.n; ++i) ss += a.grad[i] * a.grad[i];
+  const float gn = sqrtf(ss);
+  a.gnorms[t] = gn;
+  if (gn > 1000.f) {  // eval.py:375-379: grad = 1e-5 * normal (Philox draws keyed by the seed, t)
+    const uint64_t key = (a.seed ? a.seed[0] : 0ull) ^ 0x67756172645f706full;
+    for (int i = 0; i < a.n; i += 4) {
+      const U4 u = philox4x32_10(U4{(uint32_t)t, (uint32_t)(t >> 32), (uint32_t)i, 0x706f7365u}, (uint32_t)key,
+                                 (uint32_t)(key >> 32));
+      float e[4];
+      gauss4(u, e);
+      for (int j = 0; j < 4 && i + j < a.n; ++j) a.grad[i + j] = 1e-5f * e[j];
+    }
+  }
+  if (a.post) {  // eval.py:382-385
+    for (int i = 0; i < 3; ++i) {
+      if (!a.leaf_grad[i]) continue;
+      a.v[i] = 0.9f * a.v[i] + 0.1f * *a.leaf_grad[i];
+      *a.leaf_grad[i] = 0.f;
+    }
+  }
+  *a.it = t + 1;
+}
+
 }  // namespace
 }  // namespace pr
 
 using namespace pr;
+
+extern "C" int pr_pose_step(const PRPoseStepArgs* a, void* stream) {
+  if (!a || !a->loss || !a->log_rot || !a->grad || !a->it || !a->losses || !a->gnorms || !a->best_loss || !a->best ||
+      a->n <= 0 || a->n > 64 || a->niter <= 0 || (a->post && !a->v))
+    return set_error(PR_ERR_ARG, "pose_step: bad args");
+  pose_step_kernel<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(*a);
+  return check_launch("pose_step");
+}
 
 extern "C" int pr_so3_exp_fwd(const PRSO3Args* a, void* stream) {
   if (!a || a->N < 0 || (a->N > 0 && (!a->log_rot || !a->R))) return set_error(PR_ERR_ARG, "so3_exp_fwd: bad args");

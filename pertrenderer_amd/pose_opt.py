@@ -41,6 +41,7 @@ import time
 import numpy as np
 import torch
 
+from . import _native as nat
 from . import random_rasterizer as rr
 from .renderer import (BlendParams, HardPhongShader, Meshes, MeshRasterizer, MeshRenderer, OpenGLPerspectiveCameras,
                        PointLights, RasterizationSettings, Textures, load_obj, look_at_view_transform)
@@ -276,23 +277,19 @@ class _CapturedIteration:
         loss = self._forward()
         log_rot.grad.zero_()
         loss.backward()
-        with torch.no_grad():
-            it = st["it"].view(1)
-            st["losses"].index_copy_(0, it, loss.detach().view(1))
-            better = loss.detach() < st["best_loss"]
-            st["best_loss"].copy_(torch.where(better, loss.detach(), st["best_loss"]))
-            st["best"].copy_(torch.where(better, log_rot.detach(), st["best"]))
-            gn = torch.linalg.vector_norm(log_rot.grad)
-            st["gnorms"].index_copy_(0, it, gn.view(1))
-            log_rot.grad.copy_(torch.where(gn > 1000.0, 1e-5 * torch.randn_like(log_rot.grad), log_rot.grad))
+        # the records, best-loss pose, grad-norm guard, (post) smoothing-gradient EMA and the
+        # iteration counter in one native kernel (pr_pose_step) instead of ~20 one-element torch ops
+        a = nat.PRPoseStepArgs()
+        a.loss, a.log_rot, a.grad, a.it = nat.ptr(loss), nat.ptr(log_rot), nat.ptr(log_rot.grad), nat.ptr(st["it"])
+        a.losses, a.gnorms = nat.ptr(st["losses"]), nat.ptr(st["gnorms"])
+        a.best_loss, a.best, a.v = nat.ptr(st["best_loss"]), nat.ptr(st["best"]), nat.ptr(st["v"])
+        if self.post:
+            for i, l in enumerate(self.leaves[:3]):
+                a.leaf_grad[i] = nat.ptr(l.grad) if torch.is_tensor(l) and l.grad is not None else None
+        a.seed = nat.ptr(self.seed.tensor)
+        a.niter, a.n, a.post = st["losses"].numel(), log_rot.numel(), int(self.post)
+        nat.call("pr_pose_step", "pose_step", loss, a)
         self.opt.step()
-        with torch.no_grad():
-            if self.post:
-                g = torch.stack([l.grad.reshape(()) for l in self.leaves])
-                st["v"].mul_(0.9).add_(0.1 * g)
-                for l in self.leaves:
-                    l.grad.zero_()
-            st["it"].add_(1)
 
     def replay(self, n):
         for _ in range(n):
