@@ -429,6 +429,29 @@ typedef struct PRPoseStepArgs {
 
 int pr_pose_step(const PRPoseStepArgs* args, void* stream);
 
+/* eval.py's image loss ((images[..., :3] - target) ** 2).mean() (experiments/eval.py:352-353) as
+ * two kernels forward (per-workgroup partial sums, one fixed-order finalize) and one backward
+ * (ABI 19): image (P, C >= 3) with P = N*H*W pixels, target (P or P / N, 3) (one target frame
+ * broadcast over the batch when target_batched == 0).
+ *   fwd: *loss = sum_{p, c < 3} (image[p, c] - target[p, c])^2 / (3 P)
+ *   bwd: grad_image[p, c] = (*grad_loss / (3 P)) * (2 (image[p, c] - target[p, c])), 0 for c >= 3 */
+typedef struct PRRgbMseArgs {
+  int64_t P;                   /* pixels */
+  int32_t C;                   /* image channels (>= 3) */
+  int32_t HW;                  /* pixels per frame (target broadcast) */
+  int32_t target_batched;
+  const float* image;          /* (P, C) */
+  const float* target;         /* (P, 3) or (HW, 3) */
+  float* loss;                 /* fwd out, 0-d */
+  float* partials;             /* fwd workspace: pr_rgb_mse_workspace floats */
+  const float* grad_loss;      /* bwd in, 0-d */
+  float* grad_image;           /* bwd out (P, C) */
+} PRRgbMseArgs;
+
+size_t pr_rgb_mse_workspace(int64_t P);  /* floats */
+int pr_rgb_mse_fwd(const PRRgbMseArgs* args, void* stream);
+int pr_rgb_mse_bwd(const PRRgbMseArgs* args, void* stream);
+
 int pr_abi_version(void);
 const char* pr_last_error(void);
 

@@ -105,6 +105,12 @@ class PRRotateArgs(C.Structure):
                 ("out", _vp), ("grad_out", _vp), ("grad_points", _vp), ("grad_R", _vp)]
 
 
+class PRRgbMseArgs(C.Structure):
+    _fields_ = [("P", C.c_int64), ("C", C.c_int32), ("HW", C.c_int32), ("target_batched", C.c_int32),
+                ("image", _vp), ("target", _vp), ("loss", _vp), ("partials", _vp), ("grad_loss", _vp),
+                ("grad_image", _vp)]
+
+
 class PRPoseStepArgs(C.Structure):
     _fields_ = [("loss", _vp), ("log_rot", _vp), ("grad", _vp), ("it", _vp), ("losses", _vp), ("gnorms", _vp),
                 ("best_loss", _vp), ("best", _vp), ("v", _vp), ("leaf_grad", _vp * 3), ("seed", _vp),
@@ -158,6 +164,9 @@ EXPORTS = {
     "pr_project_bwd": (C.c_int, [C.POINTER(PRProjectArgs), _vp]),
     "pr_project_rast_fwd": (C.c_int, [C.POINTER(PRProjectArgs), C.POINTER(PRRastArgs), _vp]),
     "pr_pose_step": (C.c_int, [C.POINTER(PRPoseStepArgs), _vp]),
+    "pr_rgb_mse_workspace": (C.c_size_t, [C.c_int64]),
+    "pr_rgb_mse_fwd": (C.c_int, [C.POINTER(PRRgbMseArgs), _vp]),
+    "pr_rgb_mse_bwd": (C.c_int, [C.POINTER(PRRgbMseArgs), _vp]),
     "pr_so3_exp_fwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
     "pr_so3_exp_bwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),

@@ -171,10 +171,92 @@ __global__ void pose_step_kernel(PRPoseStepArgs a) {
   *a.it = t + 1;
 }
 
+// eval.py's RGB loss: per-workgroup partial sums in a fixed order, then one workgroup sums the
+// partials in block order (deterministic); the backward is one elementwise pass
+constexpr int kMseBlocks = 512;
+PR_DEV int64_t mse_tidx(const PRRgbMseArgs& a, int64_t p) { return a.target_batched ? p : p % a.HW; }
+
+__global__ void __launch_bounds__(kThreads) rgb_mse_partial_kernel(PRRgbMseArgs a) {
+  __shared__ float red[kThreads / 64];
+  float acc = 0.f;
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < a.P; p += (int64_t)gridDim.x * kThreads) {
+    const float* im = a.image + p * a.C;
+    const float* t = a.target + mse_tidx(a, p) * 3;
+    const float d0 = im[0] - t[0], d1 = im[1] - t[1], d2 = im[2] - t[2];
+    acc += (d0 * d0 + d1 * d1) + d2 * d2;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < kThreads / 64; ++w) s += red[w];
+    a.partials[blockIdx.x] = s;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) rgb_mse_finalize_kernel(PRRgbMseArgs a, int nblk) {
+  __shared__ float red[kThreads / 64];
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += kThreads) acc += a.partials[b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < kThreads / 64; ++w) s += red[w];
+    *a.loss = s / (float)(a.P * 3);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) rgb_mse_bwd_kernel(PRRgbMseArgs a) {
+  const float g = *a.grad_loss / (float)(a.P * 3);
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < a.P; p += (int64_t)gridDim.x * kThreads) {
+    const float* im = a.image + p * a.C;
+    const float* t = a.target + mse_tidx(a, p) * 3;
+    float* o = a.grad_image + p * a.C;
+    o[0] = g * (2.f * (im[0] - t[0]));
+    o[1] = g * (2.f * (im[1] - t[1]));
+    o[2] = g * (2.f * (im[2] - t[2]));
+    for (int c = 3; c < a.C; ++c) o[c] = 0.f;
+  }
+}
+
+int mse_blocks(int64_t P) { return (int)std::max<int64_t>(1, std::min<int64_t>((P + kThreads - 1) / kThreads, kMseBlocks)); }
+
+int mse_check(const PRRgbMseArgs* a) {
+  if (!a || a->P <= 0 || a->C < 3 || !a->image || !a->target || (!a->target_batched && (a->HW <= 0 || a->P % a->HW)))
+    return set_error(PR_ERR_ARG, "rgb_mse: bad args");
+  return PR_OK;
+}
+
 }  // namespace
 }  // namespace pr
 
 using namespace pr;
+
+extern "C" size_t pr_rgb_mse_workspace(int64_t P) { return P > 0 ? (size_t)mse_blocks(P) : 1; }
+
+extern "C" int pr_rgb_mse_fwd(const PRRgbMseArgs* a, void* stream) {
+  if (int e = mse_check(a)) return e;
+  if (!a->loss || !a->partials) return set_error(PR_ERR_ARG, "rgb_mse_fwd: loss / workspace missing");
+  const int nb = mse_blocks(a->P);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  rgb_mse_partial_kernel<<<nb, kThreads, 0, st>>>(*a);
+  if (int e = check_launch("rgb_mse_partial")) return e;
+  rgb_mse_finalize_kernel<<<1, kThreads, 0, st>>>(*a, nb);
+  return check_launch("rgb_mse_finalize");
+}
+
+extern "C" int pr_rgb_mse_bwd(const PRRgbMseArgs* a, void* stream) {
+  if (int e = mse_check(a)) return e;
+  if (!a->grad_loss || !a->grad_image) return set_error(PR_ERR_ARG, "rgb_mse_bwd: grads missing");
+  rgb_mse_bwd_kernel<<<(int)std::min<int64_t>((a->P + kThreads - 1) / kThreads, 4096), kThreads, 0,
+                       reinterpret_cast<hipStream_t>(stream)>>>(*a);
+  return check_launch("rgb_mse_bwd");
+}
 
 extern "C" int pr_pose_step(const PRPoseStepArgs* a, void* stream) {
   if (!a || !a->loss || !a->log_rot || !a->grad || !a->it || !a->losses || !a->gnorms || !a->best_loss || !a->best ||

@@ -229,6 +229,46 @@ def _renew_adam(opt, log_rot, lr):
         opt.param_groups[0]["lr"].fill_(float(lr))
 
 
+class _RgbMse(torch.autograd.Function):
+    """((images[..., :3] - target) ** 2).mean() (experiments/eval.py:352-353) on the native kernels
+    pr_rgb_mse_fwd / pr_rgb_mse_bwd: images (N,H,W,C>=3) float32, target (H,W,3) broadcast over
+    the batch or (N,H,W,3).  Sums in a fixed order (deterministic); gradient (g / 3P) * 2 (x - t)."""
+
+    @staticmethod
+    def _args(img, t):
+        N, H, W, C = img.shape
+        if img.dtype != torch.float32 or t.dtype != torch.float32 or C < 3 or t.shape[-1] != 3:
+            raise ValueError("rgb_mse: float32 (N,H,W,C>=3) images and (..,H,W,3) target expected")
+        if t.numel() not in (H * W * 3, N * H * W * 3):
+            raise ValueError(f"rgb_mse: target {tuple(t.shape)} does not broadcast to {(N, H, W, 3)}")
+        a = nat.PRRgbMseArgs()
+        a.P, a.C, a.HW = N * H * W, C, H * W
+        a.target_batched = int(t.numel() == N * H * W * 3 and N > 1)
+        a.image, a.target = nat.ptr(img), nat.ptr(t)
+        return a
+
+    @staticmethod
+    def forward(ctx, images, target):
+        img, t = images.detach().contiguous(), target.detach().contiguous()
+        a = _RgbMse._args(img, t)
+        loss = torch.empty((), dtype=torch.float32, device=img.device)
+        part = torch.empty(nat.load().pr_rgb_mse_workspace(a.P), dtype=torch.float32, device=img.device)
+        a.loss, a.partials = nat.ptr(loss), nat.ptr(part)
+        nat.call("pr_rgb_mse_fwd", "rgb_mse_fwd", img, a)
+        ctx.save_for_backward(img, t)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        img, t = ctx.saved_tensors
+        a = _RgbMse._args(img, t)
+        gi = torch.empty_like(img)
+        gl = g.detach().to(torch.float32).contiguous()
+        a.grad_loss, a.grad_image = nat.ptr(gl), nat.ptr(gi)
+        nat.call("pr_rgb_mse_bwd", "rgb_mse_bwd", img, a)
+        return gi, None
+
+
 class _CapturedIteration:
     """One optimize_pose iteration (eval.py:343-388) as a HIP graph for a fixed schedule state
     (nb_samples, blur_radius, lr): noise key advance, so3 pose, render, L2 loss, backward,
@@ -262,14 +302,13 @@ class _CapturedIteration:
         R = so3_exponential_map(self.log_rot)
         predicted = mesh.update_padded(Rotate(R).transform_points(mesh.verts_padded()))
         images = self.renderer(predicted, cameras=self.scene.cameras[0], lights=self.scene.lights)
-        d = (images[..., :3] - self.target) ** 2
-        # eval.py's .mean() in two single-workgroup stages (rows, then their sum).  torch's one-pass
-        # mean of a whole frame reduces across workgroups through scratch memory, and on this
-        # PyTorch-ROCm build an eager BLAS call (init_renderers' bmm, angle_deg) between the
-        # replays of a kept graph leaves that reduction wrong: GraphSession's reused graphs recorded
-        # stale losses and tracked the wrong best pose (tools/scratch/graph_mean_repro.py,
-        # profiles/r5/cfg5_graph_reuse.md).  Same gradient: 1/numel per element.
-        return d.reshape(d.shape[0] * d.shape[1], -1).sum(1).sum() / d.numel()
+        # eval.py:352-353's ((images[..., :3] - target) ** 2).mean() as two native kernels forward
+        # and one backward (pr_rgb_mse_*) instead of ~10 torch kernels.  It also keeps the loss off
+        # torch's one-pass cross-workgroup mean, which on this PyTorch-ROCm build an eager BLAS
+        # call (init_renderers' bmm, angle_deg) between the replays of a kept graph leaves wrong:
+        # GraphSession's reused graphs recorded stale losses with it and tracked the wrong best
+        # pose (tools/scratch/graph_mean_repro.py, profiles/r5/cfg5_graph_reuse.md).
+        return _RgbMse.apply(images, self.target)
 
     def _body(self):
         st, log_rot = self.st, self.log_rot

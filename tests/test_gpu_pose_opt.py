@@ -152,3 +152,21 @@ def test_kept_graphs_record_each_problems_losses(device):
     assert len(np.unique(kept[:100].round(9))) > 10, kept[:5]
     np.testing.assert_allclose(kept[:20], fresh[:20], rtol=1e-4)
     assert abs(kept[:100].mean() - fresh[:100].mean()) < 1e-3 * fresh[:100].mean()
+
+
+@pytest.mark.parametrize("shape,tshape", [((1, 256, 256, 4), (256, 256, 3)), ((2, 33, 17, 4), (2, 33, 17, 3)),
+                                          ((3, 8, 8, 3), (8, 8, 3))])
+def test_native_rgb_loss_matches_torch(device, shape, tshape):
+    """The captured step's loss (pose_opt._RgbMse, pr_rgb_mse_fwd / _bwd) against eval.py:352-353's
+    torch expression: value and image gradient at 1e-6 relative (fp32 summation order only)."""
+    torch.manual_seed(5)
+    img = torch.rand(shape, device=device, requires_grad=True)
+    t = torch.rand(tshape, device=device)
+    ref = ((img[..., :3] - t) ** 2).mean()
+    (gref,) = torch.autograd.grad(ref * 3.0, img)
+    out = pose_opt._RgbMse.apply(img, t)
+    (g,) = torch.autograd.grad(out * 3.0, img)
+    assert abs(float(out) - float(ref)) <= 1e-6 * abs(float(ref))
+    torch.testing.assert_close(g, gref, rtol=1e-6, atol=1e-9)
+    if shape[-1] > 3:
+        assert float(g[..., 3:].abs().max()) == 0.0
