@@ -314,8 +314,12 @@ class _CapturedIteration:
         st, log_rot = self.st, self.log_rot
         self.seed.advance()
         loss = self._forward()
-        log_rot.grad.zero_()
+        # optimizer.zero_grad() as set_to_none: the backward's d log_rot buffer becomes the gradient
+        # (AccumulateGrad takes it) instead of a fill and an add into the previous one
+        log_rot.grad = None
         loss.backward()
+        if log_rot.grad is None:
+            raise RuntimeError("pose step: the loss does not reach log_rot")
         # the records, best-loss pose, grad-norm guard, (post) smoothing-gradient EMA and the
         # iteration counter in one native kernel (pr_pose_step) instead of ~20 one-element torch ops
         a = nat.PRPoseStepArgs()
