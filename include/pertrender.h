@@ -408,7 +408,9 @@ int pr_rotate_bwd(const PRRotateArgs* args, void* stream);
  * graph (ABI 19).  With t = *it:
  *   losses[t] = *loss; if (*loss < *best_loss) { *best_loss = *loss; best = log_rot }
  *   gnorms[t] = |grad|; if (|grad| > 1000) grad = 1e-5 * N(0, 1) (Philox keyed by *seed and t)
- *   post: v[i] = 0.9 v[i] + 0.1 *leaf_grad[i]; *leaf_grad[i] = 0   (i < 3, null leaves skipped)
+ *   acc[i] += *leaf_grad[i]  (the smoothing leaves' gradients accumulate across iterations, as
+ *                             their .grad does in eval.py; i < 3, null leaves skipped)
+ *   post: v[i] = 0.9 v[i] + 0.1 acc[i]; acc[i] = 0
  *   *it = t + 1                                                       (t < niter checked)   */
 typedef struct PRPoseStepArgs {
   const float* loss;           /* 0-d */
@@ -420,7 +422,8 @@ typedef struct PRPoseStepArgs {
   float* best_loss;            /* 0-d */
   float* best;                 /* [n] */
   float* v;                    /* [3] EMA of the smoothing gradients (post) */
-  float* leaf_grad[3];         /* sigma / gamma / alpha gradients (post), nullable */
+  float* acc;                  /* [3] the smoothing gradients accumulated since the last EMA */
+  const float* leaf_grad[3];   /* this iteration's sigma / gamma / alpha gradients, nullable */
   const uint64_t* seed;        /* guard noise key, nullable (then key 0) */
   int64_t niter;
   int32_t n;                   /* log_rot's numel (<= 64) */

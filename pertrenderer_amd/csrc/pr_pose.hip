@@ -134,8 +134,8 @@ __global__ void __launch_bounds__(kThreads) rotate_bwd_kernel(PRRotateArgs a) {
 }
 
 // One optimize_pose iteration's bookkeeping (pr_pose_step, PRPoseStepArgs): the loss and
-// gradient-norm records, the best-loss pose, eval.py's grad-norm guard, the post-phase EMA of the
-// smoothing gradients and their zeroing, the iteration counter.  A captured step otherwise spends
+// gradient-norm records, the best-loss pose, eval.py's grad-norm guard, the accumulation of the
+// smoothing gradients and (post) their EMA and reset, the iteration counter.  A captured step otherwise spends
 // ~20 one-element torch kernels on it (index_copy, where, norm, randn, mul, add, fill, copy).
 __global__ void pose_step_kernel(PRPoseStepArgs a) {
   if (threadIdx.x != 0) return;
@@ -161,12 +161,15 @@ __global__ void pose_step_kernel(PRPoseStepArgs a) {
       for (int j = 0; j < 4 && i + j < a.n; ++j) a.grad[i + j] = 1e-5f * e[j];
     }
   }
-  if (a.post) {  // eval.py:382-385
-    for (int i = 0; i < 3; ++i) {
-      if (!a.leaf_grad[i]) continue;
-      a.v[i] = 0.9f * a.v[i] + 0.1f * *a.leaf_grad[i];
-      *a.leaf_grad[i] = 0.f;
+  for (int i = 0; i < 3; ++i) {  // eval.py:382-385: the leaves' .grad accumulates until the EMA reads it
+    if (!a.acc) break;
+    float g = a.acc[i];
+    if (a.leaf_grad[i]) g += *a.leaf_grad[i];
+    if (a.post) {
+      a.v[i] = 0.9f * a.v[i] + 0.1f * g;
+      g = 0.f;
     }
+    a.acc[i] = g;
   }
   *a.it = t + 1;
 }
@@ -260,7 +263,7 @@ extern "C" int pr_rgb_mse_bwd(const PRRgbMseArgs* a, void* stream) {
 
 extern "C" int pr_pose_step(const PRPoseStepArgs* a, void* stream) {
   if (!a || !a->loss || !a->log_rot || !a->grad || !a->it || !a->losses || !a->gnorms || !a->best_loss || !a->best ||
-      a->n <= 0 || a->n > 64 || a->niter <= 0 || (a->post && !a->v))
+      a->n <= 0 || a->n > 64 || a->niter <= 0 || (a->post && (!a->v || !a->acc)))
     return set_error(PR_ERR_ARG, "pose_step: bad args");
   pose_step_kernel<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(*a);
   return check_launch("pose_step");

@@ -281,18 +281,18 @@ class _CapturedIteration:
         leaves = list(renderer.shader.get_smoothing())
         self.leaves = leaves
         # warm-up pass on a side stream (lazy allocations and caches outside the graph); it must
-        # not change the optimisation state: the gradients it accumulates are restored
-        saved = [l.grad.detach().clone() for l in leaves]
+        # not change the optimisation state, which lives in st (the smoothing gradients' running
+        # sum is st["acc"]): the gradients it leaves are dropped
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             self.seed.advance()
             self._forward().backward()
         torch.cuda.current_stream().wait_stream(side)
-        with torch.no_grad():
-            for l, g in zip(leaves, saved):
-                l.grad.copy_(g)
-            log_rot.grad.zero_()
+        for l in leaves:
+            if torch.is_tensor(l):
+                l.grad = None
+        log_rot.grad = None
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=pool):
             self._body()
@@ -314,9 +314,14 @@ class _CapturedIteration:
         st, log_rot = self.st, self.log_rot
         self.seed.advance()
         loss = self._forward()
-        # optimizer.zero_grad() as set_to_none: the backward's d log_rot buffer becomes the gradient
-        # (AccumulateGrad takes it) instead of a fill and an add into the previous one
+        # optimizer.zero_grad() as set_to_none, and the smoothing leaves' gradients too: the
+        # backward's own buffers become the gradients (AccumulateGrad takes them) instead of a fill
+        # and an add per leaf; pr_pose_step keeps the leaves' running sum (eval.py accumulates
+        # sigma.grad etc. until the EMA reads and zeroes them) in st["acc"]
         log_rot.grad = None
+        for l in self.leaves:
+            if torch.is_tensor(l):
+                l.grad = None
         loss.backward()
         if log_rot.grad is None:
             raise RuntimeError("pose step: the loss does not reach log_rot")
@@ -325,10 +330,12 @@ class _CapturedIteration:
         a = nat.PRPoseStepArgs()
         a.loss, a.log_rot, a.grad, a.it = nat.ptr(loss), nat.ptr(log_rot), nat.ptr(log_rot.grad), nat.ptr(st["it"])
         a.losses, a.gnorms = nat.ptr(st["losses"]), nat.ptr(st["gnorms"])
-        a.best_loss, a.best, a.v = nat.ptr(st["best_loss"]), nat.ptr(st["best"]), nat.ptr(st["v"])
-        if self.post:
-            for i, l in enumerate(self.leaves[:3]):
-                a.leaf_grad[i] = nat.ptr(l.grad) if torch.is_tensor(l) and l.grad is not None else None
+        a.best_loss, a.best, a.v, a.acc = nat.ptr(st["best_loss"]), nat.ptr(st["best"]), nat.ptr(st["v"]), nat.ptr(st["acc"])
+        for i, l in enumerate(self.leaves[:3]):
+            g = l.grad if torch.is_tensor(l) else None
+            if g is not None and (g.dtype != torch.float32 or g.numel() != 1 or not g.is_cuda):
+                raise RuntimeError("pose step: smoothing gradients must be one-element float32 device tensors")
+            a.leaf_grad[i] = nat.ptr(g)
         a.seed = nat.ptr(self.seed.tensor)
         a.niter, a.n, a.post = st["losses"].numel(), log_rot.numel(), int(self.post)
         nat.call("pr_pose_step", "pose_step", loss, a)
@@ -376,7 +383,8 @@ class GraphSession:
             self.target = target_rgb[0].clone()
             self.st = dict(it=torch.zeros((), dtype=torch.int64, device=dev), losses=torch.zeros(Niter, device=dev),
                            gnorms=torch.zeros(Niter, device=dev), best_loss=torch.full((), float("inf"), device=dev),
-                           best=self.log_rot.detach().clone(), v=torch.zeros(3, device=dev))
+                           best=self.log_rot.detach().clone(), v=torch.zeros(3, device=dev),
+                           acc=torch.zeros(3, device=dev))
             self.opt = _fresh_adam(self.log_rot, lr_init)
             self.blur = torch.tensor(self.start["blur"], dtype=torch.float32, device=dev)
         else:
@@ -389,14 +397,15 @@ class GraphSession:
                              (sh.smoothagg.alpha, z["alpha"])):
                     if torch.is_tensor(t):
                         t.fill_(v)
-                        t.grad.zero_()
+                        t.grad = None
                 if z["nb"][0] is not None:
                     sh.smoothrast.nb_samples = z["nb"][0]
                 if z["nb"][1] is not None:
                     sh.smoothagg.nb_samples = z["nb"][1]
                 self.blur.fill_(z["blur"])
                 self.log_rot.copy_(init_pose.to(dev))
-                self.log_rot.grad.zero_()
+                if self.log_rot.grad is not None:
+                    self.log_rot.grad.zero_()
                 self.target.copy_(target_rgb[0])
                 st = self.st
                 st["it"].zero_()
@@ -405,6 +414,7 @@ class GraphSession:
                 st["best_loss"].fill_(float("inf"))
                 st["best"].copy_(self.log_rot)
                 st["v"].zero_()
+                st["acc"].zero_()
                 self.seed.tensor.fill_(noise.draw_key())  # a new problem's key, as a new DeviceSeed draws
                 self.seed._next, self.seed._pending = 1, 0
             _renew_adam(self.opt, self.log_rot, lr_init)
