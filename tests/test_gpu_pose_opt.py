@@ -170,3 +170,45 @@ def test_native_rgb_loss_matches_torch(device, shape, tshape):
     torch.testing.assert_close(g, gref, rtol=1e-6, atol=1e-9)
     if shape[-1] > 3:
         assert float(g[..., 3:].abs().max()) == 0.0
+
+
+def test_pose_step_kernel_bookkeeping(device):
+    """pr_pose_step (the captured step's bookkeeping) against eval.py:356-358, 372-385 restated in
+    torch: records, best-loss pose, the grad-norm guard, the smoothing gradients' running sum and
+    (post) EMA, the counter."""
+    from pertrenderer_amd import _native as nat
+    f32 = dict(dtype=torch.float32, device=device)
+    st = dict(it=torch.tensor(4, dtype=torch.int64, device=device), losses=torch.zeros(8, **f32),
+              gnorms=torch.zeros(8, **f32), best_loss=torch.tensor(0.5, **f32), best=torch.zeros(1, 3, **f32),
+              v=torch.tensor([0.1, -0.2, 0.3], **f32), acc=torch.tensor([1.0, 2.0, 3.0], **f32))
+    seed = torch.tensor([12345], dtype=torch.int64, device=device)
+
+    def run(loss, log_rot, grad, leaf, post):
+        a = nat.PRPoseStepArgs()
+        a.loss, a.log_rot, a.grad, a.it = nat.ptr(loss), nat.ptr(log_rot), nat.ptr(grad), nat.ptr(st["it"])
+        a.losses, a.gnorms, a.best_loss, a.best = (nat.ptr(st[k]) for k in ("losses", "gnorms", "best_loss", "best"))
+        a.v, a.acc, a.seed = nat.ptr(st["v"]), nat.ptr(st["acc"]), nat.ptr(seed)
+        for i in range(3):
+            a.leaf_grad[i] = nat.ptr(leaf[i])
+        a.niter, a.n, a.post = 8, 3, int(post)
+        nat.call("pr_pose_step", "pose_step", loss, a)
+        torch.cuda.synchronize()
+
+    log_rot = torch.tensor([[0.1, 0.2, 0.3]], **f32)
+    grad = torch.tensor([[3.0, 4.0, 0.0]], **f32)
+    leaf = [torch.tensor(x, **f32) for x in (0.5, -1.0, 2.0)]
+    run(torch.tensor(0.25, **f32), log_rot, grad, leaf, post=False)  # better loss, small grad, pre-phase
+    assert int(st["it"]) == 5 and float(st["losses"][4]) == 0.25 and float(st["gnorms"][4]) == 5.0
+    assert float(st["best_loss"]) == 0.25 and torch.equal(st["best"], log_rot)
+    assert torch.equal(grad, torch.tensor([[3.0, 4.0, 0.0]], **f32))
+    assert torch.equal(st["acc"], torch.tensor([1.5, 1.0, 5.0], **f32))
+    assert torch.equal(st["v"], torch.tensor([0.1, -0.2, 0.3], **f32))
+    big = torch.tensor([[3000.0, 0.0, 0.0]], **f32)
+    run(torch.tensor(0.75, **f32), log_rot * 2, big, leaf, post=True)  # worse loss, guard, post-phase EMA
+    assert int(st["it"]) == 6 and float(st["losses"][5]) == 0.75 and float(st["gnorms"][5]) == 3000.0
+    assert float(st["best_loss"]) == 0.25 and torch.equal(st["best"], log_rot)
+    assert 0.0 < float(big.norm()) < 1e-3  # eval.py:375-379: 1e-5 * normal draws
+    acc = torch.tensor([1.5, 1.0, 5.0], **f32) + torch.stack(leaf)
+    ema = torch.tensor([0.1, -0.2, 0.3], **f32) * 0.9 + 0.1 * acc
+    torch.testing.assert_close(st["v"], ema, rtol=0, atol=0)
+    assert float(st["acc"].abs().max()) == 0.0
