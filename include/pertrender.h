@@ -411,10 +411,13 @@ int pr_rotate_bwd(const PRRotateArgs* args, void* stream);
  *   acc[i] += *leaf_grad[i]  (the smoothing leaves' gradients accumulate across iterations, as
  *                             their .grad does in eval.py; i < 3, null leaves skipped)
  *   post: v[i] = 0.9 v[i] + 0.1 acc[i]; acc[i] = 0
+ *   adam: optimizer.step() of torch.optim.Adam([log_rot], lr) (eval.py:380; betas 0.9 / 0.999,
+ *         eps 1e-8, torch's fused-Adam arithmetic): *step += 1; m = b1 m + (1-b1) g;
+ *         s = b2 s + (1-b2) g g; log_rot -= (lr / (1 - b1^step)) m / (sqrt(s) / sqrt(1 - b2^step) + eps)
  *   *it = t + 1                                                       (t < niter checked)   */
 typedef struct PRPoseStepArgs {
   const float* loss;           /* 0-d */
-  const float* log_rot;        /* [n] */
+  float* log_rot;              /* [n] (the Adam step updates it) */
   float* grad;                 /* [n] log_rot's gradient (the guard rewrites it) */
   int64_t* it;                 /* iteration counter */
   float* losses;               /* [niter] */
@@ -425,9 +428,14 @@ typedef struct PRPoseStepArgs {
   float* acc;                  /* [3] the smoothing gradients accumulated since the last EMA */
   const float* leaf_grad[3];   /* this iteration's sigma / gamma / alpha gradients, nullable */
   const uint64_t* seed;        /* guard noise key, nullable (then key 0) */
+  float* exp_avg;              /* [n] Adam state (adam) */
+  float* exp_avg_sq;           /* [n] */
+  float* step;                 /* 0-d float step count */
+  const float* lr;             /* 0-d learning rate */
   int64_t niter;
   int32_t n;                   /* log_rot's numel (<= 64) */
   int32_t post;                /* eval.py's adapt_reg and i > 100 */
+  int32_t adam;                /* 1: also take the Adam step */
 } PRPoseStepArgs;
 
 int pr_pose_step(const PRPoseStepArgs* args, void* stream);

@@ -114,7 +114,8 @@ class PRRgbMseArgs(C.Structure):
 class PRPoseStepArgs(C.Structure):
     _fields_ = [("loss", _vp), ("log_rot", _vp), ("grad", _vp), ("it", _vp), ("losses", _vp), ("gnorms", _vp),
                 ("best_loss", _vp), ("best", _vp), ("v", _vp), ("acc", _vp), ("leaf_grad", _vp * 3), ("seed", _vp),
-                ("niter", C.c_int64), ("n", C.c_int32), ("post", C.c_int32)]
+                ("exp_avg", _vp), ("exp_avg_sq", _vp), ("step", _vp), ("lr", _vp),
+                ("niter", C.c_int64), ("n", C.c_int32), ("post", C.c_int32), ("adam", C.c_int32)]
 
 
 PR_TEX_GIVEN = 0

@@ -171,6 +171,22 @@ __global__ void pose_step_kernel(PRPoseStepArgs a) {
     }
     a.acc[i] = g;
   }
+  if (a.adam) {  // torch.optim.Adam's fused step: its adam_math (double hyper-parameters, float state)
+    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
+    const float step = *a.step + 1.f;
+    *a.step = step;
+    const double bc1 = 1.0 - pow(b1, (double)step), bc2 = 1.0 - pow(b2, (double)step);
+    const double step_size = (double)*a.lr / bc1, bc2_sqrt = sqrt(bc2);
+    for (int i = 0; i < a.n; ++i) {
+      const float g = a.grad[i];
+      const float m = (float)(b1 * a.exp_avg[i] + (1 - b1) * g);
+      const float s = (float)(b2 * a.exp_avg_sq[i] + (1 - b2) * g * g);
+      a.exp_avg[i] = m;
+      a.exp_avg_sq[i] = s;
+      const double denom = sqrtf(s) / bc2_sqrt + eps;
+      a.log_rot[i] = (float)(a.log_rot[i] - step_size * m / denom);
+    }
+  }
   *a.it = t + 1;
 }
 
@@ -263,7 +279,8 @@ extern "C" int pr_rgb_mse_bwd(const PRRgbMseArgs* a, void* stream) {
 
 extern "C" int pr_pose_step(const PRPoseStepArgs* a, void* stream) {
   if (!a || !a->loss || !a->log_rot || !a->grad || !a->it || !a->losses || !a->gnorms || !a->best_loss || !a->best ||
-      a->n <= 0 || a->n > 64 || a->niter <= 0 || (a->post && (!a->v || !a->acc)))
+      a->n <= 0 || a->n > 64 || a->niter <= 0 || (a->post && (!a->v || !a->acc)) ||
+      (a->adam && (!a->exp_avg || !a->exp_avg_sq || !a->step || !a->lr)))
     return set_error(PR_ERR_ARG, "pose_step: bad args");
   pose_step_kernel<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(*a);
   return check_launch("pose_step");

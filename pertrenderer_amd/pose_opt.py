@@ -337,9 +337,13 @@ class _CapturedIteration:
                 raise RuntimeError("pose step: smoothing gradients must be one-element float32 device tensors")
             a.leaf_grad[i] = nat.ptr(g)
         a.seed = nat.ptr(self.seed.tensor)
+        # and optimizer.step(): the Adam update on the same thread (self.opt holds the state and the
+        # device learning rate; _renew_adam resets them in place)
+        ost = self.opt.state[log_rot]
+        a.exp_avg, a.exp_avg_sq, a.step = nat.ptr(ost["exp_avg"]), nat.ptr(ost["exp_avg_sq"]), nat.ptr(ost["step"])
+        a.lr, a.adam = nat.ptr(self.opt.param_groups[0]["lr"]), 1
         a.niter, a.n, a.post = st["losses"].numel(), log_rot.numel(), int(self.post)
         nat.call("pr_pose_step", "pose_step", loss, a)
-        self.opt.step()
 
     def replay(self, n):
         for _ in range(n):

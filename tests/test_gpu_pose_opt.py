@@ -212,3 +212,36 @@ def test_pose_step_kernel_bookkeeping(device):
     ema = torch.tensor([0.1, -0.2, 0.3], **f32) * 0.9 + 0.1 * acc
     torch.testing.assert_close(st["v"], ema, rtol=0, atol=0)
     assert float(st["acc"].abs().max()) == 0.0
+
+
+def test_pose_step_adam_matches_torch_adam(device):
+    """pr_pose_step's Adam update against torch.optim.Adam (fused, capturable, tensor lr) over a few
+    steps on the same gradients: parameters and state at 1e-6."""
+    from pertrenderer_amd import _native as nat
+    f32 = dict(dtype=torch.float32, device=device)
+    torch.manual_seed(7)
+    ref = torch.randn(1, 3, **f32).requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=torch.tensor(5e-2, **f32), capturable=True, fused=True)
+    mine = ref.detach().clone()
+    m, s2, step = torch.zeros(1, 3, **f32), torch.zeros(1, 3, **f32), torch.zeros((), **f32)
+    lr = torch.tensor(5e-2, **f32)
+    st = dict(it=torch.zeros((), dtype=torch.int64, device=device), losses=torch.zeros(8, **f32),
+              gnorms=torch.zeros(8, **f32), best_loss=torch.tensor(float("inf"), **f32), best=torch.zeros(1, 3, **f32))
+    for k in range(5):
+        g = torch.randn(1, 3, **f32)
+        ref.grad = g.clone()
+        opt.step()
+        gm = g.clone()
+        a = nat.PRPoseStepArgs()
+        loss = torch.tensor(1.0, **f32)
+        a.loss, a.log_rot, a.grad, a.it = nat.ptr(loss), nat.ptr(mine), nat.ptr(gm), nat.ptr(st["it"])
+        a.losses, a.gnorms, a.best_loss, a.best = (nat.ptr(st[q]) for q in ("losses", "gnorms", "best_loss", "best"))
+        a.exp_avg, a.exp_avg_sq, a.step, a.lr, a.adam = nat.ptr(m), nat.ptr(s2), nat.ptr(step), nat.ptr(lr), 1
+        a.niter, a.n, a.post = 8, 3, 0
+        nat.call("pr_pose_step", "pose_step", loss, a)
+    torch.cuda.synchronize()
+    ost = opt.state[ref]
+    torch.testing.assert_close(mine, ref.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(m, ost["exp_avg"], rtol=1e-6, atol=1e-8)
+    torch.testing.assert_close(s2, ost["exp_avg_sq"], rtol=1e-6, atol=1e-10)
+    assert float(step) == float(ost["step"]) == 5.0
