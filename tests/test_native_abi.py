@@ -42,6 +42,11 @@ def test_argument_validation_without_gpu():
     assert b"empty shape" in lib.pr_last_error()
     r = nat.PRRastArgs()
     assert lib.pr_rast_fwd(r, None) == -1
+    assert lib.pr_pose_step(nat.PRPoseStepArgs(), None) == -1
+    assert b"pose_step" in lib.pr_last_error()
+    m = nat.PRRgbMseArgs()
+    assert lib.pr_rgb_mse_fwd(m, None) == -1 and lib.pr_rgb_mse_bwd(m, None) == -1
+    assert lib.pr_rgb_mse_workspace(65536) >= 1
 
 
 STRUCTS = {
@@ -49,7 +54,7 @@ STRUCTS = {
     "PRBlendBwdArgs": nat.PRBlendBwdArgs, "PRHeavisideArgs": nat.PRHeavisideArgs,
     "PRRastArgs": nat.PRRastArgs, "PRInterpArgs": nat.PRInterpArgs, "PRProjectArgs": nat.PRProjectArgs,
     "PRSO3Args": nat.PRSO3Args, "PRRotateArgs": nat.PRRotateArgs, "PRShadeArgs": nat.PRShadeArgs,
-    "PRNormalsArgs": nat.PRNormalsArgs,
+    "PRNormalsArgs": nat.PRNormalsArgs, "PRPoseStepArgs": nat.PRPoseStepArgs, "PRRgbMseArgs": nat.PRRgbMseArgs,
 }
 
 
