@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(kThreads) shade_fwd_kernel(PRShadeArgs a, int6
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t s = c0 + r * 64 + lane;
-      if (s >= c1 || live[r]) continue;
+      if (s >= c1 || live[r] || (a.pix_count && (a.flags & PR_SHADE_LIVE_ONLY))) continue;
       const V3 c = pad_colour(a, s, img[r], tab, pad);
       float* o = a.colors + s * 3;
       o[0] = c.x; o[1] = c.y; o[2] = c.z;
@@ -392,7 +392,9 @@ PR_DEV void put3(float* p, V3 g) { p[0] = g.x; p[1] = g.y; p[2] = g.z; }
 // padded slot: only the texel term can carry a gradient (p = n = 0: no light, no specular)
 template <bool DET>
 PR_DEV void pad_bwd(const PRShadeArgs& a, int64_t s, int64_t ds, int n, const ShadeDet& det) {
-  if (a.grad_bary) { a.grad_bary[s * 3] = 0.f; a.grad_bary[s * 3 + 1] = 0.f; a.grad_bary[s * 3 + 2] = 0.f; }
+  if (a.grad_bary && !(a.pix_count && (a.flags & PR_SHADE_LIVE_ONLY))) {
+    a.grad_bary[s * 3] = 0.f; a.grad_bary[s * 3 + 1] = 0.f; a.grad_bary[s * 3 + 2] = 0.f;
+  }
   if (a.texture == PR_TEX_GIVEN && a.grad_texels) {
     const V3 g = v3(a.ambient + n * 3) * v3(a.grad_colors + s * 3);
     float* o = a.grad_texels + s * 3;
@@ -690,7 +692,7 @@ __global__ void __launch_bounds__(kThreads) shade_fwd_pix_kernel(PRShadeArgs a, 
     pix_block_load(a, p0, (int)npix, HW, pb);
     __syncthreads();  // (the first also publishes the patterns)
     // the padded stores first: they drain while the live slots' load chains run
-    fill_padded(a.colors, pb, p0, (int)npix, a.K, kmag, pat);
+    if (!(a.flags & PR_SHADE_LIVE_ONLY)) fill_padded(a.colors, pb, p0, (int)npix, a.K, kmag, pat);
     const int total = pb.incl[kBlkPix - 1];
     for (int i = threadIdx.x; i < total; i += kThreads) {
       Slot sl;

@@ -806,7 +806,7 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
   // pz: bit i set = input i will want a gradient (sized and zeroed by the forward's kernel)
   static Tensor forward(AutogradContext* ctx, Tensor bary, Tensor verts, Tensor normals, Tensor tex, Tensor light,
                         Tensor camera, Tensor p2f, Opt counts_o, Tensor faces, Opt face_uvs_o, std::vector<Tensor> rows,
-                        int64_t mode, bool directional, int64_t pz) {
+                        int64_t mode, bool directional, bool live_only, int64_t pz) {
     const Tensor counts = val(counts_o), face_uvs = val(face_uvs_o);
     if (rows.size() != 6) throw std::invalid_argument("shade: 6 parameter rows expected");
     on_device({&bary, &verts, &normals, &tex, &light, &camera, &p2f, &counts, &faces, &face_uvs});
@@ -819,6 +819,7 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
     PRShadeArgs a{};
     shade_common(a, p2f_c, counts, faces, face_uvs, t, rows.data(), mode, directional);
     a.colors = ptr<float>(colors);
+    if (live_only && counts.defined()) a.flags |= PR_SHADE_LIVE_ONLY;
     Tensor acc[6];
     for (int i = 1; i < 6; ++i)
       if ((pz >> i) & 1 && prezeroable(i, mode)) acc[i] = at::empty_like(t[i]);
@@ -842,11 +843,12 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
     k.commit();
     ctx->saved_data["mode"] = mode;
     ctx->saved_data["directional"] = directional;
+    ctx->saved_data["live_only"] = live_only && counts.defined();
     return colors;
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    variable_list out(14);  // one per forward argument
+    variable_list out(15);  // one per forward argument
     if (!grads[0].defined()) return out;
     const Saved sv(ctx);
     Tensor t[6], rows[6];
@@ -886,6 +888,7 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
       a.workspace_bytes = static_cast<size_t>(ws.numel());
     }
     if (pre && !(a.flags & PR_DETERMINISTIC)) a.flags |= PR_GRAD_PREZEROED;
+    if (ctx->saved_data["live_only"].toBool()) a.flags |= PR_SHADE_LIVE_ONLY;
     check(api().shade_bwd(&a, stream_of(g)), "pr_shade_bwd");
     return once(grads, out);
   }
@@ -893,7 +896,7 @@ struct ShadeFn : public torch::autograd::Function<ShadeFn> {
 
 Tensor shade(const Tensor& bary, const Tensor& verts, const Tensor& normals, const Tensor& tex, const Tensor& light,
              const Tensor& camera, const Tensor& p2f, Opt counts, const Tensor& faces, Opt face_uvs,
-             std::vector<Tensor> rows, int64_t mode, bool directional) {
+             std::vector<Tensor> rows, int64_t mode, bool directional, bool live_only) {
   // which inputs will want a gradient (as project_rasterize: the C++ context cannot ask yet)
   int64_t pz = 0;
   if (at::GradMode::is_enabled()) {
@@ -901,7 +904,7 @@ Tensor shade(const Tensor& bary, const Tensor& verts, const Tensor& normals, con
     for (int i = 0; i < 6; ++i) pz |= in[i]->requires_grad() ? (int64_t(1) << i) : 0;
   }
   return ShadeFn::apply(bary, verts, normals, tex, light, camera, p2f, counts, faces, face_uvs, rows, mode,
-                        directional, pz);
+                        directional, live_only, pz);
 }
 
 struct VertNormalsFn : public torch::autograd::Function<VertNormalsFn> {

@@ -152,7 +152,13 @@ class RandomPhongShader(_RandomShaderBase):
         blend_params = kwargs.get("blend_params", self.blend_params)
         # texels = meshes.sample_textures(fragments); colors = phong_shading(..., texels) -- one
         # native kernel pair for TexturesUV / TexturesVertex (renderer/shading.py)
-        colors = textured_phong_shading(meshes, fragments, lights, cameras, materials)
+        # the native blends read a pixel's valid prefix only (the rasterizer's counts): the shading
+        # then leaves the padded slots' colours (and their d bary) unwritten
+        live_only = ((_is_fusable(self.smoothrast, self.smoothagg, fragments)
+                      and _multidevice.sample_devices() is None)
+                     or (type(self.smoothrast) is SoftRast and type(self.smoothagg) is SoftAgg
+                         and fragments.pix_to_face.is_cuda))
+        colors = textured_phong_shading(meshes, fragments, lights, cameras, materials, live_only=live_only)
         znear, zfar = _planes_from(cameras, kwargs)
         return smooth_rgb_blend(colors, fragments, self.smoothrast, self.smoothagg, blend_params,
                                 znear=znear, zfar=zfar)

@@ -119,7 +119,7 @@ class _ShadeFn(torch.autograd.Function):
         a.grad_light, a.grad_camera = nat.ptr(gl), nat.ptr(gc)
         ws = None
         if nat.deterministic():  # torch.use_deterministic_algorithms: in-order sums, no float atomics
-            a.flags = nat.PR_DETERMINISTIC
+            a.flags |= nat.PR_DETERMINISTIC
             ws = nat.workspace(lib.pr_shade_bwd_workspace_size(a), g.device)
             a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         nat.call("pr_shade_bwd", "pr_shade_bwd", g, a)
@@ -143,6 +143,7 @@ def _args(cfg, t):
         a.maps, a.face_uvs = nat.ptr(t["tex"]), nat.ptr(cfg["face_uvs"])
         a.Hm, a.Wm = t["tex"].shape[1], t["tex"].shape[2]
     a.directional = int(cfg["directional"])
+    a.flags = nat.PR_SHADE_LIVE_ONLY if cfg.get("live_only") and cfg["counts"] is not None else 0
     a.light, a.camera = nat.ptr(t["light"]), nat.ptr(t["camera"])
     for k in ("ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular", "shininess"):
         setattr(a, k, nat.ptr(cfg[k]))
@@ -193,7 +194,7 @@ def _native_ok(fragments, lights, materials):
     return not any(torch.is_tensor(x) and x.requires_grad for x in fixed)
 
 
-def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face_uvs=None):
+def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face_uvs=None, live_only=False):
     from .rasterizer import valid_counts
     p2f = fragments.pix_to_face
     N = p2f.shape[0]
@@ -203,7 +204,10 @@ def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face
         counts = None
     verts = meshes.verts_packed()
     faces = meshes.faces_packed().to(torch.int64).contiguous()
-    cfg = dict(p2f=nat.dense(p2f, torch.int64), counts=counts, faces=faces, mode=mode,
+    # live_only: the caller reads the valid prefix of the colours only (RandomPhongShader's native
+    # blend with the counts), so the padded slots' colours and d bary are left unwritten
+    live_only = bool(live_only) and counts is not None and mode != nat.PR_TEX_GIVEN
+    cfg = dict(p2f=nat.dense(p2f, torch.int64), counts=counts, faces=faces, mode=mode, live_only=live_only,
                face_uvs=face_uvs, directional=_is_directional(lights), **_param_rows(lights, materials, N, dev))
     light = _rows(lights.location, N, dev)
     camera = _rows(cameras.get_camera_center(), N, dev)
@@ -212,7 +216,7 @@ def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face
         return ext.shade(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg["p2f"],
                          counts, faces, face_uvs,
                          [cfg[k] for k in ("ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular",
-                                           "shininess")], int(mode), bool(cfg["directional"]))
+                                           "shininess")], int(mode), bool(cfg["directional"]), live_only)
     return _ShadeFn.apply(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg)
 
 
@@ -223,9 +227,11 @@ def phong_shading(meshes, fragments, lights, cameras, materials, texels):
     return phong_shading_reference(meshes, fragments, lights, cameras, materials, texels)
 
 
-def textured_phong_shading(meshes, fragments, lights, cameras, materials):
+def textured_phong_shading(meshes, fragments, lights, cameras, materials, live_only=False):
     """phong_shading(..., texels=meshes.sample_textures(fragments)) with the texel lookup fused
-    into the shading kernel for TexturesUV (maps of one size) and 3-channel TexturesVertex."""
+    into the shading kernel for TexturesUV (maps of one size) and 3-channel TexturesVertex.
+    live_only (an extension for callers that read the valid prefix only, with the rasterizer's
+    counts attached): the padded slots' colours, and their d bary, are left unwritten."""
     from .textures import TexturesUV
     tex = getattr(meshes, "textures", None)
     if _native_ok(fragments, lights, materials):
@@ -233,9 +239,11 @@ def textured_phong_shading(meshes, fragments, lights, cameras, materials):
             maps = tex.maps_padded().to(fragments.pix_to_face.device)
             if maps.shape[0] == fragments.pix_to_face.shape[0] and maps.shape[-1] == 3:
                 fuv = tex.faces_verts_uvs_packed().to(device=maps.device, dtype=F32).detach().contiguous()
-                return _shade_native(meshes, fragments, lights, cameras, materials, nat.PR_TEX_UV, maps, fuv)
+                return _shade_native(meshes, fragments, lights, cameras, materials, nat.PR_TEX_UV, maps, fuv,
+                                     live_only=live_only)
         if isinstance(tex, TexturesVertex):
             vc = tex.verts_features_packed()
             if vc.dim() == 2 and vc.shape[-1] == 3:
-                return _shade_native(meshes, fragments, lights, cameras, materials, nat.PR_TEX_VERTEX, vc)
+                return _shade_native(meshes, fragments, lights, cameras, materials, nat.PR_TEX_VERTEX, vc,
+                                     live_only=live_only)
     return phong_shading(meshes, fragments, lights, cameras, materials, meshes.sample_textures(fragments))

@@ -175,7 +175,7 @@ def test_renderer_uses_native_shading(device, layer):
                 fn = getattr(ext, name)
                 if name != "shade":
                     return fn
-                return lambda *a: calls.append(a[-2]) or fn(*a)
+                return lambda *a: calls.append(a[-3]) or fn(*a)  # (..., mode, directional, live_only)
 
         orig_get = host_layer.get
         try:
