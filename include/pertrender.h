@@ -82,6 +82,9 @@ extern "C" {
  * argmax: the same win counts and the same colour mix, so the image is the one-device image bit
  * for bit.  With !RAST (prob input); no agg noise is read. */
 #define PR_BLEND_WINNERS_IN 512
+#define PR_BLEND_LIVE_ONLY 1024 /* with RAST and pix_count: pr_blend_bwd leaves the masked slots' d zbuf / d dists / */
+                                /* d colour / d bary unwritten, for a caller whose consumers read the valid prefix */
+                                /* only (the rasterizer backward, the live-only shading; ABI 19) */
 
 typedef struct PRBlendParams {
   int32_t N, H, W, K;        /* fragment shape */

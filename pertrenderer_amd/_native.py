@@ -22,6 +22,7 @@ PR_BLEND_RAST_CAUCHY = 8
 PR_BLEND_AGG_CAUCHY = 16
 PR_BLEND_AGG_UNIFORM = 256
 PR_BLEND_WINNERS_IN = 512
+PR_BLEND_LIVE_ONLY = 1024
 PR_BLEND_RAST_WOVR = 32
 PR_BLEND_AGG_WOVR = 64
 PR_BLEND_SOFT = 128

@@ -573,7 +573,7 @@ def _fused(vertex, dists, zbuf, colors, vert_colors, sigma, gamma, alpha, link, 
 def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, sigma, gamma, alpha,
                            nb_samples_rast, nb_samples_agg, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0,
                            zfar=100.0, noise=None, fixed_noise=False, rast_kind="gaussian", rast_vr=True,
-                           agg_kind="gaussian", agg_vr=True):
+                           agg_kind="gaussian", agg_vr=True, live_only=False):
     """perturbed_blend(TexturesVertex(vert_colors).sample_textures(fragments), ...) as one native op:
     colours are interpolated only where a slot wins a Monte-Carlo sample (no texel tensor).
     vert_colors (V,3) and faces (F,3) are the packed mesh tensors; gradients flow to
@@ -595,6 +595,8 @@ def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, s
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
+    if live_only and cfg["counts"] is not None:  # the caller reads the valid prefix only (backward: no zero rows)
+        cfg["vflags"] |= nat.PR_BLEND_LIVE_ONLY
     (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
     return _fused(True, dists, zbuf, bary, vert_colors, sigma, gamma, alpha, link, pix_to_face, faces, znear, zfar, cfg)
 
@@ -602,7 +604,7 @@ def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, s
 def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_samples_rast,
                     nb_samples_agg, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0, zfar=100.0,
                     noise=None, fixed_noise=False, rast_kind="gaussian", rast_vr=True, agg_kind="gaussian",
-                    agg_vr=True):
+                    agg_vr=True, live_only=False):
     """smooth_rgb_blend(colors, fragments, <Rast>, <Agg>, ...) as one native op, for the
     Gaussian / Cauchy, with / without variance reduction operator pairs.
 
@@ -625,6 +627,8 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
+    if live_only and cfg["counts"] is not None:  # the caller reads the valid prefix only (backward: no zero rows)
+        cfg["vflags"] |= nat.PR_BLEND_LIVE_ONLY
     (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
     return _fused(False, dists, zbuf, colors, None, sigma, gamma, alpha, link, pix_to_face, None, znear, zfar, cfg)
 

@@ -961,8 +961,11 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   //      sample and is also the unperturbed argmax, so with the baseline every a_s = 0: no d z,
   //      no scalar partials; masked slots get zero d zbuf / d dists / d colour (the values B8m
   //      writes).  Without the baseline (GaussianAgg_wovr) a_s = dW_bg and the full path runs.
+  // PR_BLEND_LIVE_ONLY (RAST, counts): the masked slots' zero gradients are not written at all
+  const bool live_only = RAST && pcnt != nullptr && (p.flags & PR_BLEND_LIVE_ONLY);
   if (RAST && tail && g.empty && !(p.flags & PR_BLEND_AGG_WOVR) && uni(EA[bnpix]) == bnpix) {
-    if (!g.pm) {
+    if (live_only) {
+    } else if (!g.pm) {
       const int64_t s0 = bpix0 * K, n = (int64_t)bnpix * K;
       block_fill(a.grad_zbuf + s0, n, 0.f);
       block_fill(a.grad_dists + s0, n, 0.f);
@@ -1451,7 +1454,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   //           d zbuf, d dists and d colour are 0 (mask factor 0, no wins); without dists
   //           d prob keeps the alpha term g_alpha * prod_j (1 - prob_j) (its dL term is 0:
   //           prob = 0 there).  One wave per pixel: its lanes store consecutive slots.
-  if (tail) {
+  if (tail && !live_only) {
     const int lane = tid & 63;
     for (int mpl = tid >> 6; mpl < npix; mpl += kThreads / 64) {
       const int64_t gp = gpx[mpl];

@@ -53,8 +53,10 @@ def _background_tensor(bg, device):
     return t
 
 
-def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, znear=1.0, zfar=100):
-    """(N,H,W,K,3) colours + Fragments -> (N,H,W,4) RGBA (random_rasterizer.py:34-56)."""
+def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, znear=1.0, zfar=100, live_only=False):
+    """(N,H,W,K,3) colours + Fragments -> (N,H,W,4) RGBA (random_rasterizer.py:34-56).  live_only (an
+    extension, RandomPhongShader's): every consumer of the colours' and fragments' gradients reads the
+    valid prefix only, so the native backward leaves the masked slots' zero rows unwritten."""
     N, H, W, K = fragments.pix_to_face.shape
     device = fragments.pix_to_face.device
     background = blend_params.background_color
@@ -70,7 +72,7 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
             colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
             smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
             eps=smoothagg.eps, background=background, znear=znear, zfar=zfar,
-            fixed_noise=smoothagg.fixed_noise, **_variant_kw(smoothrast, smoothagg))
+            fixed_noise=smoothagg.fixed_noise, live_only=live_only, **_variant_kw(smoothrast, smoothagg))
     if type(smoothrast) is SoftRast and type(smoothagg) is SoftAgg and fragments.pix_to_face.is_cuda:
         # eval.py's "softras" pair as one native kernel pair (PR_BLEND_SOFT)
         return _blend.soft_blend(colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
@@ -160,8 +162,10 @@ class RandomPhongShader(_RandomShaderBase):
                          and fragments.pix_to_face.is_cuda))
         colors = textured_phong_shading(meshes, fragments, lights, cameras, materials, live_only=live_only)
         znear, zfar = _planes_from(cameras, kwargs)
+        # (the blend's live-only backward also needs a live-only consumer of d colours: only when
+        # the native shading ran live-only -- it marks its output -- are d colours read per live slot)
         return smooth_rgb_blend(colors, fragments, self.smoothrast, self.smoothagg, blend_params,
-                                znear=znear, zfar=zfar)
+                                znear=znear, zfar=zfar, live_only=getattr(colors, "_pr_live_only", False))
 
 
 class RandomSimpleShader(_RandomShaderBase):
@@ -205,11 +209,13 @@ class RandomSimpleShader(_RandomShaderBase):
                     sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,
                     background=blend_params.background_color, znear=znear, zfar=zfar, fixed_noise=sa.fixed_noise,
                     vert_colors=vc, faces=meshes.faces_packed(), **_variant_kw(sr, sa))
+            # live_only: the fragments' gradients go to the rasterizer's backward, which reads each
+            # pixel's valid prefix only, so the masked slots' zero rows are not written
             return _blend.perturbed_blend_vertex(
                 vc, meshes.faces_packed(), fragments.pix_to_face, fragments.bary_coords, fragments.dists,
                 fragments.zbuf, sr.sigma, sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,
                 background=blend_params.background_color, znear=znear, zfar=zfar, fixed_noise=sa.fixed_noise,
-                **_variant_kw(sr, sa))
+                live_only=True, **_variant_kw(sr, sa))
         texels = meshes.sample_textures(fragments)
         return smooth_rgb_blend(texels, fragments, self.smoothrast, self.smoothagg, blend_params,
                                 znear=znear, zfar=zfar)

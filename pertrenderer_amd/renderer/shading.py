@@ -213,11 +213,15 @@ def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face
     camera = _rows(cameras.get_camera_center(), N, dev)
     ext = host_layer.get()
     if ext is not None:  # the C++ autograd layer (host_layer.py): same kernel, same arguments
-        return ext.shade(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg["p2f"],
-                         counts, faces, face_uvs,
-                         [cfg[k] for k in ("ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular",
-                                           "shininess")], int(mode), bool(cfg["directional"]), live_only)
-    return _ShadeFn.apply(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg)
+        out = ext.shade(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg["p2f"],
+                        counts, faces, face_uvs,
+                        [cfg[k] for k in ("ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular",
+                                          "shininess")], int(mode), bool(cfg["directional"]), live_only)
+    else:
+        out = _ShadeFn.apply(fragments.bary_coords, verts, meshes.verts_normals_packed(), tex, light, camera, cfg)
+    if live_only:
+        out._pr_live_only = True  # padded colours unwritten; d colours read per live slot only
+    return out
 
 
 def phong_shading(meshes, fragments, lights, cameras, materials, texels):
