@@ -367,6 +367,8 @@ int pr_vert_normals_bwd(const PRNormalsArgs* args, void* stream);
  * pr_rast_bwd then sums every face's slot gradients in slot order, sequentially: the
  * accumulation order of PyTorch3D's CPU backward (and of oracle/rast_oracle.c), bit for bit. */
 #define PR_DETERMINISTIC 2
+#define PR_RAST_VALID_ONLY 8 /* pr_rast_fwd / pr_project_rast_fwd with pix_count: only each pixel's valid prefix of */
+                             /* p2f / zbuf / bary / dists is written (a caller that reads nothing else; ABI 19) */
 #define PR_SHADE_LIVE_ONLY 4 /* pr_shade_fwd / _bwd with pix_count: the padded slots' colours (forward) and */
                              /* d bary (backward) are left unwritten -- for a caller that reads the valid  */
                              /* prefix only (the blend and the rasterizer backward with the counts; ABI 19) */

@@ -29,6 +29,7 @@ PR_BLEND_SOFT = 128
 PR_GRAD_PREZEROED = 1
 PR_BLEND_SYNC_BYTES = 1024
 PR_DETERMINISTIC = 2
+PR_RAST_VALID_ONLY = 8  # pr_rast_fwd: only the valid prefix of the fragments is written (needs pix_count)
 PR_SHADE_LIVE_ONLY = 4  # pr_shade_*: padded slots' colours / d bary left unwritten (needs pix_count)
 
 _vp = C.c_void_p

@@ -1100,7 +1100,10 @@ __global__ void __launch_bounds__(64 * NW, NW == 2 ? PR_RAST_DUO_WPE : PR_RAST_W
     // valid slot per lane (a pixel's valid slots are its queue prefix), so no face evaluation
     // runs for a lane group that holds padding -- on a heavy tile half or more of its slots
     constexpr bool kCompact = FRAG && TP <= 16 && PR_RAST_FRAGC;
-    for (int base = 0; base < total; base += NT * U) {
+    // PR_RAST_VALID_ONLY (counts written): the padding is not written at all; the compacted pass
+    // below writes the valid slots' p2f / zbuf with their barycentrics and distances
+    const bool valid_only = kCompact && a.pix_count && (a.flags & PR_RAST_VALID_ONLY);
+    for (int base = 0; base < (valid_only ? 0 : total); base += NT * U) {
       float2 e[U];
       int sz[U], kk[U], cc[U], rr[U];
       int64_t o[U];
@@ -1190,6 +1193,10 @@ __global__ void __launch_bounds__(64 * NW, NW == 2 ? PR_RAST_DUO_WPE : PR_RAST_W
           float bc[3], pz, d;
           bool inside;
           face_eval<PERSP, CLIP>(r, pp, bc, pz, inside, d);
+          if (valid_only) {
+            a.pix_to_face[o] = (int64_t)fid;
+            a.zbuf[o] = e[u].x;
+          }
           a.dists[o] = inside ? -d : d;
           a.bary[o * 3 + 0] = bc[0];
           a.bary[o * 3 + 1] = bc[1];

@@ -473,7 +473,7 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
                                c10::optional<Tensor> csr_corners, std::vector<int64_t> cfg, double blur,
                                c10::optional<Tensor> blur_dev, bool need, c10::optional<Tensor> seed_adv,
                                int64_t seed_n) {
-    if (cfg.size() != 8) throw std::invalid_argument("project_rasterize: cfg must have 8 entries");
+    if (cfg.size() != 8 && cfg.size() != 9) throw std::invalid_argument("project_rasterize: cfg must have 8 or 9 entries");
     Tensor cs = csr_start.has_value() ? *csr_start : Tensor(), cc = csr_corners.has_value() ? *csr_corners : Tensor();
     on_device({&verts, &faces, &first, &nfaces, &w2v, &proj, &cs, &cc});
     auto v = dense(verts, at::kFloat);
@@ -508,6 +508,7 @@ struct ProjectRasterizeFn : public torch::autograd::Function<ProjectRasterizeFn>
     auto bary = empty({N, H, W, K, 3}, at::kFloat, v);
     auto dists = empty({N, H, W, K}, at::kFloat, v);
     auto counts = empty({N, H, W}, at::kInt, v);
+    if (cfg.size() == 9 && cfg[8]) a.flags |= PR_RAST_VALID_ONLY;  // the caller reads the valid prefix only
     a.pix_to_face = ptr<int64_t>(p2f);
     a.zbuf = ptr<float>(zbuf);
     a.bary = ptr<float>(bary);

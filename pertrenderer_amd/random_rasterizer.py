@@ -144,6 +144,32 @@ class RandomPhongShader(_RandomShaderBase):
         self.lights = self.lights.to(device)
         return self
 
+    def takes_valid_only(self, meshes, **kwargs):
+        """True when forward() reads each pixel's valid prefix only (MeshRenderer then rasterizes
+        without writing the padding): a native blend, and the native live-only shading of a
+        TexturesUV (one map size, 3 channels) or 3-channel TexturesVertex mesh on the GPU."""
+        from .renderer.shading import _native_ok_params
+        from .renderer.textures import TexturesUV
+        if not meshes.verts_packed().is_cuda:
+            return False
+        native_blend = ((isinstance(self.smoothrast, _PerturbedRast) and isinstance(self.smoothagg, _PerturbedAgg)
+                         and _multidevice.sample_devices() is None)
+                        or (type(self.smoothrast) is SoftRast and type(self.smoothagg) is SoftAgg))
+        if not native_blend or kwargs.get("cameras", self.cameras) is None:
+            return False
+        if not _native_ok_params(kwargs.get("lights", self.lights), kwargs.get("materials", self.materials)):
+            return False
+        tex = getattr(meshes, "textures", None)
+        if isinstance(tex, TexturesUV):
+            if not tex.fusable():
+                return False
+            maps = tex.maps_padded()
+            return maps.shape[0] == len(meshes) and maps.shape[-1] == 3
+        if isinstance(tex, TexturesVertex):
+            vc = tex.verts_features_packed()
+            return vc.dim() == 2 and vc.shape[-1] == 3
+        return False
+
     def forward(self, fragments, meshes, **kwargs):
         cameras = kwargs.get("cameras", self.cameras)
         if cameras is None:
@@ -190,6 +216,13 @@ class RandomSimpleShader(_RandomShaderBase):
         self.materials = self.materials.to(device)
         self.lights = None if self.lights is None else self.lights.to(device)
         return self
+
+    def takes_valid_only(self, meshes, **kwargs):
+        """True when forward() reads each pixel's valid prefix only: the TexturesVertex sampling
+        fused into the native blend on one device (its gradients go to the rasterizer backward)."""
+        return (_vertex_colors(meshes) is not None and isinstance(self.smoothrast, _PerturbedRast)
+                and isinstance(self.smoothagg, _PerturbedAgg) and _multidevice.sample_devices() is None
+                and kwargs.get("cameras", self.cameras) is not None)
 
     def forward(self, fragments, meshes, **kwargs):
         cameras = kwargs.get("cameras", self.cameras)

@@ -316,6 +316,9 @@ class MeshRasterizer(torch.nn.Module):
         return meshes_world.update_padded(verts_ndc)
 
     def forward(self, meshes_world, **kwargs) -> Fragments:
+        # (MeshRenderer's, for a shader that reads each pixel's valid prefix only: the padding of the
+        # fragments is then left unwritten -- PR_RAST_VALID_ONLY; never set for a caller's own use)
+        valid_only = bool(kwargs.pop("_pr_valid_only", False))
         rs = kwargs.get("raster_settings", self.raster_settings)
         clip = rs.clip_barycentric_coords
         if clip is None:  # (a device blur_radius is taken as > 0: reading it would synchronise)
@@ -340,7 +343,8 @@ class MeshRasterizer(torch.nn.Module):
                         verts, faces, first, nfaces, cameras.world_to_view_matrix(),
                         cameras.projection_matrix(), *meshes_world.corner_csr("gather"),
                         [H, W, int(rs.faces_per_pixel), int(bool(rs.perspective_correct)), int(bool(clip)),
-                         int(bool(rs.cull_backfaces)), bins[0], bins[1]], *_blur_arg(rs.blur_radius, verts.device),
+                         int(bool(rs.cull_backfaces)), bins[0], bins[1], int(valid_only)],
+                        *_blur_arg(rs.blur_radius, verts.device),
                         seed_adv, seed_n)
                 else:
                     p2f, zbuf, bary, dists, counts = _ProjectRasterizeFn.apply(

@@ -84,6 +84,11 @@ class MeshRenderer(torch.nn.Module):
         # launched (blend.prelink)
         token = blend.prelink_shader(self.shader, meshes_world)
         try:
+            # a shader that reads each pixel's valid prefix only (the native perturbed shaders, when
+            # every one of their consumers does) takes fragments whose padding is left unwritten
+            takes = getattr(self.shader, "takes_valid_only", None)
+            if takes is not None and takes(meshes_world, **kwargs):
+                kwargs = dict(kwargs, _pr_valid_only=True)
             fragments = self.rasterizer(meshes_world, **kwargs)
             return self.shader(fragments, meshes_world, **kwargs)
         finally:

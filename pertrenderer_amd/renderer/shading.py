@@ -186,12 +186,14 @@ def _param_rows(lights, materials, N, dev):
     return out
 
 
-def _native_ok(fragments, lights, materials):
-    if not fragments.pix_to_face.is_cuda:
-        return False
+def _native_ok_params(lights, materials):
     fixed = [lights.ambient_color, lights.diffuse_color, lights.specular_color, materials.ambient_color,
              materials.diffuse_color, materials.specular_color, materials.shininess]
     return not any(torch.is_tensor(x) and x.requires_grad for x in fixed)
+
+
+def _native_ok(fragments, lights, materials):
+    return fragments.pix_to_face.is_cuda and _native_ok_params(lights, materials)
 
 
 def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face_uvs=None, live_only=False):
