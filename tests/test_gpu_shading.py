@@ -355,3 +355,33 @@ def test_forward_zeroed_accumulators_once(device):
         tol = dict(rtol=1e-5, atol=1e-6 * float(c.abs().max()))  # float atomics: order differs
         torch.testing.assert_close(a, b, **tol)
         torch.testing.assert_close(a, c, **tol)
+
+
+@pytest.mark.parametrize("shader_kind,kind", [("phong", "uv"), ("phong", "vertex"), ("simple", "vertex")])
+def test_renderer_valid_only_fragments_match_full(shader_kind, kind, device):
+    """MeshRenderer hands a shader that reads each pixel's valid prefix only (takes_valid_only) fragments
+    whose padding is left unwritten (PR_RAST_VALID_ONLY): the image is the full-fragment render's bit for
+    bit, the gradients agree to float-atomic order.  (Renders compared after a first one: a process's
+    first render of a renderer differs from the later ones with or without valid-only fragments.)"""
+    import pertrenderer_amd as pa
+    from pertrenderer_amd.renderer.renderer import MeshRenderer
+    mesh, _, _, cams, mats, verts, _, extra = _scene(device, kind)
+    lights = PointLights(device=device, location=[[0.5, 2.0, -2.0]])
+    rs = RasterizationSettings(image_size=48, blur_radius=math.log(1e4 - 1) * 1e-3, faces_per_pixel=12)
+    rast = MeshRasterizer(cameras=cams, raster_settings=rs)
+    sr, sa = pa.GaussianRast(sigma=1e-3), pa.GaussianAgg(nb_samples=4, gamma=1e-2, fixed_noise=True)
+    cls = pa.RandomPhongShader if shader_kind == "phong" else pa.RandomSimpleShader
+    shader = cls(device=device, cameras=cams, lights=lights, materials=mats, smoothrast=sr, smoothagg=sa)
+    assert shader.takes_valid_only(mesh)
+    G = torch.rand((1, 48, 48, 4), device=device)
+    renderer = MeshRenderer(rast, shader)
+    with torch.no_grad():
+        renderer(mesh)
+    img_v = renderer(mesh)
+    g_v = _grads(img_v, G, [verts, extra])
+    shader.takes_valid_only = lambda *a, **k: False  # the same render with PyTorch3D's full fragments
+    img_f = renderer(mesh)
+    g_f = _grads(img_f, G, [verts, extra])
+    assert torch.equal(img_v, img_f)
+    for a, b, name in zip(g_v, g_f, ("verts", "texture")):
+        _close(a, b, 1e-5, name)
