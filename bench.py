@@ -8,7 +8,8 @@ synthetic target, backward through blend -> rasterizer -> vertices -> pose, Adam
 pose (lr 5e-2, eval.py:337).  The whole step is one captured HIP graph.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|eval]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+    python bench.py --gpus N ...                        (starts N rank processes itself, RCCL)
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL; --gpus must equal N)
 
 Multi-GPU (--shard):
   samples (default at N > 1, the north star's partition, strong scaling): every rank renders the
@@ -34,6 +35,68 @@ import math
 import os
 import sys
 import time
+
+
+def _launch_ranks():
+    """`python bench.py --gpus N` (N > 1) without a launcher: start N rank processes, one per GPU,
+    as torchrun would (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), and exit
+    with the first failing rank's code.  This parent imports neither torch nor the package, so it
+    never touches the device; each child dies with it (PR_SET_PDEATHSIG).  Under a launcher
+    (WORLD_SIZE set) a --gpus that differs from WORLD_SIZE is an error: the line would misreport
+    n_gpus."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    n = pre.parse_known_args()[0].gpus
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != n:
+            sys.stderr.write(f"bench.py: --gpus {n} but the launcher started WORLD_SIZE="
+                             f"{os.environ['WORLD_SIZE']} ranks\n")
+            sys.exit(2)
+        return
+    if n <= 1:
+        return
+    import ctypes
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    libc = ctypes.CDLL(None, use_errno=True)
+
+    def _die_with_parent():
+        libc.prctl(1, signal.SIGKILL)  # PR_SET_PDEATHSIG
+
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      preexec_fn=_die_with_parent))
+    code = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                if rc != 0 and code == 0:
+                    code = rc if rc > 0 else 128 - rc
+                    for q in live:  # one rank failed: the collectives of the others would hang
+                        q.kill()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    sys.exit(code)
+
+
+if __name__ == "__main__":
+    _launch_ranks()
 
 import numpy as np
 import torch
@@ -440,7 +503,18 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="no GPU work: join a gloo group, count the ranks by an all-reduce, print them (tests)")
     args = ap.parse_args()
+    if args.launch_check:
+        dist.init_process_group("gloo")
+        seen = torch.ones(1)
+        dist.all_reduce(seen)
+        if dist.get_rank() == 0:
+            print(json.dumps({"n_gpus": args.gpus, "world_size": dist.get_world_size(), "ranks_seen": int(seen.item()),
+                              "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}"}), flush=True)
+        dist.destroy_process_group()
+        return
     cfg = dict(CONFIGS[args.config])
     for key, val in (("image_size", args.image_size), ("K", args.faces_per_pixel), ("samples", args.samples),
                      ("batch", args.batch)):
@@ -465,6 +539,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    ranks = dist.get_world_size() if dist_on else 1  # the ranks the process group (RCCL) saw
+    if ranks != world:
+        raise RuntimeError(f"process group has {ranks} ranks, WORLD_SIZE={world}")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     torch.manual_seed(1234)  # same Philox keys on every rank
@@ -591,6 +668,7 @@ def main():
                "offsets; one RCCL all-reduce forms the full-S gradient estimate")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s (fwd+bwd)", "n_gpus": world,
+        "ranks": ranks, "backend": backend if dist_on else None,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
         "higher_is_better": True, "scaling": "strong" if shard == "samples" else "weak", "vs_baseline": None,
         "dtype": "f32",

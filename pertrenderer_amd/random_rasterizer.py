@@ -181,11 +181,14 @@ class RandomPhongShader(_RandomShaderBase):
         # texels = meshes.sample_textures(fragments); colors = phong_shading(..., texels) -- one
         # native kernel pair for TexturesUV / TexturesVertex (renderer/shading.py)
         # the native blends read a pixel's valid prefix only (the rasterizer's counts): the shading
-        # then leaves the padded slots' colours (and their d bary) unwritten
-        live_only = ((_is_fusable(self.smoothrast, self.smoothagg, fragments)
-                      and _multidevice.sample_devices() is None)
-                     or (type(self.smoothrast) is SoftRast and type(self.smoothagg) is SoftAgg
-                         and fragments.pix_to_face.is_cuda))
+        # then leaves the padded slots' colours (and their d bary) unwritten -- but only when
+        # MeshRenderer says the fragments' sole consumer is its own rasterizer backward
+        # (_pr_valid_only, takes_valid_only).  A direct shader(fragments, mesh) call gets the
+        # reference's zero rows in d dists / d zbuf / d bary (random_rasterizer.py:46-47).
+        live_only = bool(kwargs.get("_pr_valid_only", False)) and (
+            (_is_fusable(self.smoothrast, self.smoothagg, fragments) and _multidevice.sample_devices() is None)
+            or (type(self.smoothrast) is SoftRast and type(self.smoothagg) is SoftAgg
+                and fragments.pix_to_face.is_cuda))
         colors = textured_phong_shading(meshes, fragments, lights, cameras, materials, live_only=live_only)
         znear, zfar = _planes_from(cameras, kwargs)
         # (the blend's live-only backward also needs a live-only consumer of d colours: only when
@@ -242,13 +245,14 @@ class RandomSimpleShader(_RandomShaderBase):
                     sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,
                     background=blend_params.background_color, znear=znear, zfar=zfar, fixed_noise=sa.fixed_noise,
                     vert_colors=vc, faces=meshes.faces_packed(), **_variant_kw(sr, sa))
-            # live_only: the fragments' gradients go to the rasterizer's backward, which reads each
-            # pixel's valid prefix only, so the masked slots' zero rows are not written
+            # live_only (MeshRenderer's handshake only): the fragments' gradients go to the
+            # rasterizer's backward, which reads each pixel's valid prefix only, so the masked slots'
+            # zero rows are not written.  A direct call gets them written (smoothagg.py:198).
             return _blend.perturbed_blend_vertex(
                 vc, meshes.faces_packed(), fragments.pix_to_face, fragments.bary_coords, fragments.dists,
                 fragments.zbuf, sr.sigma, sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,
                 background=blend_params.background_color, znear=znear, zfar=zfar, fixed_noise=sa.fixed_noise,
-                live_only=True, **_variant_kw(sr, sa))
+                live_only=bool(kwargs.get("_pr_valid_only", False)), **_variant_kw(sr, sa))
         texels = meshes.sample_textures(fragments)
         return smooth_rgb_blend(texels, fragments, self.smoothrast, self.smoothagg, blend_params,
                                 znear=znear, zfar=zfar)

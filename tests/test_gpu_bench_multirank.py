@@ -44,3 +44,21 @@ def test_bench_two_ranks_gloo(shard, extra):
         assert ss["replicated_ms_per_rank"] > 0 and ss["sharded_ms_per_rank"] > 0 and ss["speedup_bound_vs_1gpu"] > 1
         assert "sample-parallel x2" in d["config"]["parallelism"]
     assert d["config"]["execution"] == "graph"  # the captured multi-rank step, not the eager fallback
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_spawns_two_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` (no torchrun, the way the driver runs --gpus 1) starts two rank
+    processes itself (bench._launch_ranks); here both share the box's GPU over gloo.  The line reports
+    the ranks the process group saw."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PR_BENCH_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "2", "--no-cpu-baseline",
+           "--no-dense", "--image-size", "128"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks"] == 2 and d["backend"] == "gloo"
+    assert "sample-parallel x2" in d["config"]["parallelism"]

@@ -357,19 +357,28 @@ def test_forward_zeroed_accumulators_once(device):
         torch.testing.assert_close(a, c, **tol)
 
 
-@pytest.mark.parametrize("shader_kind,kind", [("phong", "uv"), ("phong", "vertex"), ("simple", "vertex")])
-def test_renderer_valid_only_fragments_match_full(shader_kind, kind, device):
+@pytest.mark.parametrize("shader_kind,kind,pair,K", [
+    ("phong", "uv", "gaussian", 12), ("phong", "vertex", "gaussian", 12), ("simple", "vertex", "gaussian", 12),
+    # eval.py's "softras" renderer (SoftRast + SoftAgg): K <= 64 runs the 16-lane kernels, K > 64 the
+    # one-thread-per-pixel ones, both on fragments whose padding was never written
+    ("phong", "uv", "soft", 12), ("phong", "uv", "soft", 80), ("phong", "vertex", "soft", 80)])
+def test_renderer_valid_only_fragments_match_full(shader_kind, kind, pair, K, device):
     """MeshRenderer hands a shader that reads each pixel's valid prefix only (takes_valid_only) fragments
     whose padding is left unwritten (PR_RAST_VALID_ONLY): the image is the full-fragment render's bit for
-    bit, the gradients agree to float-atomic order.  (Renders compared after a first one: a process's
-    first render of a renderer differs from the later ones with or without valid-only fragments.)"""
+    bit, the gradients agree to float-atomic order.  (Renders compared after a first one: with
+    fixed_noise=True the reference reseeds after the rast draw (smoothagg.py:18-19 after smoothrast.py:21),
+    so call 1's rast noise comes from the caller's generator and every later call repeats call 2 --
+    the reference's semantics, pinned by tests/test_noise_pair.py.)"""
     import pertrenderer_amd as pa
     from pertrenderer_amd.renderer.renderer import MeshRenderer
     mesh, _, _, cams, mats, verts, _, extra = _scene(device, kind)
     lights = PointLights(device=device, location=[[0.5, 2.0, -2.0]])
-    rs = RasterizationSettings(image_size=48, blur_radius=math.log(1e4 - 1) * 1e-3, faces_per_pixel=12)
+    rs = RasterizationSettings(image_size=48, blur_radius=math.log(1e4 - 1) * 1e-3, faces_per_pixel=K)
     rast = MeshRasterizer(cameras=cams, raster_settings=rs)
-    sr, sa = pa.GaussianRast(sigma=1e-3), pa.GaussianAgg(nb_samples=4, gamma=1e-2, fixed_noise=True)
+    if pair == "soft":
+        sr, sa = pa.SoftRast(sigma=1e-3), pa.SoftAgg(gamma=1e-2)
+    else:
+        sr, sa = pa.GaussianRast(sigma=1e-3), pa.GaussianAgg(nb_samples=4, gamma=1e-2, fixed_noise=True)
     cls = pa.RandomPhongShader if shader_kind == "phong" else pa.RandomSimpleShader
     shader = cls(device=device, cameras=cams, lights=lights, materials=mats, smoothrast=sr, smoothagg=sa)
     assert shader.takes_valid_only(mesh)
