@@ -509,6 +509,149 @@ class _FusedVertexBlendFn(torch.autograd.Function):
                 s_g, g_g, a_g, _link_grad(gsc, need[7]), None, None, None, None, None)
 
 
+_SHADE_ROWS = ("ambient", "diffuse_color", "specular_color", "mat_diffuse", "mat_specular", "shininess")
+
+
+def _phong_args(sh, p2f_c, t):
+    """PRShadeArgs of the fused Phong blend (renderer.shading._args over the blend's fragments)."""
+    from .renderer.shading import _args
+    cfg = dict(p2f=p2f_c, counts=sh["counts"], faces=sh["faces"], mode=sh["mode"], face_uvs=sh["face_uvs"],
+               directional=sh["directional"], **sh["rows"])
+    return _args(cfg, t)
+
+
+class _FusedPhongBlendFn(torch.autograd.Function):
+    """perturbed_blend with RandomPhongShader's shading fused in (PR_BLEND_PHONG): each slot's
+    colour is Phong-shaded where it wins a sample (TexturesUV / TexturesVertex texel, point or
+    directional light), so no (N,H,W,K,3) colour tensor exists; gradients go to dists, zbuf, bary,
+    the vertex positions and normals, the texture, the light and the camera centre."""
+
+    @staticmethod
+    def forward(ctx, dists, zbuf, bary, verts, normals, tex, light, camera, sigma, gamma, alpha, link, p2f, znear,
+                zfar, cfg, sh):
+        nat.require_device(dists, zbuf, bary, verts, normals, tex, light, camera, p2f)
+        N, H, W, K = p2f.shape
+        dev = p2f.device
+        p2f_c = nat.dense(p2f, torch.int64)
+        d_c, z_c = _contig(dists), _contig(zbuf)
+        t = dict(bary=_contig(bary), verts=_contig(verts), normals=_contig(normals), tex=_contig(tex),
+                 light=_contig(light), camera=_contig(camera))
+        zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
+        noise = cfg["noise"].to(dev)
+        sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
+        flags = nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | nat.PR_BLEND_PHONG | cfg["vflags"]
+        p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf, flags)
+        image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
+        winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
+        cache = (torch.empty((N, H, W, K, 2), dtype=F32, device=dev)
+                 if RAST_CACHE and any(ctx.needs_input_grad[:12]) else None)
+        sync = _sync(dev)
+        shade = _phong_args(sh, p2f_c, t)
+        # a small mesh's per-vertex / per-image gradient table (zeroed by the forward's kernel)
+        tb = nat.load().pr_blend_phong_table_bytes(p, shade) if any(ctx.needs_input_grad[:12]) else 0
+        table = torch.empty(tb // 4, dtype=F32, device=dev) if tb else None
+        a = nat.PRBlendFwdArgs()
+        a.p = p
+        a.phong_table = nat.ptr(table)
+        a.pix_to_face, a.zbuf, a.dists, a.bary = nat.ptr(p2f_c), nat.ptr(z_c), nat.ptr(d_c), nat.ptr(t["bary"])
+        a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
+        a.pix_count, a.sync, a.shade = nat.ptr(cfg["counts"]), nat.ptr(sync), nat.C.addressof(shade)
+        _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
+        ctx.save_for_backward(p2f_c, d_c, z_c, zn, zf, winners, cache, sync, table, *t.values())
+        ctx.p, ctx.sc_dev, ctx.cfg, ctx.sh, ctx.noise = p, sc_dev, cfg, sh, noise
+        ctx.refs = (sigma, gamma, alpha)
+        return image
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gimg):
+        _no_uniform_grad(ctx.cfg.get("vflags", 0))
+        p2f_c, d_c, z_c, zn, zf, winners, cache, sync, table, *tv = ctx.saved_tensors
+        t = dict(zip(("bary", "verts", "normals", "tex", "light", "camera"), tv))
+        cfg, sh = ctx.cfg, ctx.sh
+        lib = nat.load()
+        dev = p2f_c.device
+        need = ctx.needs_input_grad
+        g = nat.dense(gimg, F32)
+        gd, gz, gb = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(t["bary"])
+        # mesh / texture / light / camera gradients: accumulated by the kernel, except those the
+        # small-mesh table writes (verts, normals, vertex colours, light, camera)
+        written = lambda k: table is not None and (k != "tex" or sh["mode"] == nat.PR_TEX_VERTEX)
+        acc = [(torch.empty_like(t[k]) if written(k) else torch.zeros_like(t[k])) if need[3 + i] else None
+               for i, k in enumerate(("verts", "normals", "tex", "light", "camera"))]
+        gsc = torch.empty(3, dtype=F32, device=dev)
+        shade = _phong_args(sh, p2f_c, t)
+        shade.grad_verts, shade.grad_normals = nat.ptr(acc[0]), nat.ptr(acc[1])
+        if sh["mode"] == nat.PR_TEX_VERTEX:
+            shade.grad_vert_colors = nat.ptr(acc[2])
+        else:
+            shade.grad_maps = nat.ptr(acc[2])
+        shade.grad_light, shade.grad_camera = nat.ptr(acc[3]), nat.ptr(acc[4])
+        a = nat.PRBlendBwdArgs()
+        a.p = ctx.p
+        a.pix_to_face, a.zbuf, a.dists, a.bary = nat.ptr(p2f_c), nat.ptr(z_c), nat.ptr(d_c), nat.ptr(t["bary"])
+        a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
+        a.grad_dists, a.grad_zbuf, a.grad_bary, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gb), nat.ptr(gsc)
+        a.pix_count, a.sync, a.shade = nat.ptr(cfg["counts"]), nat.ptr(sync), nat.C.addressof(shade)
+        a.phong_table = nat.ptr(table)
+        ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
+        _timed("blend_bwd", lambda: nat.call("pr_blend_bwd", "pr_blend_bwd", g, a))
+        s_g, g_g, a_g = _scalar_grads(gsc, need[8:11], ctx.refs)
+        return (gd if need[0] else None, gz if need[1] else None, gb if need[2] else None, *acc,
+                s_g, g_g, a_g, _link_grad(gsc, need[11]), None, None, None, None, None)
+
+
+def perturbed_blend_phong(sh, pix_to_face, bary, dists, zbuf, sigma, gamma, alpha, nb_samples_rast,
+                          nb_samples_agg, eps=1e-10, background=(1.0, 1.0, 1.0), znear=1.0, zfar=100.0, noise=None,
+                          fixed_noise=False, rast_kind="gaussian", rast_vr=True, agg_kind="gaussian", agg_vr=True,
+                          live_only=False):
+    """smooth_rgb_blend(phong_shading(..., meshes.sample_textures(fragments)), fragments, <Rast>, <Agg>)
+    (random_rasterizer.py:99-116) as one native op: `sh` is renderer.shading.phong_inputs(...) (mesh,
+    vertex normals, TexturesUV maps or vertex colours, light / material rows, camera centres).  The
+    colour of a slot is shaded only where it wins a Monte-Carlo sample.  Differentiable w.r.t.
+    dists, zbuf, bary, the vertex positions and normals, the texture, light, camera and the 0-d
+    smoothing tensors."""
+    shape = tuple(pix_to_face.shape)
+    N, H, W, K = shape
+    if tuple(bary.shape) != shape + (3,) or tuple(dists.shape) != shape or tuple(zbuf.shape) != shape:
+        raise ValueError("bary must be (N,H,W,K,3), dists / zbuf (N,H,W,K)")
+    vflags = variant_flags(rast_kind, rast_vr, agg_kind, agg_vr)
+    if noise is None:
+        pair = noise_mod.draw_pair(shape, nb_samples_rast, nb_samples_agg, pix_to_face.device, fixed_noise, rast_kind,
+                                   agg_kind)
+        if pair is None:
+            pair = (noise_mod.draw_rast(shape, nb_samples_rast, pix_to_face.device, rast_kind),
+                    noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind))
+        noise = _merge(*pair)
+    _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
+    counts = _counts_for(pix_to_face)
+    cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
+               bg=_background(background), noise=noise, vflags=vflags, counts=counts)
+    if live_only and counts is not None:  # every consumer reads the valid prefix only (backward: no zero rows)
+        cfg["vflags"] |= nat.PR_BLEND_LIVE_ONLY
+    sh = dict(sh, counts=counts)
+    (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
+    dev = pix_to_face.device
+    ext = host_layer.get()
+    if ext is not None:
+        sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
+        vals = (sigma, gamma, alpha)
+        if sc_dev is None or all(d is None or d.data_ptr() == v.data_ptr() for d, v in zip(sc_dev, vals)):
+            zn, zf = _planes(znear, N, dev), _planes(zfar, N, dev)
+            noise = noise.to(dev)
+            flags = nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | nat.PR_BLEND_PHONG | cfg["vflags"]
+            p = _params(shape, cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf, flags)
+            tt = lambda v: v if torch.is_tensor(v) else None
+            return ext.blend_phong(dists, zbuf, bary, sh["verts"], sh["normals"], sh["tex"], sh["light"], sh["camera"],
+                                   tt(sigma), tt(gamma), tt(alpha), link, pix_to_face, sh["faces"], counts,
+                                   sh["face_uvs"], [sh["rows"][k] for k in _SHADE_ROWS], zn, zf, noise.noise_r,
+                                   noise.noise_a, noise.seeds, nat.C.addressof(p), int(sh["mode"]),
+                                   bool(sh["directional"]), RAST_CACHE, _FUSED_FINALIZE)
+    return _FusedPhongBlendFn.apply(dists, zbuf, bary, sh["verts"], sh["normals"], sh["tex"], sh["light"],
+                                    sh["camera"], sigma, gamma, alpha, link, pix_to_face, znear, zfar, cfg, sh)
+
+
 def image_from_winners(prob, zbuf, colors, p2f, winners, gamma, alpha, eps=1e-10, background=(1.0, 1.0, 1.0),
                        znear=1.0, zfar=100.0, vert_colors=None, faces=None):
     """The fused blend's image from given per-sample winners (P, Sa) (PR_BLEND_WINNERS_IN): the win

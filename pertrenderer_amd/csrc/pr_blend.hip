@@ -29,6 +29,7 @@
 #include <mutex>
 
 #include "pr_common.h"
+#include "pr_phong.h"
 
 namespace pr {
 namespace {
@@ -526,12 +527,61 @@ PR_DEV int agg_num_groups(const PRBlendParams& p) {
   return ((p.sample_offset_a + p.Sa - 1) >> 2) - (p.sample_offset_a >> 2) + 1;
 }
 
-// Colour of slot gs: texel tensor (CM 1) or interpolated on demand from per-vertex
-// colours (CM 2; the same operation order as interp_fwd_kernel, so the result is
-// bit-identical to sampling the texels first).
+// Kernel arguments: the C ABI block plus, for PR_BLEND_PHONG (colour mode 3), a by-value copy of
+// the shading inputs the host passed by pointer (PRBlend*Args.shade)
+struct FwdK : PRBlendFwdArgs {
+  PRShadeArgs sh;
+  int pt_n;  // CM 3: floats of phong_table the forward zeroes
+};
+struct BwdK : PRBlendBwdArgs {
+  PRShadeArgs sh;
+  // CM 3 small-mesh table (pt_T > 0, PRBlendBwdArgs.phong_table): the per-vertex (verts | normals |
+  // vertex colours) and per-image (light | camera) gradients of a workgroup summed in LDS (pt_T
+  // floats), flushed by one device-scope atomic per touched entry into copy (block % pt_R) of the
+  // table, whose copies the last workgroup (or phong_table_reduce_kernel) sums into the outputs and
+  // zeroes.  A frame's slots all scatter into a few vertices: global atomics straight to them
+  // serialise on one or two cache lines (eval.py's cube: blend_bwd 1.1 ms); spread over the
+  // copies they do not.
+  int pt_T, pt_R;                 // table floats, copies
+  int pt_off;                     // LDS offset (floats) of the table, then the B2c work list
+  int pt_nrm, pt_vc, pt_l, pt_c;  // offsets of the normals / vertex colours / light / camera parts
+};
+#ifndef PR_PHONG_BWD_WPE  // waves per SIMD the CM 3 backward is built for (its Phong state: 128 VGPRs at 4)
+#define PR_PHONG_BWD_WPE 4
+#endif
+constexpr int kPhongTabMax = 4096;  // floats (16 KB of LDS) for the table, else global atomics
+constexpr int kPhongCopies = 32;
+
+// image of slot gs (one-frame calls: 0 without a division)
+template <typename A>
+PR_DEV int slot_image(const A& a, int64_t gs) {
+  return a.p.N == 1 ? 0 : (int)(gs / ((int64_t)a.p.H * a.p.W * a.p.K));
+}
+
+// the fragment slot gs as the shading sees it (face, image, barycentrics)
+template <typename A>
+PR_DEV Slot phong_slot(const A& a, int64_t gs, int64_t f) {
+  Slot sl;
+  sl.f = f;
+  sl.n = slot_image(a, gs);
+  sl.b[0] = a.bary[gs * 3]; sl.b[1] = a.bary[gs * 3 + 1]; sl.b[2] = a.bary[gs * 3 + 2];
+  return sl;
+}
+
+// Colour of slot gs: texel tensor (CM 1), interpolated on demand from per-vertex colours (CM 2;
+// the same operation order as interp_fwd_kernel, so the result is bit-identical to sampling the
+// texels first), or Phong-shaded on demand (CM 3: pr_phong.h's slot_terms, the operations of
+// pr_shade_fwd, so bit-identical to shading the slots first).
 template <int CM, typename A>
 PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
-  if constexpr (CM == 2) {
+  if constexpr (CM == 3) {
+    const int64_t f = a.pix_to_face[gs];
+    if (f < 0) { c[0] = c[1] = c[2] = 0.f; return; }
+    const Slot sl = phong_slot(a, gs, f);
+    const Terms t = slot_terms(a.sh, sl, gs, a.sh.faces + f * 3);
+    const V3 o = colour(t.lit, t.tex, t.spec);
+    c[0] = o.x; c[1] = o.y; c[2] = o.z;
+  } else if constexpr (CM == 2) {
     const int64_t f = a.pix_to_face[gs];
     if (f < 0) { c[0] = c[1] = c[2] = 0.f; return; }
     const float w0 = a.bary[gs * 3], w1 = a.bary[gs * 3 + 1], w2 = a.bary[gs * 3 + 2];
@@ -543,6 +593,99 @@ PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
   } else {
     c[0] = a.colors[gs * 3]; c[1] = a.colors[gs * 3 + 1]; c[2] = a.colors[gs * 3 + 2];
   }
+}
+
+// CM 3 backward scatters: one slot's mesh and texture gradients into the global accumulators
+// (PRBlendBwdArgs.shade's grad_*, zeroed by the caller); the interpolation weights are the slot's
+// barycentrics, as pr_shade_bwd's
+PR_DEV void atomic3(float* base, int64_t i, V3 g) {
+  atomicAdd(&base[i * 3], g.x); atomicAdd(&base[i * 3 + 1], g.y); atomicAdd(&base[i * 3 + 2], g.z);
+}
+PR_DEV void phong_scatter(const PRShadeArgs& a, const Slot& sl, const int64_t* fv, const PhongGrad& q) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int64_t vi = fv[i];
+    if (a.grad_verts) atomic3(a.grad_verts, vi, sl.b[i] * q.g_P);
+    if (a.grad_normals) atomic3(a.grad_normals, vi, sl.b[i] * q.g_Nn);
+    if (a.texture == PR_TEX_VERTEX && a.grad_vert_colors) atomic3(a.grad_vert_colors, vi, sl.b[i] * q.g_tex);
+  }
+  if (a.texture == PR_TEX_UV && a.grad_maps) {
+    float* gm = a.grad_maps + (int64_t)sl.n * a.Hm * a.Wm * 3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (q.ti[c] >= 0) atomic3(gm + q.ti[c], 0, q.w[c] * q.g_tex);
+  }
+}
+// the same scatters into the workgroup's LDS table (BwdK.pt_*): per-vertex parts by LDS atomics;
+// the map gradient (large, spread over many lines) stays global
+PR_DEV void phong_scatter_lds(const BwdK& a, float* PT, const Slot& sl, const int64_t* fv, const PhongGrad& q) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int vi = (int)fv[i] * 3;
+    const V3 gp = sl.b[i] * q.g_P, gn = sl.b[i] * q.g_Nn;
+    atomicAdd(&PT[vi], gp.x); atomicAdd(&PT[vi + 1], gp.y); atomicAdd(&PT[vi + 2], gp.z);
+    atomicAdd(&PT[a.pt_nrm + vi], gn.x); atomicAdd(&PT[a.pt_nrm + vi + 1], gn.y); atomicAdd(&PT[a.pt_nrm + vi + 2], gn.z);
+    if (a.pt_vc >= 0) {
+      const V3 gc = sl.b[i] * q.g_tex;
+      atomicAdd(&PT[a.pt_vc + vi], gc.x); atomicAdd(&PT[a.pt_vc + vi + 1], gc.y); atomicAdd(&PT[a.pt_vc + vi + 2], gc.z);
+    }
+  }
+  if (a.sh.texture == PR_TEX_UV && a.sh.grad_maps) {
+    float* gm = a.sh.grad_maps + (int64_t)sl.n * a.sh.Hm * a.sh.Wm * 3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (q.ti[c] >= 0) atomic3(gm + q.ti[c], 0, q.w[c] * q.g_tex);
+  }
+  const int l = a.pt_l + sl.n * 3, c = a.pt_c + sl.n * 3;
+  atomicAdd(&PT[l], q.g_dir.x); atomicAdd(&PT[l + 1], q.g_dir.y); atomicAdd(&PT[l + 2], q.g_dir.z);
+  atomicAdd(&PT[c], q.g_vraw.x); atomicAdd(&PT[c + 1], q.g_vraw.y); atomicAdd(&PT[c + 2], q.g_vraw.z);
+}
+
+// the table's sums -> the outputs (overwritten), the copies zeroed again (a second backward of the
+// same forward); entries i0, i0 + stride, ...  coherent: device-scope loads (the last workgroup)
+PR_DEV void phong_table_out(const BwdK& a, int i0, int stride, bool coherent) {
+  for (int i = i0; i < a.pt_T; i += stride) {
+    float v = 0.f;
+    for (int r = 0; r < a.pt_R; ++r) {
+      float* c = a.phong_table + (int64_t)r * a.pt_T + i;
+      v += coherent ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *c;
+      *c = 0.f;
+    }
+    float* dst;
+    int j;
+    if (i < a.pt_nrm) { dst = a.sh.grad_verts; j = i; }
+    else if (i < (a.pt_vc >= 0 ? a.pt_vc : a.pt_l)) { dst = a.sh.grad_normals; j = i - a.pt_nrm; }
+    else if (i < a.pt_l) { dst = a.sh.grad_vert_colors; j = i - a.pt_vc; }
+    else if (i < a.pt_c) { dst = a.sh.grad_light; j = i - a.pt_l; }
+    else { dst = a.sh.grad_camera; j = i - a.pt_c; }
+    if (dst) dst[j] = v;
+  }
+}
+__global__ void phong_table_reduce_kernel(BwdK a) {  // (without the fused last-workgroup reduction)
+  phong_table_out(a, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x, false);
+}
+
+// d light / d camera of one image (per-lane partial sums)
+PR_DEV void light_camera_atomics(const PRShadeArgs& a, int n, V3 l, V3 c) {
+  if (a.grad_light) atomic3(a.grad_light, n, l);
+  if (a.grad_camera) atomic3(a.grad_camera, n, c);
+}
+// the wave's partial d light / d camera: summed across the wave when its lanes hold one image (one
+// atomic per component per wave; every light and camera gradient of a frame goes to 6 addresses),
+// else lane by lane.  Every lane of the wave calls it (lanes without slots: n < 0, zero sums).
+PR_DEV void flush_light_camera(const PRShadeArgs& a, int n, V3 l, V3 c) {
+  const uint64_t has = __ballot(n >= 0);
+  if (!has) return;
+  const int nref = __shfl(n, __builtin_ctzll(has));
+  if (__ballot(n >= 0 && n != nref)) {
+    if (n >= 0) light_camera_atomics(a, n, l, c);
+    return;
+  }
+  float v[6] = {l.x, l.y, l.z, c.x, c.y, c.z};
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    for (int o = 32; o >= 1; o >>= 1) v[j] += __shfl_xor(v[j], o);
+  if ((threadIdx.x & 63) == 0) light_camera_atomics(a, nref, V3{v[0], v[1], v[2]}, V3{v[3], v[4], v[5]});
 }
 
 // ================================================================== forward
@@ -558,7 +701,7 @@ PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
 // One pixel block (tile) of the forward: all of its passes (static grid), or only its segment
 // part `part` of the entry-balanced plan (SEG).  rec: the profile record of this call.
 template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
-PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const Sc& sc, const int64_t blk,
+PR_DEV void fwd_tile(const FwdK& a, const Geo& g, const int NC0, const Sc& sc, const int64_t blk,
                      const int part, const int64_t rec) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
@@ -895,8 +1038,10 @@ PR_DEV void fwd_tile(const PRBlendFwdArgs& a, const Geo& g, const int NC0, const
 // Static grid: workgroup = pixel block.  SEG: workgroup b runs segment b of the plan (the grid is
 // the plan's bound on the segment count; workgroups past the plan's count exit at once).
 template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
-__global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(PRBlendFwdArgs a, Geo g, int NC) {
+__global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(FwdK a, Geo g, int NC) {
   if (a.sync && blockIdx.x == 0) sync_zero(a.sync);  // for the backward's fused reduction
+  if constexpr (CM == 3)  // the backward's small-mesh gradient table
+    for (int i = blockIdx.x * kThreads + threadIdx.x; i < a.pt_n; i += gridDim.x * kThreads) a.phong_table[i] = 0.f;
   if constexpr (!SEG) {
     fwd_tile<NOISE, RAST, CM, MULTI, false>(a, g, NC, resolve(a.p), pixel_block(g), -1, blockIdx.x);
   } else {
@@ -922,7 +1067,7 @@ constexpr int kB2R = PR_BLEND_B2R > 0 ? PR_BLEND_B2R : 1;
 // One pixel block of the backward: all passes (static grid) or segment part `part` (SEG); its
 // scalar partials go to partials[4 pidx .. 4 pidx + 4).
 template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
-PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float* partials, const int64_t blk,
+PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials, const int64_t blk,
                      const int part, const int64_t pidx) {
   extern __shared__ float smem[];
   const PRBlendParams& p = a.p;
@@ -970,7 +1115,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
       block_fill(a.grad_zbuf + s0, n, 0.f);
       block_fill(a.grad_dists + s0, n, 0.f);
       if constexpr (CM == 1) block_fill(a.grad_colors + 3 * s0, 3 * n, 0.f);
-      if constexpr (CM == 2) block_fill(a.grad_bary + 3 * s0, 3 * n, 0.f);
+      if constexpr (CM >= 2) block_fill(a.grad_bary + 3 * s0, 3 * n, 0.f);
     } else {  // interleaved: one K-slot row per pixel
       for (int i = tid; i < bnpix * K; i += kThreads) {
         const int pl = i / K;
@@ -978,7 +1123,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
         a.grad_zbuf[s] = 0.f;
         a.grad_dists[s] = 0.f;
         if constexpr (CM == 1) a.grad_colors[3 * s] = a.grad_colors[3 * s + 1] = a.grad_colors[3 * s + 2] = 0.f;
-        if constexpr (CM == 2) a.grad_bary[3 * s] = a.grad_bary[3 * s + 1] = a.grad_bary[3 * s + 2] = 0.f;
+        if constexpr (CM >= 2) a.grad_bary[3 * s] = a.grad_bary[3 * s + 1] = a.grad_bary[3 * s + 2] = 0.f;
       }
     }
     if (tid < 4) put_partial(a, partials + pidx * 4 + tid, 0.f);
@@ -986,6 +1131,15 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
     return;
   }
 
+  // CM 3: the workgroup's LDS table (small meshes), zeroed before the passes' barriers
+  float* PT = smem + a.pt_off;
+  int* WL = reinterpret_cast<int*>(PT + a.pt_T);  // [CAP] B2c's work list, [CAP] its length
+  if constexpr (CM == 3)
+    for (int i = tid; i < a.pt_T; i += kThreads) PT[i] = 0.f;
+  // CM 3 without the table: this thread's d light / d camera (image lc_n), flushed per wave after
+  // the passes
+  int lc_n = -1;
+  V3 lc_l{0.f, 0.f, 0.f}, lc_c{0.f, 0.f, 0.f};
   const int npass = SEG ? 1 : (MULTI ? uni(PS[PB + 1]) : 1);
   for (int it = 0; it < npass; ++it) {
   const int pass = SEG ? part : it;
@@ -1003,6 +1157,8 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   const float zf0 = p.zfar[n0], zn0 = p.znear[n0];
   fill_owner(OWN, ea, eb, cl, npix, lsh, lpp, CN);
+  if constexpr (CM == 3)
+    if (tid == 0) WL[CAP] = 0;  // B2c's work list (the previous pass's readers are past barriers)
   __syncthreads();
   PR_BSTAMP(0);
 
@@ -1232,17 +1388,23 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
       PX[pl * 12 + 2] = (float)km;   // its first index
       PX[pl * 12 + 3] = (float)jb;   // unperturbed argmax of the K+1 logits
     }
-    if constexpr (CM == 2) {
+    if constexpr (CM >= 2) {
 #ifdef PR_BLEND_PROF_SPLIT_B2  // diagnostic: B2's pixel part to slot 7, its colour gathers to slot 2
       PR_BSTAMP(7);
 #endif
       // dW = g_rgb . colour of the slot entries B5 reads (a win, or j0): the colour is
-      // interpolated from the vertex colours here, once per such entry
+      // interpolated from the vertex colours here (CM 2), once per such entry; CM 3 lists them for
+      // B2c
       if (act) {
         const float* gi = PX + pl * 12 + 8;
         for (int e = l; e < c; e += lpp) {
-          if (CN[e0 + e] == 0 && e != jb) continue;
+          const int cnt = CN[e0 + e];
+          if (cnt == 0 && e != jb) continue;
           float cc[3];
+          if constexpr (CM == 3) {  // listed for B2c
+            WL[atomicAdd(&WL[CAP], 1)] = e0 + e;
+            continue;
+          }
           slot_color<CM>(a, (int64_t)gpx[pl] * K + e, cc);
           DW[e0 + e] = (gi[0] * cc[0] + gi[1] * cc[1]) + gi[2] * cc[2];
         }
@@ -1251,6 +1413,53 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   }
   __syncthreads();
   PR_BSTAMP(2);
+
+  // ---- B2c (CM 3): the listed entries (a win, or j0) over the whole workgroup: each entry's
+  //      Phong colour -> dW, and for a winner its shading backward on the same state (d colour =
+  //      wins / Sa * g_rgb, known from B1): d bary, the mesh / texture / light / camera gradients
+  //      (B8 writes the other entries' zero d bary).  One entry per thread: the per-pixel lanes of
+  //      B2 left most threads idle behind each winner's dependent load chain.
+  if constexpr (CM == 3) {
+    const int nw = WL[CAP];
+    for (int wi = tid; wi < nw; wi += kThreads) {
+      const int li = WL[wi];
+      const int pl = OWN[li], e = li - (ea[pl] - eb);
+      const int64_t gs = (int64_t)gpx[pl] * K + e;
+      const float* gi = PX + pl * 12 + 8;
+      const int cnt = CN[li];
+      const int64_t f = a.pix_to_face[gs];
+      if (f < 0) {  // (not a winner: masked slots never win)
+        DW[li] = (gi[0] * 0.f + gi[1] * 0.f) + gi[2] * 0.f;
+        continue;
+      }
+      const Slot sl = phong_slot(a, gs, f);
+      const int64_t* fv = a.sh.faces + f * 3;
+      const Shade z = shade(a.sh, sl, gs, fv);
+      const Terms t = terms_of(a.sh, sl.n, z);
+      const V3 col = colour(t.lit, t.tex, t.spec);
+      DW[li] = (gi[0] * col.x + gi[1] * col.y) + gi[2] * col.z;
+      if (cnt == 0) continue;
+      const float w = (float)cnt / (float)Sa;
+      const PhongGrad q = phong_bwd_z(a.sh, sl, z, fv, V3{w * gi[0], w * gi[1], w * gi[2]});
+      a.grad_bary[gs * 3] = q.gb[0];
+      a.grad_bary[gs * 3 + 1] = q.gb[1];
+      a.grad_bary[gs * 3 + 2] = q.gb[2];
+      if (a.pt_T > 0) {
+        phong_scatter_lds(a, PT, sl, fv, q);
+      } else {
+        phong_scatter(a.sh, sl, fv, q);
+        if (sl.n != lc_n) {
+          if (lc_n >= 0) light_camera_atomics(a.sh, lc_n, lc_l, lc_c);
+          lc_n = sl.n;
+          lc_l = V3{0.f, 0.f, 0.f};
+          lc_c = V3{0.f, 0.f, 0.f};
+        }
+        lc_l = lc_l + q.g_dir;
+        lc_c = lc_c + q.g_vraw;
+      }
+    }
+    __syncthreads();
+  }
 
   // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0] (win counts: B1, CM 2's dW: B2)
   PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
@@ -1447,6 +1656,9 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
       a.grad_bary[gs * 3] = gb[0];
       a.grad_bary[gs * 3 + 1] = gb[1];
       a.grad_bary[gs * 3 + 2] = gb[2];
+    } else if constexpr (CM == 3) {
+      // a winner's d bary (and the rest of its shading backward) came from B2; zeros elsewhere
+      if (CN[li] == 0 || !m) a.grad_bary[gs * 3] = a.grad_bary[gs * 3 + 1] = a.grad_bary[gs * 3 + 2] = 0.f;
     }
   }
 
@@ -1468,7 +1680,7 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
         if constexpr (CM == 1) {
           float* dc = a.grad_colors + gs * 3;
           dc[0] = dc[1] = dc[2] = 0.f;
-        } else if constexpr (CM == 2) {
+        } else if constexpr (CM >= 2) {
           a.grad_bary[gs * 3] = a.grad_bary[gs * 3 + 1] = a.grad_bary[gs * 3 + 2] = 0.f;
         }
       }
@@ -1477,6 +1689,22 @@ PR_DEV void bwd_tile(const PRBlendBwdArgs& a, const Geo& g, const Sc& sc, float*
   __syncthreads();  // the next pass reuses every LDS record
   PR_BSTAMP(6);
   }  // passes
+
+  if constexpr (CM == 3) {
+    if (a.pt_T > 0) {
+      __syncthreads();
+      float* cp = a.phong_table + (int64_t)(blockIdx.x % a.pt_R) * a.pt_T;
+      for (int i = tid; i < a.pt_T; i += kThreads) {
+        const float v = PT[i];
+        if (v != 0.f) {  // (waits for the return: performed before this workgroup's arrival)
+          const float old = __hip_atomic_fetch_add(&cp[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("" ::"v"(old));
+        }
+      }
+    } else {
+      flush_light_camera(a.sh, lc_n, lc_l, lc_c);
+    }
+  }
 
   // ---- block reduction of the scalar partials (fixed order -> deterministic)
 #pragma unroll
@@ -1554,7 +1782,7 @@ PR_DEV void finalize_scalars(const float* partials, int nblk, const PRBlendParam
 }
 
 template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
-__global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_bwd_kernel(PRBlendBwdArgs a, Geo g, float* partials) {
+__global__ void __launch_bounds__(kThreads, CM == 3 ? PR_PHONG_BWD_WPE : (MULTI ? 6 : PR_BLEND_BWD_WPE)) blend_bwd_kernel(BwdK a, Geo g, float* partials) {
   int nblk = (int)gridDim.x;
   if constexpr (!SEG) {
     const int64_t blk = pixel_block(g);
@@ -1574,6 +1802,8 @@ __global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_
     __shared__ int flag;
     if (last_arrival(a.sync, (int)gridDim.x, &flag, g.sync_rel != 0)) {
       finalize_scalars(partials, nblk, a.p, RAST ? 1 : 0, a.grad_scalars, red, true);
+      if constexpr (CM == 3)
+        if (a.pt_T > 0) phong_table_out(a, threadIdx.x, kThreads, true);
       sync_zero(a.sync);
     }
   }
@@ -1829,7 +2059,7 @@ int check_params(const PRBlendParams& p, bool need_rast) {
 }
 
 int color_mode(int flags) {
-  return !(flags & PR_BLEND_COLOR) ? 0 : ((flags & PR_BLEND_VERTEX) ? 2 : 1);
+  return !(flags & PR_BLEND_COLOR) ? 0 : ((flags & PR_BLEND_VERTEX) ? 2 : ((flags & PR_BLEND_PHONG) ? 3 : 1));
 }
 
 template <typename Fn, typename... Args>
@@ -1838,11 +2068,13 @@ void launch_grid(Fn* fn, int nblk, size_t lds, hipStream_t st, Args... args) {
 }
 
 template <int NOISE, bool MULTI, bool SEG>
-void launch_fwd(const PRBlendFwdArgs& a, Geo geo, int NC, hipStream_t st, size_t lds, int nblk) {
+void launch_fwd(const FwdK& a, Geo geo, int NC, hipStream_t st, size_t lds, int nblk) {
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
   ktimer_mark(0, "blend_fwd_kernel", st);
-  if (rast && cm == 2) launch_grid(blend_fwd_kernel<NOISE, true, 2, MULTI, SEG>, nblk, lds, st, a, geo, NC);
+  if (cm == 3) {  // (RAST only, static grid: pr_blend_fwd checks)
+    if constexpr (!SEG) launch_grid(blend_fwd_kernel<NOISE, true, 3, MULTI, false>, nblk, lds, st, a, geo, NC);
+  } else if (rast && cm == 2) launch_grid(blend_fwd_kernel<NOISE, true, 2, MULTI, SEG>, nblk, lds, st, a, geo, NC);
   else if (rast && cm == 1) launch_grid(blend_fwd_kernel<NOISE, true, 1, MULTI, SEG>, nblk, lds, st, a, geo, NC);
   else if (rast) launch_grid(blend_fwd_kernel<NOISE, true, 0, MULTI, SEG>, nblk, lds, st, a, geo, NC);
   else if (cm == 1) launch_grid(blend_fwd_kernel<NOISE, false, 1, MULTI, SEG>, nblk, lds, st, a, geo, NC);
@@ -1852,11 +2084,13 @@ void launch_fwd(const PRBlendFwdArgs& a, Geo geo, int NC, hipStream_t st, size_t
 }
 
 template <int NOISE, bool MULTI, bool SEG>
-void launch_bwd(const PRBlendBwdArgs& a, Geo geo, hipStream_t st, size_t lds, int nblk, float* part) {
+void launch_bwd(const BwdK& a, Geo geo, hipStream_t st, size_t lds, int nblk, float* part) {
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
   ktimer_mark(0, "blend_bwd_kernel", st);
-  if (rast && cm == 2) launch_grid(blend_bwd_kernel<NOISE, true, 2, MULTI, SEG>, nblk, lds, st, a, geo, part);
+  if (cm == 3) {
+    if constexpr (!SEG) launch_grid(blend_bwd_kernel<NOISE, true, 3, MULTI, false>, nblk, lds, st, a, geo, part);
+  } else if (rast && cm == 2) launch_grid(blend_bwd_kernel<NOISE, true, 2, MULTI, SEG>, nblk, lds, st, a, geo, part);
   else if (rast && cm == 1) launch_grid(blend_bwd_kernel<NOISE, true, 1, MULTI, SEG>, nblk, lds, st, a, geo, part);
   else if (rast) launch_grid(blend_bwd_kernel<NOISE, true, 0, MULTI, SEG>, nblk, lds, st, a, geo, part);
   else if (cm == 1) launch_grid(blend_bwd_kernel<NOISE, false, 1, MULTI, SEG>, nblk, lds, st, a, geo, part);
@@ -1941,7 +2175,7 @@ PlanCfg plan_cfg(const PRBlendParams& p, const int32_t* pcnt) {
   // workgroups (forward kernel 46 -> 53 us): a net loss of ~20 us per step.
   const char* env = getenv("PR_BLEND_SEG");
   const int64_t P = (int64_t)p.N * p.H * p.W;
-  if (!pcnt || P > kPlanMaxPixels || !(env && atoi(env) != 0)) return c;
+  if (!pcnt || P > kPlanMaxPixels || !(env && atoi(env) != 0) || (p.flags & PR_BLEND_PHONG)) return c;
   const int KP1 = p.K + 1;
   // (read per call: tests drive several segment sizes in one process)
   const int e_env[2] = {getenv("PR_BLEND_SEG_FWD") ? atoi(getenv("PR_BLEND_SEG_FWD")) : 0,
@@ -1985,6 +2219,31 @@ PlanCfg plan_cfg(const PRBlendParams& p, const int32_t* pcnt) {
   c.bytes = (size_t)off * sizeof(int32_t);
   c.on = true;
   return c;
+}
+
+// PR_BLEND_PHONG's shading block: RAST, no VERTEX, texture UV or VERTEX with its buffers (pr_shade's
+// checks, minus the per-slot tensors the blend owns)
+int phong_check(const PRBlendParams& p, const PRShadeArgs* sh) {
+  if (!(p.flags & PR_BLEND_RAST) || (p.flags & PR_BLEND_VERTEX) || !(p.flags & PR_BLEND_COLOR))
+    return set_error(PR_ERR_ARG, "blend: PR_BLEND_PHONG needs RAST | COLOR and no VERTEX");
+  if (!sh) return set_error(PR_ERR_ARG, "blend: PR_BLEND_PHONG without shade args");
+  const PRShadeArgs& a = *sh;
+  if (!a.faces || !a.verts || !a.normals || !a.light || !a.ambient || !a.diffuse_color || !a.specular_color ||
+      !a.mat_diffuse || !a.mat_specular || !a.shininess || !a.camera)
+    return set_error(PR_ERR_ARG, "blend: PR_BLEND_PHONG mesh / lighting buffer missing");
+  if (a.texture == PR_TEX_UV ? (!a.face_uvs || !a.maps || a.Hm <= 0 || a.Wm <= 0)
+      : a.texture == PR_TEX_VERTEX ? !a.vert_colors : true)
+    return set_error(PR_ERR_ARG, "blend: PR_BLEND_PHONG texture must be PR_TEX_UV or PR_TEX_VERTEX with its buffers");
+  if (a.V < 0 || a.F < 0 || a.V >= (int64_t(1) << 31)) return set_error(PR_ERR_ARG, "blend: bad mesh size");
+  return PR_OK;
+}
+
+// CM 3's LDS table size (floats) for the call's mesh: verts | normals (| vertex colours) per vertex,
+// light | camera per image; 0 when it exceeds kPhongTabMax (global atomics instead)
+int phong_table_floats(const PRBlendParams& p, const PRShadeArgs* sh) {
+  if (!(p.flags & PR_BLEND_PHONG) || !sh) return 0;
+  const int64_t T = sh->V * (sh->texture == PR_TEX_VERTEX ? 9 : 6) + (int64_t)p.N * 6;
+  return T <= kPhongTabMax ? (int)T : 0;
 }
 
 int64_t bwd_blocks(const PRBlendParams& p) {
@@ -2046,8 +2305,17 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
     return set_error(PR_ERR_ARG, "blend_fwd: PR_BLEND_WINNERS_IN takes probabilities (no PR_BLEND_RAST)");
   if (!a.zbuf || !a.winners || (rast && !a.dists) || (!rast && !a.prob) ||
       (cm == 1 && (!a.colors || !a.image)) || (!color && !a.weights) ||
-      (cm == 2 && (!a.image || !a.bary || !a.faces || !a.vert_colors || !a.pix_to_face)))
+      (cm == 2 && (!a.image || !a.bary || !a.faces || !a.vert_colors || !a.pix_to_face)) ||
+      (cm == 3 && (!a.image || !a.bary || !a.pix_to_face)))
     return set_error(PR_ERR_ARG, "blend_fwd: missing buffer");
+  if (cm == 3)
+    if (int e = phong_check(a.p, a.shade)) return e;
+  FwdK k{};
+  static_cast<PRBlendFwdArgs&>(k) = a;
+  if (cm == 3) {
+    k.sh = *a.shade;
+    k.pt_n = a.phong_table ? kPhongCopies * phong_table_floats(a.p, a.shade) : 0;
+  }
   const int KP1 = a.p.K + 1;
   const Shape sh = pick_shape(KP1, a.p.Sa, (int64_t)a.p.N * a.p.H * a.p.W, false);
   const int PB = sh.PB;
@@ -2070,16 +2338,21 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
     geo.plan_fwd_list = pc.q.list[0];
     geo.pm = 0;  // the plan cuts consecutive pixel blocks
     nblk = pc.q.T[0] + pc.q.X[0];  // the plan's bound on the segments
-    if (a.p.noise_mode == PR_NOISE_INJECTED) launch_fwd<PR_NOISE_INJECTED, false, true>(a, geo, NC, st, lds, (int)nblk);
-    else launch_fwd<PR_NOISE_PHILOX, false, true>(a, geo, NC, st, lds, (int)nblk);
+    if (a.p.noise_mode == PR_NOISE_INJECTED) launch_fwd<PR_NOISE_INJECTED, false, true>(k, geo, NC, st, lds, (int)nblk);
+    else launch_fwd<PR_NOISE_PHILOX, false, true>(k, geo, NC, st, lds, (int)nblk);
   } else if (a.p.noise_mode == PR_NOISE_INJECTED) {
-    if (multi) launch_fwd<PR_NOISE_INJECTED, true, false>(a, geo, NC, st, lds, (int)nblk);
-    else launch_fwd<PR_NOISE_INJECTED, false, false>(a, geo, NC, st, lds, (int)nblk);
+    if (multi) launch_fwd<PR_NOISE_INJECTED, true, false>(k, geo, NC, st, lds, (int)nblk);
+    else launch_fwd<PR_NOISE_INJECTED, false, false>(k, geo, NC, st, lds, (int)nblk);
   } else {
-    if (multi) launch_fwd<PR_NOISE_PHILOX, true, false>(a, geo, NC, st, lds, (int)nblk);
-    else launch_fwd<PR_NOISE_PHILOX, false, false>(a, geo, NC, st, lds, (int)nblk);
+    if (multi) launch_fwd<PR_NOISE_PHILOX, true, false>(k, geo, NC, st, lds, (int)nblk);
+    else launch_fwd<PR_NOISE_PHILOX, false, false>(k, geo, NC, st, lds, (int)nblk);
   }
   return check_launch("blend_fwd");
+}
+
+extern "C" size_t pr_blend_phong_table_bytes(const PRBlendParams* p, const PRShadeArgs* shade) {
+  if (!p || !shade) return 0;
+  return (size_t)kPhongCopies * phong_table_floats(*p, shade) * sizeof(float);
 }
 
 extern "C" size_t pr_blend_plan_size(const PRBlendParams* p) {
@@ -2093,7 +2366,8 @@ extern "C" size_t pr_blend_bwd_workspace_size(const PRBlendBwdArgs* args) {
   if (!args) return 0;
   if (args->p.flags & PR_BLEND_SOFT) return soft_blend_workspace(args->p);
   const PlanCfg pc = args->plan ? plan_cfg(args->p, args->pix_count) : PlanCfg{};
-  return (size_t)(pc.on ? pc.q.T[1] + pc.q.X[1] : bwd_blocks(args->p)) * 4 * sizeof(float);
+  const size_t part = (size_t)(pc.on ? pc.q.T[1] + pc.q.X[1] : bwd_blocks(args->p)) * 4 * sizeof(float);
+  return part;
 }
 
 extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
@@ -2110,17 +2384,35 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
       (color_mode(a.p.flags) == 1 && (!a.colors || !a.grad_image || !a.grad_colors)) ||
       (color_mode(a.p.flags) == 2 && (!a.grad_image || !a.bary || !a.faces || !a.vert_colors ||
                                       !a.grad_bary || !a.pix_to_face)) ||
+      (color_mode(a.p.flags) == 3 && (!a.grad_image || !a.bary || !a.grad_bary || !a.pix_to_face)) ||
       (!color && !a.grad_weights))
     return set_error(PR_ERR_ARG, "blend_bwd: missing buffer");
+  if (color_mode(a.p.flags) == 3)
+    if (int e = phong_check(a.p, a.shade)) return e;
   const size_t need = pr_blend_bwd_workspace_size(args);
   if (!a.workspace || a.workspace_bytes < need) return set_error(PR_ERR_WORKSPACE, "blend_bwd: workspace too small");
+  BwdK k{};
+  static_cast<PRBlendBwdArgs&>(k) = a;
+  if (color_mode(a.p.flags) == 3) k.sh = *a.shade;
+  const int ptT = phong_table_floats(a.p, a.shade);
   const int KP1 = a.p.K + 1;
   const Shape sh = pick_shape(KP1, a.p.Sa, (int64_t)a.p.N * a.p.H * a.p.W, true);
   const int PB = sh.PB;
   Geo geo = make_geo(a.p, PB, true);
   geo.cap = sh.cap;
   int64_t nblk = (geo.P + PB - 1) / PB;
-  const size_t lds = bwd_lds(PB, sh.cap, a.p.Sa);
+  size_t lds = bwd_lds(PB, sh.cap, a.p.Sa);
+  if (color_mode(a.p.flags) == 3) {  // CM 3: LDS table (small meshes), then B2c's work list
+    k.pt_off = (int)((lds + 15) / 16 * 4);
+    k.pt_T = a.phong_table ? ptT : 0;
+    k.pt_R = kPhongCopies;
+    lds = (size_t)k.pt_off * sizeof(float) + (size_t)k.pt_T * sizeof(float) + (size_t)(sh.cap + 1) * sizeof(int);
+    const int64_t V = a.shade->V;
+    k.pt_nrm = (int)(V * 3);
+    k.pt_vc = a.shade->texture == PR_TEX_VERTEX ? (int)(V * 6) : -1;
+    k.pt_l = (int)(V * (a.shade->texture == PR_TEX_VERTEX ? 9 : 6));
+    k.pt_c = k.pt_l + a.p.N * 3;
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* part = reinterpret_cast<float*>(a.workspace);
   const bool multi = sh.cap < PB * KP1;
@@ -2130,16 +2422,20 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
     geo.plan_bwd_list = pc.q.list[1];
     geo.pm = 0;  // the plan cuts consecutive pixel blocks
     nblk = pc.q.T[1] + pc.q.X[1];  // the plan's bound on the segments
-    if (a.p.noise_mode == PR_NOISE_INJECTED) launch_bwd<PR_NOISE_INJECTED, false, true>(a, geo, st, lds, (int)nblk, part);
-    else launch_bwd<PR_NOISE_PHILOX, false, true>(a, geo, st, lds, (int)nblk, part);
+    if (a.p.noise_mode == PR_NOISE_INJECTED) launch_bwd<PR_NOISE_INJECTED, false, true>(k, geo, st, lds, (int)nblk, part);
+    else launch_bwd<PR_NOISE_PHILOX, false, true>(k, geo, st, lds, (int)nblk, part);
   } else if (a.p.noise_mode == PR_NOISE_INJECTED) {
-    if (multi) launch_bwd<PR_NOISE_INJECTED, true, false>(a, geo, st, lds, (int)nblk, part);
-    else launch_bwd<PR_NOISE_INJECTED, false, false>(a, geo, st, lds, (int)nblk, part);
+    if (multi) launch_bwd<PR_NOISE_INJECTED, true, false>(k, geo, st, lds, (int)nblk, part);
+    else launch_bwd<PR_NOISE_INJECTED, false, false>(k, geo, st, lds, (int)nblk, part);
   } else {
-    if (multi) launch_bwd<PR_NOISE_PHILOX, true, false>(a, geo, st, lds, (int)nblk, part);
-    else launch_bwd<PR_NOISE_PHILOX, false, false>(a, geo, st, lds, (int)nblk, part);
+    if (multi) launch_bwd<PR_NOISE_PHILOX, true, false>(k, geo, st, lds, (int)nblk, part);
+    else launch_bwd<PR_NOISE_PHILOX, false, false>(k, geo, st, lds, (int)nblk, part);
   }
   if (int e = check_launch("blend_bwd")) return e;
+  if (k.pt_T > 0 && !a.sync) {  // (else the kernel's last workgroup wrote the table's sums)
+    phong_table_reduce_kernel<<<(k.pt_T + kThreads - 1) / kThreads, kThreads, 0, st>>>(k);
+    if (int e = check_launch("blend_bwd_phong_reduce")) return e;
+  }
   if (a.sync) return PR_OK;  // the scalars were reduced by the kernel's last workgroup
   blend_finalize_kernel<<<1, kThreads, 0, st>>>(part, (int)nblk, a.p, rast ? 1 : 0, a.grad_scalars,
                                                 pc.on ? a.plan : nullptr);

@@ -11,92 +11,10 @@
 //     (wave_compact).
 //
 #include "pr_common.h"
+#include "pr_phong.h"
 
 namespace pr {
 namespace {
-
-constexpr float kNormEps = 1e-6f;  // F.normalize(eps=1e-6)
-constexpr int kLdsFloats = 8192;   // 32 KB reduction table per workgroup
-
-struct V3 {
-  float x, y, z;
-};
-PR_DEV V3 v3(const float* p) { return V3{p[0], p[1], p[2]}; }
-PR_DEV V3 operator+(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
-PR_DEV V3 operator-(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-PR_DEV V3 operator*(float s, V3 a) { return V3{s * a.x, s * a.y, s * a.z}; }
-PR_DEV V3 operator*(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
-PR_DEV float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
-PR_DEV float sum3(V3 a) { return (a.x + a.y) + a.z; }
-
-// x / max(|x|, eps) and its backward
-PR_DEV float nrm(V3 x) { return fmaxf(sqrtf(dot(x, x)), kNormEps); }
-PR_DEV V3 normalize(V3 x) {
-  const float r = nrm(x);
-  return V3{x.x / r, x.y / r, x.z / r};
-}
-PR_DEV V3 normalize_bwd(V3 x, V3 g) {
-  const float r = sqrtf(dot(x, x));
-  if (!(r > kNormEps)) return (1.f / kNormEps) * g;
-  const V3 y = V3{x.x / r, x.y / r, x.z / r};
-  return (1.f / r) * (g - dot(y, g) * y);
-}
-
-// (w0 r0 + w1 r1) + w2 r2 over a per-vertex table (interpolate_face_attributes order)
-PR_DEV V3 interp3(const float* tab, const int64_t* fv, const float* b) {
-  const float* r0 = tab + fv[0] * 3;
-  const float* r1 = tab + fv[1] * 3;
-  const float* r2 = tab + fv[2] * 3;
-  return V3{(b[0] * r0[0] + b[1] * r1[0]) + b[2] * r2[0], (b[0] * r0[1] + b[1] * r1[1]) + b[2] * r2[1],
-            (b[0] * r0[2] + b[1] * r1[2]) + b[2] * r2[2]};
-}
-
-// torch grid_sample, bilinear, align_corners=True, padding "border", on the vertically
-// flipped map (v = 0 is the bottom row): source coordinate in the flipped map and the
-// clip gradient (0 where the coordinate was clamped, as clip_coordinates_set_grad)
-struct Bilin {
-  int x0, y0;      // north-west corner in the flipped map
-  float ix, iy;    // source coordinates
-  float gx, gy;    // d ix / d u, d iy / d v (0 when clamped)
-};
-PR_DEV float src_coord(float uv, int size, float& grad) {
-  const float g = uv * 2.f - 1.f;  // TexturesUV: uv * 2 - 1
-  float c = ((g + 1.f) / 2.f) * (float)(size - 1);
-  grad = (float)(size - 1);
-  if (c <= 0.f) { c = 0.f; grad = 0.f; }
-  else if (c >= (float)(size - 1)) { c = (float)(size - 1); grad = 0.f; }
-  return c;
-}
-PR_DEV Bilin bilin(float u, float v, int Hm, int Wm) {
-  Bilin b;
-  b.ix = src_coord(u, Wm, b.gx);
-  b.iy = src_coord(v, Hm, b.gy);
-  b.x0 = (int)floorf(b.ix);
-  b.y0 = (int)floorf(b.iy);
-  return b;
-}
-// texel (flipped row r -> map row Hm-1-r) with torch's corner order nw, ne, sw, se
-PR_DEV V3 bilin_sample(const float* map, int Hm, int Wm, const Bilin& b) {
-  const float x1 = (float)(b.x0 + 1), y1 = (float)(b.y0 + 1), x0 = (float)b.x0, y0 = (float)b.y0;
-  const float w[4] = {(x1 - b.ix) * (y1 - b.iy), (b.ix - x0) * (y1 - b.iy), (x1 - b.ix) * (b.iy - y0),
-                      (b.ix - x0) * (b.iy - y0)};
-  const int cx[4] = {b.x0, b.x0 + 1, b.x0, b.x0 + 1}, cy[4] = {b.y0, b.y0, b.y0 + 1, b.y0 + 1};
-  V3 o{0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    if (cx[c] >= 0 && cx[c] < Wm && cy[c] >= 0 && cy[c] < Hm) {
-      const float* t = map + ((int64_t)(Hm - 1 - cy[c]) * Wm + cx[c]) * 3;
-      o = o + w[c] * v3(t);
-    }
-  }
-  return o;
-}
-
-struct Slot {
-  int64_t f;
-  int n;
-  float b[3];
-};
 
 // (pixel, slot, image) of slot s: 32-bit divisions when the frame's slots fit (idx32, every
 // BASELINE configuration), a 64-bit division costs ~4x as many instructions per slot
@@ -128,71 +46,6 @@ PR_DEV Slot load_slot(const PRShadeArgs& a, int64_t s, int64_t HW, bool idx32) {
   return sl;
 }
 
-PR_DEV Slot pad_slot(int n) { return Slot{-1, n, {0.f, 0.f, 0.f}}; }
-
-// everything the colour depends on, recomputed identically by the backward
-struct Shade {
-  V3 P, Nn, uvw;     // interpolated position, normal, (u, v, -)
-  V3 tex;            // texel
-  V3 dir, dh, nh;    // light direction (raw, normalized), normal (normalized)
-  float cosang;
-  V3 vraw, view, refl;
-  float dotvr, alpha, mask;
-  Bilin bl;
-};
-
-// fv: the face's vertices (read only when sl.f >= 0); s < 0 skips the per-slot texel of
-// PR_TEX_GIVEN (the per-image padded terms)
-PR_DEV Shade shade(const PRShadeArgs& a, const Slot& sl, int64_t s, const int64_t* fv) {
-  Shade z;
-  const V3 zero{0.f, 0.f, 0.f};
-  z.P = sl.f >= 0 ? interp3(a.verts, fv, sl.b) : zero;
-  z.Nn = sl.f >= 0 ? interp3(a.normals, fv, sl.b) : zero;
-  z.uvw = zero;
-  if (a.texture == PR_TEX_GIVEN) {
-    z.tex = s >= 0 ? v3(a.texels + s * 3) : zero;
-  } else if (a.texture == PR_TEX_VERTEX) {
-    z.tex = sl.f >= 0 ? interp3(a.vert_colors, fv, sl.b) : zero;
-  } else {
-    if (sl.f >= 0) {
-      const float* q = a.face_uvs + sl.f * 6;
-      z.uvw.x = (sl.b[0] * q[0] + sl.b[1] * q[2]) + sl.b[2] * q[4];
-      z.uvw.y = (sl.b[0] * q[1] + sl.b[1] * q[3]) + sl.b[2] * q[5];
-    }
-    z.bl = bilin(z.uvw.x, z.uvw.y, a.Hm, a.Wm);
-    z.tex = bilin_sample(a.maps + (int64_t)sl.n * a.Hm * a.Wm * 3, a.Hm, a.Wm, z.bl);
-  }
-  const V3 L = v3(a.light + sl.n * 3);
-  z.dir = a.directional ? L : L - z.P;
-  z.dh = normalize(z.dir);
-  z.nh = normalize(z.Nn);
-  z.cosang = dot(z.nh, z.dh);
-  z.vraw = v3(a.camera + sl.n * 3) - z.P;
-  z.view = normalize(z.vraw);
-  z.refl = V3{-z.dh.x + 2.f * (z.cosang * z.nh.x), -z.dh.y + 2.f * (z.cosang * z.nh.y),
-              -z.dh.z + 2.f * (z.cosang * z.nh.z)};
-  z.mask = z.cosang > 0.f ? 1.f : 0.f;
-  z.dotvr = dot(z.view, z.refl);
-  z.alpha = fmaxf(z.dotvr, 0.f) * z.mask;
-  return z;
-}
-
-// colour = lit * tex + spec
-struct Terms {
-  V3 lit, spec, tex;
-};
-
-PR_DEV Terms slot_terms(const PRShadeArgs& a, const Slot& sl, int64_t s, const int64_t* fv) {
-  const Shade z = shade(a, sl, s, fv);
-  const int n = sl.n;
-  const float angle = fmaxf(z.cosang, 0.f);
-  const V3 dl = angle * v3(a.diffuse_color + n * 3);
-  const float pw = powf(z.alpha, a.shininess[n]);
-  const V3 sp = pw * v3(a.specular_color + n * 3);
-  return Terms{v3(a.ambient + n * 3) + v3(a.mat_diffuse + n * 3) * dl, v3(a.mat_specular + n * 3) * sp, z.tex};
-}
-
-PR_DEV V3 colour(V3 lit, V3 tex, V3 spec) { return lit * tex + spec; }
 
 // ---- per-wave compaction of the live slots ---------------------------------------------------
 // Each wave takes chunks of 64 R consecutive slots: one pass of flags (the counts, one small read
@@ -409,120 +262,83 @@ PR_DEV void pad_bwd(const PRShadeArgs& a, int64_t s, int64_t ds, int n, const Sh
   }
 }
 
-// live slot: per-slot chain rule in registers, scatters into the LDS table (or the ordered sums)
+// valid slot whose d colour is exactly 0 (every slot the blend gave no weight: all but the
+// winners of some Monte-Carlo sample): every gradient it carries is 0 (finite shading terms times
+// 0), so only its zero d bary (and zero d texel) is written -- the chain rule runs for the others
+template <bool DET>
+PR_DEV void zero_bwd(const PRShadeArgs& a, int64_t s, int64_t ds, const ShadeDet& det) {
+  if (a.grad_bary) { a.grad_bary[s * 3] = 0.f; a.grad_bary[s * 3 + 1] = 0.f; a.grad_bary[s * 3 + 2] = 0.f; }
+  if (a.texture == PR_TEX_GIVEN && a.grad_texels) {
+    float* o = a.grad_texels + s * 3;
+    o[0] = 0.f; o[1] = 0.f; o[2] = 0.f;
+  }
+  if (DET) {
+    if (det.v.n)
+      for (int i = 0; i < 3; ++i) det.v.keys[ds * 3 + i] = (uint32_t)det.v.M;
+    if (det.b.n) det.b.keys[ds] = (uint32_t)det.b.M;
+    if (det.m.n)
+      for (int c = 0; c < 4; ++c) det.m.keys[ds * 4 + c] = (uint32_t)det.m.M;
+  }
+}
+
+// live slot: per-slot chain rule in registers (phong_bwd), scatters into the LDS table (or the
+// ordered sums)
 template <bool DET>
 PR_DEV void slot_bwd(const PRShadeArgs& a, const Slot& sl, int64_t s, int64_t ds, const Tab& tab,
                      const ShadeDet& det, float* lds) {
   const int n = sl.n;
-  const V3 gc = v3(a.grad_colors + s * 3);
   const int64_t* fv = a.faces + sl.f * 3;
-  const Shade z = shade(a, sl, s, fv);
-  const float angle = fmaxf(z.cosang, 0.f);
-  const V3 dcol = v3(a.diffuse_color + n * 3), scol = v3(a.specular_color + n * 3);
-  const V3 mdif = v3(a.mat_diffuse + n * 3), mspec = v3(a.mat_specular + n * 3);
-  const V3 lit = v3(a.ambient + n * 3) + mdif * (angle * dcol);
-  // colour = lit * tex + mspec * (pow(alpha, sh) * scol)
-  const V3 g_tex = lit * gc;
-  const float g_angle = dot(dcol, mdif * z.tex * gc);
-  const float g_pow = dot(scol, mspec * gc);
-  const float sh = a.shininess[n];
-  const float g_alpha = z.alpha > 0.f ? g_pow * sh * powf(z.alpha, sh - 1.f) : 0.f;
-  const float g_dotvr = z.dotvr > 0.f ? g_alpha * z.mask : 0.f;
-  const V3 g_view = g_dotvr * z.refl, g_refl = g_dotvr * z.view;
-  // refl = -dh + 2 c nh
-  V3 g_dh = V3{0.f, 0.f, 0.f} - g_refl;
-  float g_cos = 2.f * dot(g_refl, z.nh) + (z.cosang > 0.f ? g_angle : 0.f);
-  V3 g_nh = (2.f * z.cosang) * g_refl;
-  // c = nh . dh
-  g_nh = g_nh + g_cos * z.dh;
-  g_dh = g_dh + g_cos * z.nh;
-  const V3 g_vraw = normalize_bwd(z.vraw, g_view);
-  const V3 g_dir = normalize_bwd(z.dir, g_dh);
-  const V3 g_Nn = normalize_bwd(z.Nn, g_nh);
-  V3 g_P = V3{0.f, 0.f, 0.f} - g_vraw;
-  if (!a.directional) g_P = g_P - g_dir;
-  // interpolations: d bary and per-vertex scatters
-  float gb[3];
+  const PhongGrad q = phong_bwd(a, sl, s, fv, v3(a.grad_colors + s * 3));
   const float* b = sl.b;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int64_t vi = fv[i];
-    gb[i] = dot(g_P, v3(a.verts + vi * 3)) + dot(g_Nn, v3(a.normals + vi * 3));
     if (DET) {
       if (det.v.n) {
         det.v.keys[ds * 3 + i] = (uint32_t)vi;
         float* e = det.v.vals + (ds * 3 + i) * 9;
-        put3(e, b[i] * g_P);
-        put3(e + 3, b[i] * g_Nn);
-        put3(e + 6, V3{0.f, 0.f, 0.f});
+        put3(e, b[i] * q.g_P);
+        put3(e + 3, b[i] * q.g_Nn);
+        put3(e + 6, a.texture == PR_TEX_VERTEX ? b[i] * q.g_tex : V3{0.f, 0.f, 0.f});
       }
       continue;
     }
-    if (a.grad_verts) acc(lds, tab.useV, tab.vOff + (int)vi * 3, a.grad_verts, vi, b[i] * g_P);
-    if (a.grad_normals) acc(lds, tab.useV, tab.nOff + (int)vi * 3, a.grad_normals, vi, b[i] * g_Nn);
+    if (a.grad_verts) acc(lds, tab.useV, tab.vOff + (int)vi * 3, a.grad_verts, vi, b[i] * q.g_P);
+    if (a.grad_normals) acc(lds, tab.useV, tab.nOff + (int)vi * 3, a.grad_normals, vi, b[i] * q.g_Nn);
+    if (a.texture == PR_TEX_VERTEX && a.grad_vert_colors)
+      acc(lds, tab.useV, tab.cOff + (int)vi * 3, a.grad_vert_colors, vi, b[i] * q.g_tex);
   }
   if (a.texture == PR_TEX_GIVEN) {
     if (a.grad_texels) {
       float* o = a.grad_texels + s * 3;
-      o[0] = g_tex.x; o[1] = g_tex.y; o[2] = g_tex.z;
+      o[0] = q.g_tex.x; o[1] = q.g_tex.y; o[2] = q.g_tex.z;
     }
-  } else if (a.texture == PR_TEX_VERTEX) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int64_t vi = fv[i];
-      gb[i] += dot(g_tex, v3(a.vert_colors + vi * 3));
-      if (DET) {
-        if (det.v.n) put3(det.v.vals + (ds * 3 + i) * 9 + 6, b[i] * g_tex);
-        continue;
-      }
-      if (a.grad_vert_colors) acc(lds, tab.useV, tab.cOff + (int)vi * 3, a.grad_vert_colors, vi, b[i] * g_tex);
-    }
-  } else {
-    // bilinear backward: d texel / d (ix, iy) from the four corners, then d (u, v)
-    const Bilin& bl = z.bl;
-    const float* map = a.maps + (int64_t)n * a.Hm * a.Wm * 3;
-    const float x0 = (float)bl.x0, y0 = (float)bl.y0, x1 = x0 + 1.f, y1 = y0 + 1.f;
-    const int cx[4] = {bl.x0, bl.x0 + 1, bl.x0, bl.x0 + 1}, cy[4] = {bl.y0, bl.y0, bl.y0 + 1, bl.y0 + 1};
-    const float dwx[4] = {-(y1 - bl.iy), (y1 - bl.iy), -(bl.iy - y0), (bl.iy - y0)};
-    const float dwy[4] = {-(x1 - bl.ix), -(bl.ix - x0), (x1 - bl.ix), (bl.ix - x0)};
-    const float w[4] = {(x1 - bl.ix) * (y1 - bl.iy), (bl.ix - x0) * (y1 - bl.iy), (x1 - bl.ix) * (bl.iy - y0),
-                        (bl.ix - x0) * (bl.iy - y0)};
-    float gix = 0.f, giy = 0.f;
+  } else if (a.texture == PR_TEX_UV) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const bool in = cx[c] >= 0 && cx[c] < a.Wm && cy[c] >= 0 && cy[c] < a.Hm;
+      const bool in = q.ti[c] >= 0;
       if (DET && det.m.n) {
-        det.m.keys[ds * 4 + c] = in ? (uint32_t)(((int64_t)n * a.Hm + (a.Hm - 1 - cy[c])) * a.Wm + cx[c])
-                                   : (uint32_t)det.m.M;
-        if (in) put3(det.m.vals + (ds * 4 + c) * 3, w[c] * g_tex);
+        det.m.keys[ds * 4 + c] = in ? (uint32_t)((int64_t)n * a.Hm * a.Wm + q.ti[c] / 3) : (uint32_t)det.m.M;
+        if (in) put3(det.m.vals + (ds * 4 + c) * 3, q.w[c] * q.g_tex);
       }
-      if (in) {
-        const int64_t ti = ((int64_t)(a.Hm - 1 - cy[c]) * a.Wm + cx[c]) * 3;
-        const float gv = dot(v3(map + ti), g_tex);
-        gix += dwx[c] * gv;
-        giy += dwy[c] * gv;
-        if (!DET && a.grad_maps) {
-          float* gm = a.grad_maps + (int64_t)n * a.Hm * a.Wm * 3 + ti;
-          atomicAdd(&gm[0], w[c] * g_tex.x); atomicAdd(&gm[1], w[c] * g_tex.y); atomicAdd(&gm[2], w[c] * g_tex.z);
-        }
+      if (!DET && in && a.grad_maps) {
+        float* gm = a.grad_maps + (int64_t)n * a.Hm * a.Wm * 3 + q.ti[c];
+        atomicAdd(&gm[0], q.w[c] * q.g_tex.x); atomicAdd(&gm[1], q.w[c] * q.g_tex.y);
+        atomicAdd(&gm[2], q.w[c] * q.g_tex.z);
       }
     }
-    const float gu = gix * bl.gx, gvv = giy * bl.gy;
-    const float* q = a.face_uvs + sl.f * 6;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) gb[i] += gu * q[2 * i] + gvv * q[2 * i + 1];
   }
-  if (a.grad_bary) { a.grad_bary[s * 3] = gb[0]; a.grad_bary[s * 3 + 1] = gb[1]; a.grad_bary[s * 3 + 2] = gb[2]; }
+  if (a.grad_bary) { a.grad_bary[s * 3] = q.gb[0]; a.grad_bary[s * 3 + 1] = q.gb[1]; a.grad_bary[s * 3 + 2] = q.gb[2]; }
   if (DET) {
     if (det.b.n) {
       det.b.keys[ds] = (uint32_t)n;
-      put3(det.b.vals + ds * 6, g_dir);
-      put3(det.b.vals + ds * 6 + 3, g_vraw);
+      put3(det.b.vals + ds * 6, q.g_dir);
+      put3(det.b.vals + ds * 6 + 3, q.g_vraw);
     }
     return;
   }
-  if (a.grad_light) acc(lds, tab.useB, tab.lOff + n * 3, a.grad_light, n, g_dir);
-  if (a.grad_camera) acc(lds, tab.useB, tab.camOff + n * 3, a.grad_camera, n, g_vraw);
+  if (a.grad_light) acc(lds, tab.useB, tab.lOff + n * 3, a.grad_light, n, q.g_dir);
+  if (a.grad_camera) acc(lds, tab.useB, tab.camOff + n * 3, a.grad_camera, n, q.g_vraw);
 }
 
 // (slots [s0, PK): the deterministic mode runs the frame in batches; the fast path s0 = 0)
@@ -540,13 +356,18 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
     __syncthreads();
   }
   PR_WAVE_CHUNKS(R, s0, PK, c0, c1) {
-    bool live[R];
+    bool live[R], zero[R];
     int img[R];
     SlotPos q = slot_pos(c0 + lane, a.K, HW, i32);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t s = c0 + r * 64 + lane;
-      live[r] = s < c1 && (a.pix_count ? q.k < a.pix_count[q.p] : a.pix_to_face[s] >= 0);
+      const bool valid = s < c1 && (a.pix_count ? q.k < a.pix_count[q.p] : a.pix_to_face[s] >= 0);
+      // (the list holds the slots with a non-zero d colour only: on a perturbed-blend frame those are
+      // the slots that won a sample, a fraction of the valid ones)
+      const float* gc = a.grad_colors + s * 3;
+      zero[r] = valid && gc[0] == 0.f && gc[1] == 0.f && gc[2] == 0.f;
+      live[r] = valid && !zero[r];
       img[r] = q.n;
       if (r + 1 < R) step64(q, a.K, HW, q64, r64);
     }
@@ -554,7 +375,8 @@ __global__ void __launch_bounds__(kThreads) shade_bwd_kernel(PRShadeArgs a, int6
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t s = c0 + r * 64 + lane;
-      if (s < c1 && !live[r]) pad_bwd<DET>(a, s, s - s0, img[r], det);
+      if (zero[r]) zero_bwd<DET>(a, s, s - s0, det);
+      else if (s < c1 && !live[r]) pad_bwd<DET>(a, s, s - s0, img[r], det);
     }
     for (int i = lane; i < total; i += 64) {
       const int64_t s = c0 + list[i];

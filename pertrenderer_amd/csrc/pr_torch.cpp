@@ -53,6 +53,7 @@ struct Api {
   decltype(&pr_blend_plan_size) blend_plan_size = nullptr;
   decltype(&pr_blend_bwd_workspace_size) blend_bwd_workspace_size = nullptr;
   decltype(&pr_blend_bwd) blend_bwd = nullptr;
+  decltype(&pr_blend_phong_table_bytes) blend_phong_table_bytes = nullptr;
   decltype(&pr_shade_fwd) shade_fwd = nullptr;
   decltype(&pr_shade_bwd_workspace_size) shade_bwd_workspace_size = nullptr;
   decltype(&pr_shade_bwd) shade_bwd = nullptr;
@@ -86,6 +87,7 @@ void bind(const std::unordered_map<std::string, int64_t>& addrs) {
   bind_one(addrs, "pr_blend_plan_size", a.blend_plan_size);
   bind_one(addrs, "pr_blend_bwd_workspace_size", a.blend_bwd_workspace_size);
   bind_one(addrs, "pr_blend_bwd", a.blend_bwd);
+  bind_one(addrs, "pr_blend_phong_table_bytes", a.blend_phong_table_bytes);
   bind_one(addrs, "pr_shade_fwd", a.shade_fwd);
   bind_one(addrs, "pr_shade_bwd_workspace_size", a.shade_bwd_workspace_size);
   bind_one(addrs, "pr_shade_bwd", a.shade_bwd);
@@ -908,6 +910,174 @@ Tensor shade(const Tensor& bary, const Tensor& verts, const Tensor& normals, con
                         directional, live_only, pz);
 }
 
+// ------------------------------------------------------------------ fused Phong blend
+// blend.py _FusedPhongBlendFn: RandomPhongShader's sample_textures -> phong_shading ->
+// smooth_rgb_blend (random_rasterizer.py:99-116) as one pr_blend_fwd / pr_blend_bwd pair
+// (PR_BLEND_PHONG): each slot's colour is shaded where it wins a sample, no (N,H,W,K,3) colour
+// tensor and no pr_shade_* launch.  Gradients: dists, zbuf, bary (-> rasterizer), verts, normals
+// (-> vertex normals), the UV maps or vertex colours, light, camera and the smoothing scalars.
+constexpr int kPhongIn = 28;  // forward arguments
+
+struct BlendPhongFn : public torch::autograd::Function<BlendPhongFn> {
+  // differentiable: 0 dists, 1 zbuf, 2 bary, 3 verts, 4 normals, 5 tex, 6 light, 7 camera,
+  // 8 sigma, 9 gamma, 10 alpha, 11 link
+  static Tensor forward(AutogradContext* ctx, Tensor dists, Tensor zbuf, Tensor bary, Tensor verts, Tensor normals,
+                        Tensor tex, Tensor light, Tensor camera, Opt sigma_o, Opt gamma_o, Opt alpha_o, Opt link_o,
+                        Tensor p2f, Tensor faces, Opt counts_o, Opt face_uvs_o, std::vector<Tensor> rows,
+                        Tensor znear, Tensor zfar, Opt noise_r_o, Opt noise_a_o, Opt seeds_o, int64_t params,
+                        int64_t mode, bool directional, bool cache_on, bool sync_on, bool grad_on) {
+    const Tensor sigma = val(sigma_o), gamma = val(gamma_o), alpha = val(alpha_o), link = val(link_o);
+    const Tensor counts = val(counts_o), face_uvs = val(face_uvs_o);
+    const Tensor noise_r = val(noise_r_o), noise_a = val(noise_a_o), seeds = val(seeds_o);
+    if (rows.size() != 6) throw std::invalid_argument("blend_phong: 6 parameter rows expected");
+    on_device({&dists, &zbuf, &bary, &verts, &normals, &tex, &light, &camera, &p2f, &faces, &counts, &face_uvs,
+               &znear, &zfar, &noise_r, &noise_a, &seeds});
+    for (const auto& r : rows) on_device({&r});
+    const Tensor diff[12] = {dists, zbuf, bary, verts, normals, tex, light, camera, sigma, gamma, alpha, link};
+    int64_t need = 0;
+    for (int i = 0; i < 12; ++i)
+      need |= (grad_on && diff[i].defined() && diff[i].requires_grad()) ? (int64_t{1} << i) : 0;
+    ctx->saved_data["need"] = need;
+    PRBlendParams p;
+    std::memcpy(&p, reinterpret_cast<const void*>(static_cast<intptr_t>(params)), sizeof(p));
+    const int64_t N = p.N, H = p.H, W = p.W, K = p.K;
+    auto p2f_c = dense(p2f, at::kLong), f_c = dense(faces, at::kLong);
+    auto d_c = dense(dists, at::kFloat), z_c = dense(zbuf, at::kFloat);
+    Tensor t[6] = {dense(bary, at::kFloat),  dense(verts, at::kFloat), dense(normals, at::kFloat),
+                   dense(tex, at::kFloat),   dense(light, at::kFloat), dense(camera, at::kFloat)};
+    auto image = empty({N, H, W, 4}, at::kFloat, p2f_c);
+    auto winners = empty({N * H * W, p.Sa}, at::kByte, p2f_c);
+    Tensor cache = cache_on && need != 0 ? empty({N, H, W, K, 2}, at::kFloat, p2f_c) : Tensor();
+    PRShadeArgs sh{};
+    shade_common(sh, p2f_c, counts, f_c, face_uvs, t, rows.data(), mode, directional);
+    PRBlendFwdArgs a{};
+    a.p = p;
+    a.pix_to_face = ptr<int64_t>(p2f_c);
+    a.dists = ptr<float>(d_c);
+    a.zbuf = ptr<float>(z_c);
+    a.bary = ptr<float>(t[0]);
+    a.image = ptr<float>(image);
+    a.winners = ptr<uint8_t>(winners);
+    a.rast_cache = ptr<float>(cache);
+    a.pix_count = ptr<int32_t>(counts);
+    a.shade = &sh;
+    at::DeviceGuard dg(p2f_c.device());
+    Tensor sync = sync_on ? at::empty({PR_BLEND_SYNC_BYTES / 4}, p2f_c.options().dtype(at::kInt)) : Tensor();
+    // a small mesh's per-vertex / per-image gradient table (zeroed by the forward's kernel)
+    const size_t tb = need != 0 ? api().blend_phong_table_bytes(&p, &sh) : 0;
+    Tensor table = tb ? at::empty({static_cast<int64_t>(tb / 4)}, p2f_c.options().dtype(at::kFloat)) : Tensor();
+    a.phong_table = ptr<float>(table);
+    a.sync = ptr<int32_t>(sync);
+    check(api().blend_fwd(&a, stream_of(image)), "pr_blend_fwd (phong)");
+    ctx->saved_data["p"] = std::string(reinterpret_cast<const char*>(&p), sizeof(p));
+    ctx->saved_data["mode"] = mode;
+    ctx->saved_data["directional"] = directional;
+    Keep k(ctx);
+    for (int i = 0; i < 6; ++i) k(kShadeKeys[i], t[i]);
+    for (int i = 0; i < 6; ++i) k(kShadeRows[i], rows[i]);
+    const char* names[] = {"p2f", "d", "z", "f", "counts", "face_uvs", "zn", "zf", "nr", "na", "seeds",
+                           "winners", "cache", "sync", "table", "s0", "s1", "s2"};
+    const Tensor ts[] = {p2f_c, d_c, z_c, f_c, counts, face_uvs, znear, zfar, noise_r, noise_a, seeds,
+                         winners, cache, sync, table, sigma, gamma, alpha};
+    for (size_t i = 0; i < sizeof(ts) / sizeof(ts[0]); ++i) k(names[i], ts[i]);
+    k.commit();
+    return image;
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    variable_list out(kPhongIn);
+    const auto pb = ctx->saved_data["p"].toStringRef();
+    PRBlendParams p;
+    std::memcpy(&p, pb.data(), sizeof(p));
+    if (p.flags & PR_BLEND_AGG_UNIFORM)
+      throw std::runtime_error("UniformAgg: the reference implements no gradient for uniform noise "
+                               "(smoothagg.py:64-70)");
+    if (!grads[0].defined()) return out;
+    const int64_t need = ctx->saved_data["need"].toInt();
+    auto needs = [need](int i) { return ((need >> i) & 1) != 0; };
+    const int64_t mode = ctx->saved_data["mode"].toInt();
+    const Saved sv(ctx);
+    Tensor t[6], rows[6];
+    for (int i = 0; i < 6; ++i) t[i] = sv(kShadeKeys[i]);
+    for (int i = 0; i < 6; ++i) rows[i] = sv(kShadeRows[i]);
+    auto p2f = sv("p2f"), d = sv("d"), z = sv("z");
+    auto g = dense(grads[0], at::kFloat);
+    auto gd = at::empty_like(d), gz = at::empty_like(z), gb = at::empty_like(t[0]);
+    // the mesh / texture / light / camera gradients: accumulated by the kernel, except those the
+    // small-mesh table writes (verts, normals, vertex colours, light, camera)
+    const Tensor table = sv("table");
+    Tensor acc[6];
+    for (int i = 1; i < 6; ++i) {
+      if (!needs(2 + i)) continue;
+      const bool written = table.defined() && (i != 3 || mode == PR_TEX_VERTEX);
+      acc[i] = written ? at::empty_like(t[i]) : at::zeros_like(t[i]);
+    }
+    auto gsc = at::empty({3}, d.options());
+    PRShadeArgs sh{};
+    shade_common(sh, p2f, sv("counts"), sv("f"), sv("face_uvs"), t, rows, mode,
+                 ctx->saved_data["directional"].toBool());
+    sh.grad_verts = ptr<float>(acc[1]);
+    sh.grad_normals = ptr<float>(acc[2]);
+    if (mode == PR_TEX_VERTEX) sh.grad_vert_colors = ptr<float>(acc[3]);
+    else sh.grad_maps = ptr<float>(acc[3]);
+    sh.grad_light = ptr<float>(acc[4]);
+    sh.grad_camera = ptr<float>(acc[5]);
+    PRBlendBwdArgs a{};
+    a.p = p;
+    a.pix_to_face = ptr<int64_t>(p2f);
+    a.dists = ptr<float>(d);
+    a.zbuf = ptr<float>(z);
+    a.bary = ptr<float>(t[0]);
+    a.grad_bary = ptr<float>(gb);
+    a.winners = ptr<uint8_t>(sv("winners"));
+    a.grad_image = ptr<float>(g);
+    a.rast_cache = ptr<float>(sv("cache"));
+    a.grad_dists = ptr<float>(gd);
+    a.grad_zbuf = ptr<float>(gz);
+    a.grad_scalars = ptr<float>(gsc);
+    a.pix_count = ptr<int32_t>(sv("counts"));
+    a.sync = ptr<int32_t>(sv("sync"));
+    a.shade = &sh;
+    a.phong_table = ptr<float>(table);
+    at::DeviceGuard dg(d.device());
+    auto ws = workspace(api().blend_bwd_workspace_size(&a), d);
+    a.workspace = ws.data_ptr();
+    a.workspace_bytes = static_cast<size_t>(ws.numel());
+    void* st = stream_of(g);
+    check(api().blend_bwd(&a, st), "pr_blend_bwd (phong)");
+    if (needs(0)) out[0] = gd;
+    if (needs(1)) out[1] = gz;
+    if (needs(2)) out[2] = gb;
+    for (int i = 1; i < 6; ++i) out[2 + i] = acc[i];
+    Tensor host;
+    for (int i = 0; i < 3; ++i) {
+      auto ref = sv(i == 0 ? "s0" : i == 1 ? "s1" : "s2");
+      if (!needs(8 + i) || !ref.defined()) continue;
+      if (ref.device().is_cpu()) {
+        if (!host.defined()) host = gsc.to(at::kCPU);
+        out[8 + i] = host[i].to(ref.scalar_type()).reshape(ref.sizes());
+      } else {
+        out[8 + i] = gsc[i].to(ref.scalar_type()).reshape(ref.sizes());
+      }
+    }
+    if (needs(11)) {
+      mark_ready(gsc, st);
+      out[11] = gsc;
+    }
+    return once(grads, out);
+  }
+};
+
+Tensor blend_phong(const Tensor& dists, const Tensor& zbuf, const Tensor& bary, const Tensor& verts,
+                   const Tensor& normals, const Tensor& tex, const Tensor& light, const Tensor& camera, Opt sigma,
+                   Opt gamma, Opt alpha, Opt link, const Tensor& p2f, const Tensor& faces, Opt counts, Opt face_uvs,
+                   std::vector<Tensor> rows, const Tensor& znear, const Tensor& zfar, Opt noise_r, Opt noise_a,
+                   Opt seeds, int64_t params, int64_t mode, bool directional, bool cache_on, bool sync_on) {
+  return BlendPhongFn::apply(dists, zbuf, bary, verts, normals, tex, light, camera, sigma, gamma, alpha, link, p2f,
+                             faces, counts, face_uvs, rows, znear, zfar, noise_r, noise_a, seeds, params, mode,
+                             directional, cache_on, sync_on, at::GradMode::is_enabled());
+}
+
 struct VertNormalsFn : public torch::autograd::Function<VertNormalsFn> {
   static Tensor forward(AutogradContext* ctx, Tensor verts, Tensor faces, Opt csr_start_o, Opt csr_corners_o) {
     const Tensor cs = val(csr_start_o), cc = val(csr_corners_o);
@@ -979,5 +1149,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("blend", &blend);
   m.def("scalar_link", &scalar_link);
   m.def("shade", &shade);
+  m.def("blend_phong", &blend_phong);
   m.def("vert_normals", &vert_normals);
 }

@@ -11,6 +11,8 @@ RandomSimpleShader / RandomPhongShader (random_rasterizer.py:60-191) are
 smoothing mutators.  SimpleShader / SoftSimpleShader (random_rasterizer.py:194-214)
 wrap the hard / softmax blends.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -22,7 +24,7 @@ from .renderer.cameras import OpenGLPerspectiveCameras, look_at_view_transform
 from .renderer.blending import hard_rgb_blend, sigmoid_alpha_blend, softmax_rgb_blend  # noqa: F401
 from .renderer.mesh import TexturesVertex
 from .renderer.renderer import BlendParams, Materials, PointLights
-from .renderer.shading import phong_shading, textured_phong_shading  # noqa: F401
+from .renderer.shading import phong_inputs, phong_shading, textured_phong_shading  # noqa: F401
 from .smoothagg import GaussianAgg, SoftAgg, _PerturbedAgg
 from .smoothrast import GaussianRast, SoftRast, _PerturbedRast
 
@@ -90,6 +92,10 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
 # RandomSimpleShader fuses TexturesVertex sampling into the blend on the GPU (set
 # False to sample texels first; results are bit-identical, see tests/test_gpu_fused_texture.py)
 FUSE_VERTEX_TEXTURES = True
+# RandomPhongShader fuses the Phong shading (TexturesUV / TexturesVertex) into the blend on the GPU
+# (set False to shade every slot first: pr_shade_* then the texel blend; the image is bit-identical,
+# gradients agree to float-atomic order, tests/test_gpu_phong_fused.py)
+FUSE_PHONG = os.environ.get("PR_FUSE_PHONG", "1") != "0"
 
 
 def _vertex_colors(meshes):
@@ -189,8 +195,22 @@ class RandomPhongShader(_RandomShaderBase):
             (_is_fusable(self.smoothrast, self.smoothagg, fragments) and _multidevice.sample_devices() is None)
             or (type(self.smoothrast) is SoftRast and type(self.smoothagg) is SoftAgg
                 and fragments.pix_to_face.is_cuda))
-        colors = textured_phong_shading(meshes, fragments, lights, cameras, materials, live_only=live_only)
         znear, zfar = _planes_from(cameras, kwargs)
+        sr, sa = self.smoothrast, self.smoothagg
+        if (FUSE_PHONG and _is_fusable(sr, sa, fragments) and _multidevice.sample_devices() is None
+                and not torch.are_deterministic_algorithms_enabled()):
+            # the shading fused into the blend (PR_BLEND_PHONG): a slot is shaded only where it wins
+            # a sample, no (N,H,W,K,3) colour tensor, no shading kernels.  (Its mesh / texture / light
+            # gradients are float-atomic sums: deterministic mode shades first, pr_shade_bwd's
+            # ordered sums.)
+            sh = phong_inputs(meshes, fragments, lights, cameras, materials)
+            if sh is not None:
+                return _blend.perturbed_blend_phong(
+                    sh, fragments.pix_to_face, fragments.bary_coords, fragments.dists, fragments.zbuf, sr.sigma,
+                    sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,
+                    background=blend_params.background_color, znear=znear, zfar=zfar, fixed_noise=sa.fixed_noise,
+                    live_only=live_only, **_variant_kw(sr, sa))
+        colors = textured_phong_shading(meshes, fragments, lights, cameras, materials, live_only=live_only)
         # (the blend's live-only backward also needs a live-only consumer of d colours: only when
         # the native shading ran live-only -- it marks its output -- are d colours read per live slot)
         return smooth_rgb_blend(colors, fragments, self.smoothrast, self.smoothagg, blend_params,

@@ -226,6 +226,41 @@ def _shade_native(meshes, fragments, lights, cameras, materials, mode, tex, face
     return out
 
 
+def phong_inputs(meshes, fragments, lights, cameras, materials):
+    """The native shading's inputs for a TexturesUV (maps of one size, 3 channels) or 3-channel
+    TexturesVertex mesh on the GPU with constant lights / materials -- what pr_shade_* and the blend's
+    fused Phong colour mode (PR_BLEND_PHONG) take -- or None when the texture or parameters are
+    outside the native path."""
+    from .rasterizer import valid_counts
+    from .textures import TexturesUV
+    if not _native_ok(fragments, lights, materials):
+        return None
+    tex = getattr(meshes, "textures", None)
+    p2f = fragments.pix_to_face
+    N = p2f.shape[0]
+    dev = p2f.device
+    if isinstance(tex, TexturesUV) and tex.fusable():
+        maps = tex.maps_padded().to(dev)
+        if maps.shape[0] != N or maps.shape[-1] != 3:
+            return None
+        mode, texture = nat.PR_TEX_UV, maps
+        face_uvs = tex.faces_verts_uvs_packed().to(device=dev, dtype=F32).detach().contiguous()
+    elif isinstance(tex, TexturesVertex):
+        vc = tex.verts_features_packed()
+        if vc.dim() != 2 or vc.shape[-1] != 3:
+            return None
+        mode, texture, face_uvs = nat.PR_TEX_VERTEX, vc, None
+    else:
+        return None
+    counts = valid_counts(p2f)
+    if counts is not None and (counts.device != dev or tuple(counts.shape) != tuple(p2f.shape[:3])):
+        counts = None
+    return dict(mode=mode, tex=texture, face_uvs=face_uvs, verts=meshes.verts_packed(),
+                normals=meshes.verts_normals_packed(), faces=meshes.faces_packed().to(torch.int64).contiguous(),
+                light=_rows(lights.location, N, dev), camera=_rows(cameras.get_camera_center(), N, dev),
+                rows=_param_rows(lights, materials, N, dev), directional=_is_directional(lights), counts=counts)
+
+
 def phong_shading(meshes, fragments, lights, cameras, materials, texels):
     """PyTorch3D phong_shading(meshes, fragments, lights, cameras, materials, texels)."""
     if _native_ok(fragments, lights, materials):

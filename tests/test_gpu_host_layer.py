@@ -139,10 +139,17 @@ def test_layer_is_used_in_eager_step(device):
     assert any("ProjectRasterizeFn" in n for n in names), names
 
 
-def test_eval_scene_uses_cpp_shading_and_normals(device):
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_eval_scene_uses_cpp_shading_and_normals(device, deterministic):
+    """eval.py's renderer in the C++ layer: the fused Phong blend node (BlendPhongFn) and the vertex
+    normals; in deterministic mode the shading node (ShadeFn, ordered sums) then the texel blend."""
     import bench
     wl = bench.Workload(device, image_size=64, K=20, samples=8, eval_scene=True, rast_samples=16)
-    loss = wl.forward()
+    torch.use_deterministic_algorithms(deterministic, warn_only=True)
+    try:
+        loss = wl.forward()
+    finally:
+        torch.use_deterministic_algorithms(False)
     names, stack, seen, held = [], [loss.grad_fn], set(), []
     while stack:
         fn = stack.pop()
@@ -152,5 +159,6 @@ def test_eval_scene_uses_cpp_shading_and_normals(device):
         seen.add(id(fn))
         names.append(fn.name())
         stack.extend(f for f, _ in fn.next_functions)
-    assert any("ShadeFn" in n for n in names) and any("VertNormalsFn" in n for n in names), names
+    shading = "ShadeFn" if deterministic else "BlendPhongFn"
+    assert any(shading in n for n in names) and any("VertNormalsFn" in n for n in names), names
     assert not any(n.startswith("_") and n.endswith("Backward") for n in names), names
