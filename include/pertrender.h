@@ -85,12 +85,18 @@ extern "C" {
 #define PR_BLEND_LIVE_ONLY 1024 /* with RAST and pix_count: pr_blend_bwd leaves the masked slots' d zbuf / d dists / */
                                 /* d colour / d bary unwritten, for a caller whose consumers read the valid prefix */
                                 /* only (the rasterizer backward, the live-only shading; ABI 19) */
-#define PR_BLEND_PHONG 2048     /* with RAST | COLOR (not VERTEX): each slot's colour is Phong-shaded on demand */
-                                /* from `shade` (PRShadeArgs: mesh, vertex normals, TexturesUV map or vertex  */
-                                /* colours, lights, materials, camera) -- RandomPhongShader's sample_textures */
-                                /* -> phong_shading -> smooth_rgb_blend (random_rasterizer.py:99-116) with no */
-                                /* (N,H,W,K,3) colour tensor: the forward shades the slots that win a sample, */
-                                /* the backward the winners and the unperturbed argmax (ABI 20)              */
+#define PR_BLEND_PHONG 2048     /* pr_blend_fwd with RAST | COLOR (not VERTEX): each slot's colour is Phong-     */
+                                /* shaded on demand from `shade` (PRShadeArgs: mesh, vertex normals, TexturesUV */
+                                /* map or vertex colours, lights, materials, camera) -- RandomPhongShader's     */
+                                /* sample_textures -> phong_shading -> smooth_rgb_blend (random_rasterizer.py:  */
+                                /* 99-116) shading only the slots that win a sample.  With `colors` given (an   */
+                                /* OUTPUT here) the colours of exactly the slots the backward reads -- the      */
+                                /* winners and each pixel's unperturbed argmax -- are written there, nothing    */
+                                /* else; the non-null shade.grad_verts / grad_normals / grad_vert_colors        */
+                                /* (VERTEX) / grad_light / grad_camera are zeroed, for a PR_GRAD_PREZEROED      */
+                                /* pr_shade_bwd (ABI 20)                                                        */
+#define PR_BLEND_COLOR_SPARSE 4096 /* pr_blend_bwd with RAST | COLOR: `colors` holds valid values at the slots */
+                                /* PR_BLEND_PHONG's forward wrote only; d colors as usual (then pr_shade_bwd)   */
 
 struct PRShadeArgs;
 
@@ -149,14 +155,10 @@ typedef struct PRBlendFwdArgs {
    * package passes it unless PR_BLEND_SYNC=0 */
   int32_t* sync;
   /* PHONG: the shading inputs (texture PR_TEX_UV or PR_TEX_VERTEX; its N,H,W,K, pix_to_face, pix_count, */
-  /* bary are the blend's own and ignored; colors / grad_* ignored in the forward).  Host memory, read */
-  /* during the call (the kernels get a copy).  The blend's `bary` is the fragments' barycentrics.     */
+  /* bary are the blend's own and ignored; its colors / grad_colors / grad_bary / grad_maps ignored).   */
+  /* Host memory, read during the call (the kernels get a copy).  The blend's `bary` is the fragments'  */
+  /* barycentrics.                                                                                    */
   const struct PRShadeArgs* shade;
-  /* PHONG, nullable: >= pr_blend_phong_table_bytes(&p, shade) bytes (0: none for this mesh) that the
-   * forward zeroes; handed to pr_blend_bwd of the same call, its workgroups sum a small mesh's      */
-  /* per-vertex (verts, normals, vertex colours) and per-image (light, camera) gradients there and   */
-  /* its last workgroup writes them out (those outputs are then overwritten, not accumulated)        */
-  float* phong_table;
 } PRBlendFwdArgs;
 
 typedef struct PRBlendBwdArgs {
@@ -189,8 +191,6 @@ typedef struct PRBlendBwdArgs {
   /* PHONG: as in PRBlendFwdArgs; its non-null grad_verts, grad_normals, grad_maps (UV) or     */
   /* grad_vert_colors (VERTEX), grad_light, grad_camera are ACCUMULATED (the caller zeroes them); */
   /* d bary goes to grad_bary (replaces grad_colors)                                            */
-  const struct PRShadeArgs* shade;
-  float* phong_table;         /* PHONG, nullable: the forward's phong_table of the same call */
 } PRBlendBwdArgs;
 
 typedef struct PRHeavisideArgs {
@@ -352,9 +352,6 @@ typedef struct PRShadeArgs {
 } PRShadeArgs;
 
 int pr_shade_fwd(const PRShadeArgs* args, void* stream);
-/* PR_BLEND_PHONG's small-mesh table (PRBlendFwdArgs.phong_table): its bytes for the call, 0 when the
- * mesh is too large for it (the backward then accumulates into caller-zeroed outputs) */
-size_t pr_blend_phong_table_bytes(const PRBlendParams* p, const PRShadeArgs* shade);
 size_t pr_shade_bwd_workspace_size(const PRShadeArgs* args);
 int pr_shade_bwd(const PRShadeArgs* args, void* stream);
 

@@ -23,7 +23,8 @@ PR_BLEND_AGG_CAUCHY = 16
 PR_BLEND_AGG_UNIFORM = 256
 PR_BLEND_WINNERS_IN = 512
 PR_BLEND_LIVE_ONLY = 1024
-PR_BLEND_PHONG = 2048  # RandomPhongShader's shading fused into the blend (PRBlend*Args.shade)
+PR_BLEND_PHONG = 2048  # forward: RandomPhongShader's shading on demand (PRBlendFwdArgs.shade)
+PR_BLEND_COLOR_SPARSE = 4096  # backward of PR_BLEND_PHONG: colours valid at the slots it reads only
 PR_BLEND_RAST_WOVR = 32
 PR_BLEND_AGG_WOVR = 64
 PR_BLEND_SOFT = 128
@@ -51,8 +52,7 @@ class PRBlendFwdArgs(C.Structure):
     _fields_ = [("p", PRBlendParams), ("pix_to_face", _vp), ("mask", _vp), ("dists", _vp),
                 ("prob", _vp), ("zbuf", _vp), ("colors", _vp), ("image", _vp), ("weights", _vp),
                 ("winners", _vp), ("rast_cache", _vp), ("bary", _vp), ("faces", _vp), ("vert_colors", _vp),
-                ("pix_count", _vp), ("plan", _vp), ("sync", _vp), ("shade", _vp),
-                ("phong_table", _vp)]
+                ("pix_count", _vp), ("plan", _vp), ("sync", _vp), ("shade", _vp)]
 
 
 class PRBlendBwdArgs(C.Structure):
@@ -62,8 +62,7 @@ class PRBlendBwdArgs(C.Structure):
                 ("grad_zbuf", _vp), ("grad_colors", _vp), ("grad_scalars", _vp),
                 ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("rast_cache", _vp), ("bary", _vp),
                 ("faces", _vp), ("vert_colors", _vp), ("grad_bary", _vp), ("grad_vert_colors", _vp),
-                ("pix_count", _vp), ("plan", _vp), ("sync", _vp), ("shade", _vp),
-                ("phong_table", _vp)]
+                ("pix_count", _vp), ("plan", _vp), ("sync", _vp)]
 
 
 class PRHeavisideArgs(C.Structure):
@@ -153,7 +152,6 @@ EXPORTS = {
     "pr_last_error": (C.c_char_p, []),
     "pr_ktimer_arm": (C.c_int, [C.c_int32]),
     "pr_blend_plan_size": (C.c_size_t, [C.POINTER(PRBlendParams)]),
-    "pr_blend_phong_table_bytes": (C.c_size_t, [C.POINTER(PRBlendParams), C.POINTER(PRShadeArgs)]),
     "pr_ktimer_read": (C.c_int, [C.c_int32, C.POINTER(C.c_float), C.c_char_p, C.c_int32]),
     "pr_blend_fwd": (C.c_int, [C.POINTER(PRBlendFwdArgs), _vp]),
     "pr_blend_bwd_workspace_size": (C.c_size_t, [C.POINTER(PRBlendBwdArgs)]),

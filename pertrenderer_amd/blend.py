@@ -521,10 +521,12 @@ def _phong_args(sh, p2f_c, t):
 
 
 class _FusedPhongBlendFn(torch.autograd.Function):
-    """perturbed_blend with RandomPhongShader's shading fused in (PR_BLEND_PHONG): each slot's
-    colour is Phong-shaded where it wins a sample (TexturesUV / TexturesVertex texel, point or
-    directional light), so no (N,H,W,K,3) colour tensor exists; gradients go to dists, zbuf, bary,
-    the vertex positions and normals, the texture, the light and the camera centre."""
+    """perturbed_blend with RandomPhongShader's shading fused into the forward (PR_BLEND_PHONG):
+    a slot's colour is Phong-shaded only where it wins a sample (TexturesUV / TexturesVertex texel,
+    point or directional light), and only the colours the backward reads (winners, each pixel's
+    unperturbed argmax) are kept.  Backward: pr_blend_bwd on those (PR_BLEND_COLOR_SPARSE) -> d colours
+    -> pr_shade_bwd (its chain rule for the slots with a non-zero d colour only); gradients go to
+    dists, zbuf, bary, the vertex positions and normals, the texture, the light and the camera."""
 
     @staticmethod
     def forward(ctx, dists, zbuf, bary, verts, normals, tex, light, camera, sigma, gamma, alpha, link, p2f, znear,
@@ -541,23 +543,22 @@ class _FusedPhongBlendFn(torch.autograd.Function):
         sc, sc_dev = _scalars((sigma, gamma, alpha), dev)
         flags = nat.PR_BLEND_RAST | nat.PR_BLEND_COLOR | nat.PR_BLEND_PHONG | cfg["vflags"]
         p = _params((N, H, W, K), cfg["Sr"], cfg["Sa"], sc, sc_dev, cfg["eps"], cfg["bg"], noise, zn, zf, flags)
+        need = ctx.needs_input_grad
+        any_grad = any(need[:12])
         image = torch.empty((N, H, W, 4), dtype=F32, device=dev)
         winners = torch.empty((N * H * W, cfg["Sa"]), dtype=torch.uint8, device=dev)
-        cache = (torch.empty((N, H, W, K, 2), dtype=F32, device=dev)
-                 if RAST_CACHE and any(ctx.needs_input_grad[:12]) else None)
+        cache = torch.empty((N, H, W, K, 2), dtype=F32, device=dev) if RAST_CACHE and any_grad else None
+        # the colours the backward reads, written at those slots only
+        colors = torch.empty((N, H, W, K, 3), dtype=F32, device=dev) if any_grad else None
         sync = _sync(dev)
         shade = _phong_args(sh, p2f_c, t)
-        # a small mesh's per-vertex / per-image gradient table (zeroed by the forward's kernel)
-        tb = nat.load().pr_blend_phong_table_bytes(p, shade) if any(ctx.needs_input_grad[:12]) else 0
-        table = torch.empty(tb // 4, dtype=F32, device=dev) if tb else None
         a = nat.PRBlendFwdArgs()
         a.p = p
-        a.phong_table = nat.ptr(table)
         a.pix_to_face, a.zbuf, a.dists, a.bary = nat.ptr(p2f_c), nat.ptr(z_c), nat.ptr(d_c), nat.ptr(t["bary"])
-        a.image, a.winners, a.rast_cache = nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
+        a.colors, a.image, a.winners, a.rast_cache = nat.ptr(colors), nat.ptr(image), nat.ptr(winners), nat.ptr(cache)
         a.pix_count, a.sync, a.shade = nat.ptr(cfg["counts"]), nat.ptr(sync), nat.C.addressof(shade)
         _timed("blend_fwd", lambda: nat.call("pr_blend_fwd", "pr_blend_fwd", image, a))
-        ctx.save_for_backward(p2f_c, d_c, z_c, zn, zf, winners, cache, sync, table, *t.values())
+        ctx.save_for_backward(p2f_c, d_c, z_c, zn, zf, winners, cache, sync, colors, *t.values())
         ctx.p, ctx.sc_dev, ctx.cfg, ctx.sh, ctx.noise = p, sc_dev, cfg, sh, noise
         ctx.refs = (sigma, gamma, alpha)
         return image
@@ -566,39 +567,44 @@ class _FusedPhongBlendFn(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, gimg):
         _no_uniform_grad(ctx.cfg.get("vflags", 0))
-        p2f_c, d_c, z_c, zn, zf, winners, cache, sync, table, *tv = ctx.saved_tensors
+        p2f_c, d_c, z_c, zn, zf, winners, cache, sync, colors, *tv = ctx.saved_tensors
         t = dict(zip(("bary", "verts", "normals", "tex", "light", "camera"), tv))
         cfg, sh = ctx.cfg, ctx.sh
         lib = nat.load()
         dev = p2f_c.device
         need = ctx.needs_input_grad
         g = nat.dense(gimg, F32)
-        gd, gz, gb = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(t["bary"])
-        # mesh / texture / light / camera gradients: accumulated by the kernel, except those the
-        # small-mesh table writes (verts, normals, vertex colours, light, camera)
-        written = lambda k: table is not None and (k != "tex" or sh["mode"] == nat.PR_TEX_VERTEX)
-        acc = [(torch.empty_like(t[k]) if written(k) else torch.zeros_like(t[k])) if need[3 + i] else None
-               for i, k in enumerate(("verts", "normals", "tex", "light", "camera"))]
+        # 1. blend backward on the sparse colours
+        p = nat.PRBlendParams.from_buffer_copy(ctx.p)
+        p.flags = (p.flags & ~nat.PR_BLEND_PHONG) | nat.PR_BLEND_COLOR_SPARSE
+        gd, gz, gc = torch.empty_like(d_c), torch.empty_like(z_c), torch.empty_like(colors)
         gsc = torch.empty(3, dtype=F32, device=dev)
-        shade = _phong_args(sh, p2f_c, t)
-        shade.grad_verts, shade.grad_normals = nat.ptr(acc[0]), nat.ptr(acc[1])
-        if sh["mode"] == nat.PR_TEX_VERTEX:
-            shade.grad_vert_colors = nat.ptr(acc[2])
-        else:
-            shade.grad_maps = nat.ptr(acc[2])
-        shade.grad_light, shade.grad_camera = nat.ptr(acc[3]), nat.ptr(acc[4])
         a = nat.PRBlendBwdArgs()
-        a.p = ctx.p
-        a.pix_to_face, a.zbuf, a.dists, a.bary = nat.ptr(p2f_c), nat.ptr(z_c), nat.ptr(d_c), nat.ptr(t["bary"])
+        a.p = p
+        a.pix_to_face, a.zbuf, a.dists, a.colors = nat.ptr(p2f_c), nat.ptr(z_c), nat.ptr(d_c), nat.ptr(colors)
         a.winners, a.grad_image, a.rast_cache = nat.ptr(winners), nat.ptr(g), nat.ptr(cache)
-        a.grad_dists, a.grad_zbuf, a.grad_bary, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gb), nat.ptr(gsc)
-        a.pix_count, a.sync, a.shade = nat.ptr(cfg["counts"]), nat.ptr(sync), nat.C.addressof(shade)
-        a.phong_table = nat.ptr(table)
+        a.grad_dists, a.grad_zbuf, a.grad_colors, a.grad_scalars = nat.ptr(gd), nat.ptr(gz), nat.ptr(gc), nat.ptr(gsc)
+        a.pix_count, a.sync = nat.ptr(cfg["counts"]), nat.ptr(sync)
         ws = torch.empty(max(1, lib.pr_blend_bwd_workspace_size(a)), dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = nat.ptr(ws), ws.numel()
         _timed("blend_bwd", lambda: nat.call("pr_blend_bwd", "pr_blend_bwd", g, a))
+        # 2. shading backward (the zero-d-colour slots skipped by the kernel)
+        keys = ("bary", "verts", "normals", "tex", "light", "camera")
+        out = [torch.empty_like(t[k]) if need[2 + i] else None for i, k in enumerate(keys)]
+        if any(o is not None for o in out):
+            from .renderer.shading import _shade_bwd_args
+            sa = _shade_bwd_args(_phong_args(sh, p2f_c, t), sh["mode"], gc, out)
+            if p.flags & nat.PR_BLEND_LIVE_ONLY and cfg["counts"] is not None:
+                sa.flags |= nat.PR_SHADE_LIVE_ONLY
+            wss = None
+            if nat.deterministic():
+                sa.flags |= nat.PR_DETERMINISTIC
+                wss = nat.workspace(lib.pr_shade_bwd_workspace_size(sa), dev)
+                sa.workspace, sa.workspace_bytes = nat.ptr(wss), wss.numel()
+            nat.call("pr_shade_bwd", "pr_shade_bwd", g, sa)
+            del wss
         s_g, g_g, a_g = _scalar_grads(gsc, need[8:11], ctx.refs)
-        return (gd if need[0] else None, gz if need[1] else None, gb if need[2] else None, *acc,
+        return (gd if need[0] else None, gz if need[1] else None, *out,
                 s_g, g_g, a_g, _link_grad(gsc, need[11]), None, None, None, None, None)
 
 

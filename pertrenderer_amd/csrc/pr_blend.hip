@@ -531,26 +531,8 @@ PR_DEV int agg_num_groups(const PRBlendParams& p) {
 // the shading inputs the host passed by pointer (PRBlend*Args.shade)
 struct FwdK : PRBlendFwdArgs {
   PRShadeArgs sh;
-  int pt_n;  // CM 3: floats of phong_table the forward zeroes
 };
-struct BwdK : PRBlendBwdArgs {
-  PRShadeArgs sh;
-  // CM 3 small-mesh table (pt_T > 0, PRBlendBwdArgs.phong_table): the per-vertex (verts | normals |
-  // vertex colours) and per-image (light | camera) gradients of a workgroup summed in LDS (pt_T
-  // floats), flushed by one device-scope atomic per touched entry into copy (block % pt_R) of the
-  // table, whose copies the last workgroup (or phong_table_reduce_kernel) sums into the outputs and
-  // zeroes.  A frame's slots all scatter into a few vertices: global atomics straight to them
-  // serialise on one or two cache lines (eval.py's cube: blend_bwd 1.1 ms); spread over the
-  // copies they do not.
-  int pt_T, pt_R;                 // table floats, copies
-  int pt_off;                     // LDS offset (floats) of the table, then the B2c work list
-  int pt_nrm, pt_vc, pt_l, pt_c;  // offsets of the normals / vertex colours / light / camera parts
-};
-#ifndef PR_PHONG_BWD_WPE  // waves per SIMD the CM 3 backward is built for (its Phong state: 128 VGPRs at 4)
-#define PR_PHONG_BWD_WPE 4
-#endif
-constexpr int kPhongTabMax = 4096;  // floats (16 KB of LDS) for the table, else global atomics
-constexpr int kPhongCopies = 32;
+struct BwdK : PRBlendBwdArgs {};
 
 // image of slot gs (one-frame calls: 0 without a division)
 template <typename A>
@@ -568,10 +550,11 @@ PR_DEV Slot phong_slot(const A& a, int64_t gs, int64_t f) {
   return sl;
 }
 
-// Colour of slot gs: texel tensor (CM 1), interpolated on demand from per-vertex colours (CM 2;
+// Colour of slot gs: texel tensor (CM 1, and CM 4: the backward of PR_BLEND_PHONG reading the
+// forward's colours of the slots it needs), interpolated on demand from per-vertex colours (CM 2;
 // the same operation order as interp_fwd_kernel, so the result is bit-identical to sampling the
-// texels first), or Phong-shaded on demand (CM 3: pr_phong.h's slot_terms, the operations of
-// pr_shade_fwd, so bit-identical to shading the slots first).
+// texels first), or Phong-shaded on demand (CM 3, forward: pr_phong.h's slot_terms, the operations
+// of pr_shade_fwd, so bit-identical to shading the slots first).
 template <int CM, typename A>
 PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
   if constexpr (CM == 3) {
@@ -595,98 +578,6 @@ PR_DEV void slot_color(const A& a, int64_t gs, float c[3]) {
   }
 }
 
-// CM 3 backward scatters: one slot's mesh and texture gradients into the global accumulators
-// (PRBlendBwdArgs.shade's grad_*, zeroed by the caller); the interpolation weights are the slot's
-// barycentrics, as pr_shade_bwd's
-PR_DEV void atomic3(float* base, int64_t i, V3 g) {
-  atomicAdd(&base[i * 3], g.x); atomicAdd(&base[i * 3 + 1], g.y); atomicAdd(&base[i * 3 + 2], g.z);
-}
-PR_DEV void phong_scatter(const PRShadeArgs& a, const Slot& sl, const int64_t* fv, const PhongGrad& q) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int64_t vi = fv[i];
-    if (a.grad_verts) atomic3(a.grad_verts, vi, sl.b[i] * q.g_P);
-    if (a.grad_normals) atomic3(a.grad_normals, vi, sl.b[i] * q.g_Nn);
-    if (a.texture == PR_TEX_VERTEX && a.grad_vert_colors) atomic3(a.grad_vert_colors, vi, sl.b[i] * q.g_tex);
-  }
-  if (a.texture == PR_TEX_UV && a.grad_maps) {
-    float* gm = a.grad_maps + (int64_t)sl.n * a.Hm * a.Wm * 3;
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (q.ti[c] >= 0) atomic3(gm + q.ti[c], 0, q.w[c] * q.g_tex);
-  }
-}
-// the same scatters into the workgroup's LDS table (BwdK.pt_*): per-vertex parts by LDS atomics;
-// the map gradient (large, spread over many lines) stays global
-PR_DEV void phong_scatter_lds(const BwdK& a, float* PT, const Slot& sl, const int64_t* fv, const PhongGrad& q) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int vi = (int)fv[i] * 3;
-    const V3 gp = sl.b[i] * q.g_P, gn = sl.b[i] * q.g_Nn;
-    atomicAdd(&PT[vi], gp.x); atomicAdd(&PT[vi + 1], gp.y); atomicAdd(&PT[vi + 2], gp.z);
-    atomicAdd(&PT[a.pt_nrm + vi], gn.x); atomicAdd(&PT[a.pt_nrm + vi + 1], gn.y); atomicAdd(&PT[a.pt_nrm + vi + 2], gn.z);
-    if (a.pt_vc >= 0) {
-      const V3 gc = sl.b[i] * q.g_tex;
-      atomicAdd(&PT[a.pt_vc + vi], gc.x); atomicAdd(&PT[a.pt_vc + vi + 1], gc.y); atomicAdd(&PT[a.pt_vc + vi + 2], gc.z);
-    }
-  }
-  if (a.sh.texture == PR_TEX_UV && a.sh.grad_maps) {
-    float* gm = a.sh.grad_maps + (int64_t)sl.n * a.sh.Hm * a.sh.Wm * 3;
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (q.ti[c] >= 0) atomic3(gm + q.ti[c], 0, q.w[c] * q.g_tex);
-  }
-  const int l = a.pt_l + sl.n * 3, c = a.pt_c + sl.n * 3;
-  atomicAdd(&PT[l], q.g_dir.x); atomicAdd(&PT[l + 1], q.g_dir.y); atomicAdd(&PT[l + 2], q.g_dir.z);
-  atomicAdd(&PT[c], q.g_vraw.x); atomicAdd(&PT[c + 1], q.g_vraw.y); atomicAdd(&PT[c + 2], q.g_vraw.z);
-}
-
-// the table's sums -> the outputs (overwritten), the copies zeroed again (a second backward of the
-// same forward); entries i0, i0 + stride, ...  coherent: device-scope loads (the last workgroup)
-PR_DEV void phong_table_out(const BwdK& a, int i0, int stride, bool coherent) {
-  for (int i = i0; i < a.pt_T; i += stride) {
-    float v = 0.f;
-    for (int r = 0; r < a.pt_R; ++r) {
-      float* c = a.phong_table + (int64_t)r * a.pt_T + i;
-      v += coherent ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *c;
-      *c = 0.f;
-    }
-    float* dst;
-    int j;
-    if (i < a.pt_nrm) { dst = a.sh.grad_verts; j = i; }
-    else if (i < (a.pt_vc >= 0 ? a.pt_vc : a.pt_l)) { dst = a.sh.grad_normals; j = i - a.pt_nrm; }
-    else if (i < a.pt_l) { dst = a.sh.grad_vert_colors; j = i - a.pt_vc; }
-    else if (i < a.pt_c) { dst = a.sh.grad_light; j = i - a.pt_l; }
-    else { dst = a.sh.grad_camera; j = i - a.pt_c; }
-    if (dst) dst[j] = v;
-  }
-}
-__global__ void phong_table_reduce_kernel(BwdK a) {  // (without the fused last-workgroup reduction)
-  phong_table_out(a, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x, false);
-}
-
-// d light / d camera of one image (per-lane partial sums)
-PR_DEV void light_camera_atomics(const PRShadeArgs& a, int n, V3 l, V3 c) {
-  if (a.grad_light) atomic3(a.grad_light, n, l);
-  if (a.grad_camera) atomic3(a.grad_camera, n, c);
-}
-// the wave's partial d light / d camera: summed across the wave when its lanes hold one image (one
-// atomic per component per wave; every light and camera gradient of a frame goes to 6 addresses),
-// else lane by lane.  Every lane of the wave calls it (lanes without slots: n < 0, zero sums).
-PR_DEV void flush_light_camera(const PRShadeArgs& a, int n, V3 l, V3 c) {
-  const uint64_t has = __ballot(n >= 0);
-  if (!has) return;
-  const int nref = __shfl(n, __builtin_ctzll(has));
-  if (__ballot(n >= 0 && n != nref)) {
-    if (n >= 0) light_camera_atomics(a, n, l, c);
-    return;
-  }
-  float v[6] = {l.x, l.y, l.z, c.x, c.y, c.z};
-#pragma unroll
-  for (int j = 0; j < 6; ++j)
-    for (int o = 32; o >= 1; o >>= 1) v[j] += __shfl_xor(v[j], o);
-  if ((threadIdx.x & 63) == 0) light_camera_atomics(a, nref, V3{v[0], v[1], v[2]}, V3{v[3], v[4], v[5]});
-}
 
 // ================================================================== forward
 // CM: colour mode, 0 = weights out (no colour), 1 = texel colours, 2 = vertex colours
@@ -1001,6 +892,12 @@ PR_DEV void fwd_tile(const FwdK& a, const Geo& g, const int NC0, const Sc& sc, c
         const float w = (float)cw / fSa;
         float c[3];
         slot_color<CM>(a, (int64_t)gpx[pl] * K + k, c);
+        if constexpr (CM == 3) {  // the backward's colour of this winner (PR_BLEND_COLOR_SPARSE)
+          if (a.colors) {
+            float* o = const_cast<float*>(a.colors) + ((int64_t)gpx[pl] * K + k) * 3;  // (an output here)
+            o[0] = c[0]; o[1] = c[1]; o[2] = c[2];
+          }
+        }
         acc0 += w * c[0];
         acc1 += w * c[1];
         acc2 += w * c[2];
@@ -1010,6 +907,26 @@ PR_DEV void fwd_tile(const FwdK& a, const Geo& g, const int NC0, const Sc& sc, c
       acc0 += __shfl_xor(acc0, m);
       acc1 += __shfl_xor(acc1, m);
       acc2 += __shfl_xor(acc2, m);
+    }
+    if constexpr (CM == 3) {
+      // and the colour of the unperturbed argmax j0 (the backward's baseline slot): the first entry
+      // holding the largest logit (phase 2's zl; background last, so a slot wins a tie), found
+      // among the ascending candidates; shaded here unless it won a sample above
+      if (a.colors && pl < npix && l == 0) {
+        const int e0 = ea[pl] - eb, c = cl[pl], tot = PXI[pl * 4 + 3];
+        const float zl = PX[pl * 4 + 2];
+        int j0 = K;
+        for (int i = 0; i < tot; ++i) {
+          const int j = LC[e0 + i];
+          if (B[e0 + (j == K ? c : j)] == zl) { j0 = j; break; }
+        }
+        if (j0 < K && CNT[e0 + j0] == 0) {
+          float c3[3];
+          slot_color<CM>(a, (int64_t)gpx[pl] * K + j0, c3);
+          float* o = const_cast<float*>(a.colors) + ((int64_t)gpx[pl] * K + j0) * 3;
+          o[0] = c3[0]; o[1] = c3[1]; o[2] = c3[2];
+        }
+      }
     }
     if (pl < npix && l == 0) {
       const float wb = (float)CNT[ea[pl] - eb + cl[pl]] / fSa;
@@ -1040,8 +957,18 @@ PR_DEV void fwd_tile(const FwdK& a, const Geo& g, const int NC0, const Sc& sc, c
 template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
 __global__ void __launch_bounds__(kThreads, PR_BLEND_FWD_WPE) blend_fwd_kernel(FwdK a, Geo g, int NC) {
   if (a.sync && blockIdx.x == 0) sync_zero(a.sync);  // for the backward's fused reduction
-  if constexpr (CM == 3)  // the backward's small-mesh gradient table
-    for (int i = blockIdx.x * kThreads + threadIdx.x; i < a.pt_n; i += gridDim.x * kThreads) a.phong_table[i] = 0.f;
+  if constexpr (CM == 3) {  // the shading backward's small accumulators (a PR_GRAD_PREZEROED pr_shade_bwd)
+    const PRShadeArgs& sh = a.sh;
+    const int64_t t0 = (int64_t)blockIdx.x * kThreads + threadIdx.x, st = (int64_t)gridDim.x * kThreads;
+    float* vb[3] = {sh.grad_verts, sh.grad_normals, sh.texture == PR_TEX_VERTEX ? sh.grad_vert_colors : nullptr};
+    for (int j = 0; j < 3; ++j)
+      if (vb[j])
+        for (int64_t i = t0; i < sh.V * 3; i += st) vb[j][i] = 0.f;
+    float* nb[2] = {sh.grad_light, sh.grad_camera};
+    for (int j = 0; j < 2; ++j)
+      if (nb[j])
+        for (int64_t i = t0; i < (int64_t)a.p.N * 3; i += st) nb[j][i] = 0.f;
+  }
   if constexpr (!SEG) {
     fwd_tile<NOISE, RAST, CM, MULTI, false>(a, g, NC, resolve(a.p), pixel_block(g), -1, blockIdx.x);
   } else {
@@ -1114,16 +1041,16 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
       const int64_t s0 = bpix0 * K, n = (int64_t)bnpix * K;
       block_fill(a.grad_zbuf + s0, n, 0.f);
       block_fill(a.grad_dists + s0, n, 0.f);
-      if constexpr (CM == 1) block_fill(a.grad_colors + 3 * s0, 3 * n, 0.f);
-      if constexpr (CM >= 2) block_fill(a.grad_bary + 3 * s0, 3 * n, 0.f);
+      if constexpr (CM == 1 || CM == 4) block_fill(a.grad_colors + 3 * s0, 3 * n, 0.f);
+      if constexpr (CM == 2) block_fill(a.grad_bary + 3 * s0, 3 * n, 0.f);
     } else {  // interleaved: one K-slot row per pixel
       for (int i = tid; i < bnpix * K; i += kThreads) {
         const int pl = i / K;
         const int64_t s = (int64_t)GPX[pl] * K + (i - pl * K);
         a.grad_zbuf[s] = 0.f;
         a.grad_dists[s] = 0.f;
-        if constexpr (CM == 1) a.grad_colors[3 * s] = a.grad_colors[3 * s + 1] = a.grad_colors[3 * s + 2] = 0.f;
-        if constexpr (CM >= 2) a.grad_bary[3 * s] = a.grad_bary[3 * s + 1] = a.grad_bary[3 * s + 2] = 0.f;
+        if constexpr (CM == 1 || CM == 4) a.grad_colors[3 * s] = a.grad_colors[3 * s + 1] = a.grad_colors[3 * s + 2] = 0.f;
+        if constexpr (CM == 2) a.grad_bary[3 * s] = a.grad_bary[3 * s + 1] = a.grad_bary[3 * s + 2] = 0.f;
       }
     }
     if (tid < 4) put_partial(a, partials + pidx * 4 + tid, 0.f);
@@ -1131,15 +1058,6 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
     return;
   }
 
-  // CM 3: the workgroup's LDS table (small meshes), zeroed before the passes' barriers
-  float* PT = smem + a.pt_off;
-  int* WL = reinterpret_cast<int*>(PT + a.pt_T);  // [CAP] B2c's work list, [CAP] its length
-  if constexpr (CM == 3)
-    for (int i = tid; i < a.pt_T; i += kThreads) PT[i] = 0.f;
-  // CM 3 without the table: this thread's d light / d camera (image lc_n), flushed per wave after
-  // the passes
-  int lc_n = -1;
-  V3 lc_l{0.f, 0.f, 0.f}, lc_c{0.f, 0.f, 0.f};
   const int npass = SEG ? 1 : (MULTI ? uni(PS[PB + 1]) : 1);
   for (int it = 0; it < npass; ++it) {
   const int pass = SEG ? part : it;
@@ -1157,8 +1075,6 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
   const int n0 = (int)(pix0 / g.HW), rem0 = (int)(pix0 - (int64_t)n0 * g.HW);
   const float zf0 = p.zfar[n0], zn0 = p.znear[n0];
   fill_owner(OWN, ea, eb, cl, npix, lsh, lpp, CN);
-  if constexpr (CM == 3)
-    if (tid == 0) WL[CAP] = 0;  // B2c's work list (the previous pass's readers are past barriers)
   __syncthreads();
   PR_BSTAMP(0);
 
@@ -1198,7 +1114,7 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
             const float4 gi = reinterpret_cast<const float4*>(a.grad_image)[gp];
             const float* c = a.colors + gs * 3;
             dw[u] = (gi.x * c[0] + gi.y * c[1]) + gi.z * c[2];
-          } else if constexpr (CM == 0) {  // (CM 2: dW of the slots that won a sample, B5b)
+          } else if constexpr (CM == 0) {  // (CM 2 / 4: dW of the slots B5 reads, B2)
             dw[u] = a.grad_weights[gp * KP1 + k];
           }
         } else {
@@ -1393,18 +1309,14 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
       PR_BSTAMP(7);
 #endif
       // dW = g_rgb . colour of the slot entries B5 reads (a win, or j0): the colour is
-      // interpolated from the vertex colours here (CM 2), once per such entry; CM 3 lists them for
-      // B2c
+      // interpolated from the vertex colours here (CM 2), or read from the forward's colours of
+      // exactly those slots (CM 4: PR_BLEND_PHONG's sparse colours), once per such entry
       if (act) {
         const float* gi = PX + pl * 12 + 8;
         for (int e = l; e < c; e += lpp) {
           const int cnt = CN[e0 + e];
           if (cnt == 0 && e != jb) continue;
           float cc[3];
-          if constexpr (CM == 3) {  // listed for B2c
-            WL[atomicAdd(&WL[CAP], 1)] = e0 + e;
-            continue;
-          }
           slot_color<CM>(a, (int64_t)gpx[pl] * K + e, cc);
           DW[e0 + e] = (gi[0] * cc[0] + gi[1] * cc[1]) + gi[2] * cc[2];
         }
@@ -1414,52 +1326,6 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
   __syncthreads();
   PR_BSTAMP(2);
 
-  // ---- B2c (CM 3): the listed entries (a win, or j0) over the whole workgroup: each entry's
-  //      Phong colour -> dW, and for a winner its shading backward on the same state (d colour =
-  //      wins / Sa * g_rgb, known from B1): d bary, the mesh / texture / light / camera gradients
-  //      (B8 writes the other entries' zero d bary).  One entry per thread: the per-pixel lanes of
-  //      B2 left most threads idle behind each winner's dependent load chain.
-  if constexpr (CM == 3) {
-    const int nw = WL[CAP];
-    for (int wi = tid; wi < nw; wi += kThreads) {
-      const int li = WL[wi];
-      const int pl = OWN[li], e = li - (ea[pl] - eb);
-      const int64_t gs = (int64_t)gpx[pl] * K + e;
-      const float* gi = PX + pl * 12 + 8;
-      const int cnt = CN[li];
-      const int64_t f = a.pix_to_face[gs];
-      if (f < 0) {  // (not a winner: masked slots never win)
-        DW[li] = (gi[0] * 0.f + gi[1] * 0.f) + gi[2] * 0.f;
-        continue;
-      }
-      const Slot sl = phong_slot(a, gs, f);
-      const int64_t* fv = a.sh.faces + f * 3;
-      const Shade z = shade(a.sh, sl, gs, fv);
-      const Terms t = terms_of(a.sh, sl.n, z);
-      const V3 col = colour(t.lit, t.tex, t.spec);
-      DW[li] = (gi[0] * col.x + gi[1] * col.y) + gi[2] * col.z;
-      if (cnt == 0) continue;
-      const float w = (float)cnt / (float)Sa;
-      const PhongGrad q = phong_bwd_z(a.sh, sl, z, fv, V3{w * gi[0], w * gi[1], w * gi[2]});
-      a.grad_bary[gs * 3] = q.gb[0];
-      a.grad_bary[gs * 3 + 1] = q.gb[1];
-      a.grad_bary[gs * 3 + 2] = q.gb[2];
-      if (a.pt_T > 0) {
-        phong_scatter_lds(a, PT, sl, fv, q);
-      } else {
-        phong_scatter(a.sh, sl, fv, q);
-        if (sl.n != lc_n) {
-          if (lc_n >= 0) light_camera_atomics(a.sh, lc_n, lc_l, lc_c);
-          lc_n = sl.n;
-          lc_l = V3{0.f, 0.f, 0.f};
-          lc_c = V3{0.f, 0.f, 0.f};
-        }
-        lc_l = lc_l + q.g_dir;
-        lc_c = lc_c + q.g_vraw;
-      }
-    }
-    __syncthreads();
-  }
 
   // ---- B5: per (pixel, sample): a_s = dW[j*_s] - dW[j0] (win counts: B1, CM 2's dW: B2)
   PR_FOR_SLOTS(Sa, g.qS, g.rS, npix * Sa) {
@@ -1628,7 +1494,7 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
     } else {
       a.grad_prob[gs] = dprob;
     }
-    if constexpr (CM == 1) {
+    if constexpr (CM == 1 || CM == 4) {
       const float w = (float)CN[li] / (float)Sa;
       float* dc = a.grad_colors + gs * 3;
       dc[0] = w * gi.x;
@@ -1656,9 +1522,6 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
       a.grad_bary[gs * 3] = gb[0];
       a.grad_bary[gs * 3 + 1] = gb[1];
       a.grad_bary[gs * 3 + 2] = gb[2];
-    } else if constexpr (CM == 3) {
-      // a winner's d bary (and the rest of its shading backward) came from B2; zeros elsewhere
-      if (CN[li] == 0 || !m) a.grad_bary[gs * 3] = a.grad_bary[gs * 3 + 1] = a.grad_bary[gs * 3 + 2] = 0.f;
     }
   }
 
@@ -1677,10 +1540,10 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
         a.grad_zbuf[gs] = 0.f;
         if constexpr (RAST) a.grad_dists[gs] = 0.f;
         else a.grad_prob[gs] = dprob;
-        if constexpr (CM == 1) {
+        if constexpr (CM == 1 || CM == 4) {
           float* dc = a.grad_colors + gs * 3;
           dc[0] = dc[1] = dc[2] = 0.f;
-        } else if constexpr (CM >= 2) {
+        } else if constexpr (CM == 2) {
           a.grad_bary[gs * 3] = a.grad_bary[gs * 3 + 1] = a.grad_bary[gs * 3 + 2] = 0.f;
         }
       }
@@ -1689,22 +1552,6 @@ PR_DEV void bwd_tile(const BwdK& a, const Geo& g, const Sc& sc, float* partials,
   __syncthreads();  // the next pass reuses every LDS record
   PR_BSTAMP(6);
   }  // passes
-
-  if constexpr (CM == 3) {
-    if (a.pt_T > 0) {
-      __syncthreads();
-      float* cp = a.phong_table + (int64_t)(blockIdx.x % a.pt_R) * a.pt_T;
-      for (int i = tid; i < a.pt_T; i += kThreads) {
-        const float v = PT[i];
-        if (v != 0.f) {  // (waits for the return: performed before this workgroup's arrival)
-          const float old = __hip_atomic_fetch_add(&cp[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("" ::"v"(old));
-        }
-      }
-    } else {
-      flush_light_camera(a.sh, lc_n, lc_l, lc_c);
-    }
-  }
 
   // ---- block reduction of the scalar partials (fixed order -> deterministic)
 #pragma unroll
@@ -1782,7 +1629,7 @@ PR_DEV void finalize_scalars(const float* partials, int nblk, const PRBlendParam
 }
 
 template <int NOISE, bool RAST, int CM, bool MULTI, bool SEG>
-__global__ void __launch_bounds__(kThreads, CM == 3 ? PR_PHONG_BWD_WPE : (MULTI ? 6 : PR_BLEND_BWD_WPE)) blend_bwd_kernel(BwdK a, Geo g, float* partials) {
+__global__ void __launch_bounds__(kThreads, MULTI ? 6 : PR_BLEND_BWD_WPE) blend_bwd_kernel(BwdK a, Geo g, float* partials) {
   int nblk = (int)gridDim.x;
   if constexpr (!SEG) {
     const int64_t blk = pixel_block(g);
@@ -1802,8 +1649,6 @@ __global__ void __launch_bounds__(kThreads, CM == 3 ? PR_PHONG_BWD_WPE : (MULTI 
     __shared__ int flag;
     if (last_arrival(a.sync, (int)gridDim.x, &flag, g.sync_rel != 0)) {
       finalize_scalars(partials, nblk, a.p, RAST ? 1 : 0, a.grad_scalars, red, true);
-      if constexpr (CM == 3)
-        if (a.pt_T > 0) phong_table_out(a, threadIdx.x, kThreads, true);
       sync_zero(a.sync);
     }
   }
@@ -2059,7 +1904,10 @@ int check_params(const PRBlendParams& p, bool need_rast) {
 }
 
 int color_mode(int flags) {
-  return !(flags & PR_BLEND_COLOR) ? 0 : ((flags & PR_BLEND_VERTEX) ? 2 : ((flags & PR_BLEND_PHONG) ? 3 : 1));
+  if (!(flags & PR_BLEND_COLOR)) return 0;
+  if (flags & PR_BLEND_VERTEX) return 2;
+  if (flags & PR_BLEND_PHONG) return 3;
+  return (flags & PR_BLEND_COLOR_SPARSE) ? 4 : 1;
 }
 
 template <typename Fn, typename... Args>
@@ -2088,8 +1936,8 @@ void launch_bwd(const BwdK& a, Geo geo, hipStream_t st, size_t lds, int nblk, fl
   const bool rast = a.p.flags & PR_BLEND_RAST;
   const int cm = color_mode(a.p.flags);
   ktimer_mark(0, "blend_bwd_kernel", st);
-  if (cm == 3) {
-    if constexpr (!SEG) launch_grid(blend_bwd_kernel<NOISE, true, 3, MULTI, false>, nblk, lds, st, a, geo, part);
+  if (cm == 4) {  // (RAST only, static grid: pr_blend_bwd checks)
+    if constexpr (!SEG) launch_grid(blend_bwd_kernel<NOISE, true, 4, MULTI, false>, nblk, lds, st, a, geo, part);
   } else if (rast && cm == 2) launch_grid(blend_bwd_kernel<NOISE, true, 2, MULTI, SEG>, nblk, lds, st, a, geo, part);
   else if (rast && cm == 1) launch_grid(blend_bwd_kernel<NOISE, true, 1, MULTI, SEG>, nblk, lds, st, a, geo, part);
   else if (rast) launch_grid(blend_bwd_kernel<NOISE, true, 0, MULTI, SEG>, nblk, lds, st, a, geo, part);
@@ -2175,7 +2023,7 @@ PlanCfg plan_cfg(const PRBlendParams& p, const int32_t* pcnt) {
   // workgroups (forward kernel 46 -> 53 us): a net loss of ~20 us per step.
   const char* env = getenv("PR_BLEND_SEG");
   const int64_t P = (int64_t)p.N * p.H * p.W;
-  if (!pcnt || P > kPlanMaxPixels || !(env && atoi(env) != 0) || (p.flags & PR_BLEND_PHONG)) return c;
+  if (!pcnt || P > kPlanMaxPixels || !(env && atoi(env) != 0) || (p.flags & (PR_BLEND_PHONG | PR_BLEND_COLOR_SPARSE))) return c;
   const int KP1 = p.K + 1;
   // (read per call: tests drive several segment sizes in one process)
   const int e_env[2] = {getenv("PR_BLEND_SEG_FWD") ? atoi(getenv("PR_BLEND_SEG_FWD")) : 0,
@@ -2238,13 +2086,6 @@ int phong_check(const PRBlendParams& p, const PRShadeArgs* sh) {
   return PR_OK;
 }
 
-// CM 3's LDS table size (floats) for the call's mesh: verts | normals (| vertex colours) per vertex,
-// light | camera per image; 0 when it exceeds kPhongTabMax (global atomics instead)
-int phong_table_floats(const PRBlendParams& p, const PRShadeArgs* sh) {
-  if (!(p.flags & PR_BLEND_PHONG) || !sh) return 0;
-  const int64_t T = sh->V * (sh->texture == PR_TEX_VERTEX ? 9 : 6) + (int64_t)p.N * 6;
-  return T <= kPhongTabMax ? (int)T : 0;
-}
 
 int64_t bwd_blocks(const PRBlendParams& p) {
   const int PB = pick_shape(p.K + 1, p.Sa, (int64_t)p.N * p.H * p.W, true).PB;
@@ -2312,10 +2153,7 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
     if (int e = phong_check(a.p, a.shade)) return e;
   FwdK k{};
   static_cast<PRBlendFwdArgs&>(k) = a;
-  if (cm == 3) {
-    k.sh = *a.shade;
-    k.pt_n = a.phong_table ? kPhongCopies * phong_table_floats(a.p, a.shade) : 0;
-  }
+  if (cm == 3) k.sh = *a.shade;
   const int KP1 = a.p.K + 1;
   const Shape sh = pick_shape(KP1, a.p.Sa, (int64_t)a.p.N * a.p.H * a.p.W, false);
   const int PB = sh.PB;
@@ -2350,10 +2188,6 @@ extern "C" int pr_blend_fwd(const PRBlendFwdArgs* args, void* stream) {
   return check_launch("blend_fwd");
 }
 
-extern "C" size_t pr_blend_phong_table_bytes(const PRBlendParams* p, const PRShadeArgs* shade) {
-  if (!p || !shade) return 0;
-  return (size_t)kPhongCopies * phong_table_floats(*p, shade) * sizeof(float);
-}
 
 extern "C" size_t pr_blend_plan_size(const PRBlendParams* p) {
   if (!p || (p->flags & PR_BLEND_SOFT)) return 0;
@@ -2384,17 +2218,18 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
       (color_mode(a.p.flags) == 1 && (!a.colors || !a.grad_image || !a.grad_colors)) ||
       (color_mode(a.p.flags) == 2 && (!a.grad_image || !a.bary || !a.faces || !a.vert_colors ||
                                       !a.grad_bary || !a.pix_to_face)) ||
-      (color_mode(a.p.flags) == 3 && (!a.grad_image || !a.bary || !a.grad_bary || !a.pix_to_face)) ||
+      (color_mode(a.p.flags) == 4 && (!a.colors || !a.grad_image || !a.grad_colors)) ||
       (!color && !a.grad_weights))
     return set_error(PR_ERR_ARG, "blend_bwd: missing buffer");
-  if (color_mode(a.p.flags) == 3)
-    if (int e = phong_check(a.p, a.shade)) return e;
+  if (a.p.flags & PR_BLEND_PHONG)
+    return set_error(PR_ERR_ARG, "blend_bwd: PR_BLEND_PHONG is forward only (its backward: PR_BLEND_COLOR_SPARSE, then pr_shade_bwd)");
+  if (color_mode(a.p.flags) == 4 && (!rast || (a.p.flags & PR_BLEND_VERTEX)))
+    return set_error(PR_ERR_ARG, "blend_bwd: PR_BLEND_COLOR_SPARSE needs RAST and no VERTEX");
   const size_t need = pr_blend_bwd_workspace_size(args);
   if (!a.workspace || a.workspace_bytes < need) return set_error(PR_ERR_WORKSPACE, "blend_bwd: workspace too small");
   BwdK k{};
   static_cast<PRBlendBwdArgs&>(k) = a;
-  if (color_mode(a.p.flags) == 3) k.sh = *a.shade;
-  const int ptT = phong_table_floats(a.p, a.shade);
+
   const int KP1 = a.p.K + 1;
   const Shape sh = pick_shape(KP1, a.p.Sa, (int64_t)a.p.N * a.p.H * a.p.W, true);
   const int PB = sh.PB;
@@ -2402,17 +2237,6 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
   geo.cap = sh.cap;
   int64_t nblk = (geo.P + PB - 1) / PB;
   size_t lds = bwd_lds(PB, sh.cap, a.p.Sa);
-  if (color_mode(a.p.flags) == 3) {  // CM 3: LDS table (small meshes), then B2c's work list
-    k.pt_off = (int)((lds + 15) / 16 * 4);
-    k.pt_T = a.phong_table ? ptT : 0;
-    k.pt_R = kPhongCopies;
-    lds = (size_t)k.pt_off * sizeof(float) + (size_t)k.pt_T * sizeof(float) + (size_t)(sh.cap + 1) * sizeof(int);
-    const int64_t V = a.shade->V;
-    k.pt_nrm = (int)(V * 3);
-    k.pt_vc = a.shade->texture == PR_TEX_VERTEX ? (int)(V * 6) : -1;
-    k.pt_l = (int)(V * (a.shade->texture == PR_TEX_VERTEX ? 9 : 6));
-    k.pt_c = k.pt_l + a.p.N * 3;
-  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* part = reinterpret_cast<float*>(a.workspace);
   const bool multi = sh.cap < PB * KP1;
@@ -2432,10 +2256,6 @@ extern "C" int pr_blend_bwd(const PRBlendBwdArgs* args, void* stream) {
     else launch_bwd<PR_NOISE_PHILOX, false, false>(k, geo, st, lds, (int)nblk, part);
   }
   if (int e = check_launch("blend_bwd")) return e;
-  if (k.pt_T > 0 && !a.sync) {  // (else the kernel's last workgroup wrote the table's sums)
-    phong_table_reduce_kernel<<<(k.pt_T + kThreads - 1) / kThreads, kThreads, 0, st>>>(k);
-    if (int e = check_launch("blend_bwd_phong_reduce")) return e;
-  }
   if (a.sync) return PR_OK;  // the scalars were reduced by the kernel's last workgroup
   blend_finalize_kernel<<<1, kThreads, 0, st>>>(part, (int)nblk, a.p, rast ? 1 : 0, a.grad_scalars,
                                                 pc.on ? a.plan : nullptr);

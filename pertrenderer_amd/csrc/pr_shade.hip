@@ -533,6 +533,44 @@ __global__ void __launch_bounds__(kThreads) shade_fwd_pix_kernel(PRShadeArgs a, 
   }
 }
 
+// Pixel-block backward (counts attached, no per-slot texels, fast path): the block's valid slots are
+// enumerated from the counts' prefix (the padded ones only get their zero d bary, and none with
+// PR_SHADE_LIVE_ONLY), and the chain rule runs for the valid slots with a non-zero d colour: on a
+// perturbed-blend frame those are the slots that won a sample (pr_blend_bwd's d colour is wins / Sa
+// times g_rgb), a fraction of the valid ones; the chunked kernel walked every slot of the frame.
+__global__ void __launch_bounds__(kThreads) shade_bwd_pix_kernel(PRShadeArgs a, int64_t P, int64_t HW, Tab tab,
+                                                                 uint32_t kmag) {
+  extern __shared__ float lds[];
+  __shared__ PixBlock pb;
+  for (int i = threadIdx.x; i < tab.size; i += kThreads) lds[i] = 0.f;
+  const bool live_only = a.flags & PR_SHADE_LIVE_ONLY;
+  PR_PIX_BLOCKS(P, p0, npix) {
+    pix_block_load(a, p0, (int)npix, HW, pb);
+    __syncthreads();  // (the first also publishes the zeroed table)
+    if (!live_only && a.grad_bary) {
+      for (int x = threadIdx.x; x < (int)npix * a.K; x += kThreads) {
+        const int pl = div_k(x, a.K, kmag), k = x - pl * a.K;
+        if (k < pb.cnt[pl]) continue;
+        float* o = a.grad_bary + ((p0 + pl) * a.K + k) * 3;
+        o[0] = 0.f; o[1] = 0.f; o[2] = 0.f;
+      }
+    }
+    const int total = pb.incl[kBlkPix - 1];
+    for (int i = threadIdx.x; i < total; i += kThreads) {
+      Slot sl;
+      const int64_t s = live_slot(a, pb, p0, i, sl);
+      const float* gc = a.grad_colors + s * 3;
+      if (sl.f < 0 || (gc[0] == 0.f && gc[1] == 0.f && gc[2] == 0.f)) {
+        zero_bwd<false>(a, s, s, ShadeDet{});
+        continue;
+      }
+      slot_bwd<false>(a, sl, s, s, tab, ShadeDet{}, lds);
+    }
+    __syncthreads();  // pb is rewritten by the next block
+  }
+  flush_table(a, tab, lds);
+}
+
 int shade_check(const PRShadeArgs& a) {
   if (a.N <= 0 || a.H <= 0 || a.W <= 0 || a.K <= 0) return set_error(PR_ERR_ARG, "shade: bad shape");
   if (!a.pix_to_face || !a.bary || !a.faces || !a.verts || !a.normals)
@@ -724,6 +762,13 @@ extern "C" int pr_shade_bwd(const PRShadeArgs* args, void* stream) {
   // fewer, fatter workgroups when the LDS table is large (its zero + flush is per workgroup)
   const size_t sh = (size_t)tab.size * sizeof(float);
   const int64_t HW = (int64_t)a.H * a.W;
+  if (pix_path(a, nullptr)) {
+    const int64_t P = (int64_t)a.N * HW;
+    static const int cap_env = getenv("PR_SHADE_BWD_BLOCKS") ? atoi(getenv("PR_SHADE_BWD_BLOCKS")) : 0;
+    const int nbp = std::min(pix_blocks(P), cap_env > 0 ? cap_env : (tab.size > 1024 ? 1024 : 4096));
+    shade_bwd_pix_kernel<<<nbp, kThreads, sh, st>>>(a, P, HW, tab, k_magic(a.K));
+    return check_launch("shade_bwd");
+  }
   const int R = shade_rounds();
   const int nb = std::min(shade_blocks(PK, R), tab.size > 1024 ? 1024 : 16384);
   if (R == 4) shade_bwd_kernel<false, 4><<<nb, kThreads, sh, st>>>(a, 0, PK, HW, tab, ShadeDet{}, idx32(a));

@@ -53,7 +53,6 @@ struct Api {
   decltype(&pr_blend_plan_size) blend_plan_size = nullptr;
   decltype(&pr_blend_bwd_workspace_size) blend_bwd_workspace_size = nullptr;
   decltype(&pr_blend_bwd) blend_bwd = nullptr;
-  decltype(&pr_blend_phong_table_bytes) blend_phong_table_bytes = nullptr;
   decltype(&pr_shade_fwd) shade_fwd = nullptr;
   decltype(&pr_shade_bwd_workspace_size) shade_bwd_workspace_size = nullptr;
   decltype(&pr_shade_bwd) shade_bwd = nullptr;
@@ -87,7 +86,6 @@ void bind(const std::unordered_map<std::string, int64_t>& addrs) {
   bind_one(addrs, "pr_blend_plan_size", a.blend_plan_size);
   bind_one(addrs, "pr_blend_bwd_workspace_size", a.blend_bwd_workspace_size);
   bind_one(addrs, "pr_blend_bwd", a.blend_bwd);
-  bind_one(addrs, "pr_blend_phong_table_bytes", a.blend_phong_table_bytes);
   bind_one(addrs, "pr_shade_fwd", a.shade_fwd);
   bind_one(addrs, "pr_shade_bwd_workspace_size", a.shade_bwd_workspace_size);
   bind_one(addrs, "pr_shade_bwd", a.shade_bwd);
@@ -912,10 +910,12 @@ Tensor shade(const Tensor& bary, const Tensor& verts, const Tensor& normals, con
 
 // ------------------------------------------------------------------ fused Phong blend
 // blend.py _FusedPhongBlendFn: RandomPhongShader's sample_textures -> phong_shading ->
-// smooth_rgb_blend (random_rasterizer.py:99-116) as one pr_blend_fwd / pr_blend_bwd pair
-// (PR_BLEND_PHONG): each slot's colour is shaded where it wins a sample, no (N,H,W,K,3) colour
-// tensor and no pr_shade_* launch.  Gradients: dists, zbuf, bary (-> rasterizer), verts, normals
-// (-> vertex normals), the UV maps or vertex colours, light, camera and the smoothing scalars.
+// smooth_rgb_blend (random_rasterizer.py:99-116).  Forward: one pr_blend_fwd (PR_BLEND_PHONG) that
+// shades a slot only where it wins a sample and keeps the colours of the slots the backward reads
+// (winners, unperturbed argmax) in a sparse colour buffer.  Backward: pr_blend_bwd reading those
+// (PR_BLEND_COLOR_SPARSE) -> d colours -> pr_shade_bwd, whose chain rule runs for the slots with a
+// non-zero d colour only.  Gradients: dists, zbuf, bary (-> rasterizer), verts, normals (-> vertex
+// normals), the UV maps or vertex colours, light, camera and the smoothing scalars.
 constexpr int kPhongIn = 28;  // forward arguments
 
 struct BlendPhongFn : public torch::autograd::Function<BlendPhongFn> {
@@ -947,15 +947,28 @@ struct BlendPhongFn : public torch::autograd::Function<BlendPhongFn> {
                    dense(tex, at::kFloat),   dense(light, at::kFloat), dense(camera, at::kFloat)};
     auto image = empty({N, H, W, 4}, at::kFloat, p2f_c);
     auto winners = empty({N * H * W, p.Sa}, at::kByte, p2f_c);
-    Tensor cache = cache_on && need != 0 ? empty({N, H, W, K, 2}, at::kFloat, p2f_c) : Tensor();
+    const bool any_grad = need != 0;
+    Tensor cache = cache_on && any_grad ? empty({N, H, W, K, 2}, at::kFloat, p2f_c) : Tensor();
+    // the colours the backward reads (written at those slots only: no other slot is touched)
+    Tensor colors = any_grad ? empty({N, H, W, K, 3}, at::kFloat, p2f_c) : Tensor();
     PRShadeArgs sh{};
     shade_common(sh, p2f_c, counts, f_c, face_uvs, t, rows.data(), mode, directional);
+    // the shading backward's small accumulators, zeroed by the forward's kernel
+    Tensor acc[6];
+    for (int i = 1; i < 6; ++i)
+      if (((need >> (2 + i)) & 1) && prezeroable(i, mode)) acc[i] = at::empty_like(t[i]);
+    sh.grad_verts = ptr<float>(acc[1]);
+    sh.grad_normals = ptr<float>(acc[2]);
+    sh.grad_vert_colors = ptr<float>(acc[3]);
+    sh.grad_light = ptr<float>(acc[4]);
+    sh.grad_camera = ptr<float>(acc[5]);
     PRBlendFwdArgs a{};
     a.p = p;
     a.pix_to_face = ptr<int64_t>(p2f_c);
     a.dists = ptr<float>(d_c);
     a.zbuf = ptr<float>(z_c);
     a.bary = ptr<float>(t[0]);
+    a.colors = ptr<float>(colors);
     a.image = ptr<float>(image);
     a.winners = ptr<uint8_t>(winners);
     a.rast_cache = ptr<float>(cache);
@@ -963,22 +976,21 @@ struct BlendPhongFn : public torch::autograd::Function<BlendPhongFn> {
     a.shade = &sh;
     at::DeviceGuard dg(p2f_c.device());
     Tensor sync = sync_on ? at::empty({PR_BLEND_SYNC_BYTES / 4}, p2f_c.options().dtype(at::kInt)) : Tensor();
-    // a small mesh's per-vertex / per-image gradient table (zeroed by the forward's kernel)
-    const size_t tb = need != 0 ? api().blend_phong_table_bytes(&p, &sh) : 0;
-    Tensor table = tb ? at::empty({static_cast<int64_t>(tb / 4)}, p2f_c.options().dtype(at::kFloat)) : Tensor();
-    a.phong_table = ptr<float>(table);
     a.sync = ptr<int32_t>(sync);
     check(api().blend_fwd(&a, stream_of(image)), "pr_blend_fwd (phong)");
     ctx->saved_data["p"] = std::string(reinterpret_cast<const char*>(&p), sizeof(p));
     ctx->saved_data["mode"] = mode;
     ctx->saved_data["directional"] = directional;
+    ctx->saved_data["prezeroed"] = true;
     Keep k(ctx);
     for (int i = 0; i < 6; ++i) k(kShadeKeys[i], t[i]);
     for (int i = 0; i < 6; ++i) k(kShadeRows[i], rows[i]);
+    const char* kAcc[6] = {"", "acc1", "acc2", "acc3", "acc4", "acc5"};
+    for (int i = 1; i < 6; ++i) k(kAcc[i], acc[i]);
     const char* names[] = {"p2f", "d", "z", "f", "counts", "face_uvs", "zn", "zf", "nr", "na", "seeds",
-                           "winners", "cache", "sync", "table", "s0", "s1", "s2"};
+                           "winners", "cache", "sync", "colors", "s0", "s1", "s2"};
     const Tensor ts[] = {p2f_c, d_c, z_c, f_c, counts, face_uvs, znear, zfar, noise_r, noise_a, seeds,
-                         winners, cache, sync, table, sigma, gamma, alpha};
+                         winners, cache, sync, colors, sigma, gamma, alpha};
     for (size_t i = 0; i < sizeof(ts) / sizeof(ts[0]); ++i) k(names[i], ts[i]);
     k.commit();
     return image;
@@ -1000,35 +1012,19 @@ struct BlendPhongFn : public torch::autograd::Function<BlendPhongFn> {
     Tensor t[6], rows[6];
     for (int i = 0; i < 6; ++i) t[i] = sv(kShadeKeys[i]);
     for (int i = 0; i < 6; ++i) rows[i] = sv(kShadeRows[i]);
-    auto p2f = sv("p2f"), d = sv("d"), z = sv("z");
+    auto p2f = sv("p2f"), d = sv("d"), z = sv("z"), colors = sv("colors");
     auto g = dense(grads[0], at::kFloat);
-    auto gd = at::empty_like(d), gz = at::empty_like(z), gb = at::empty_like(t[0]);
-    // the mesh / texture / light / camera gradients: accumulated by the kernel, except those the
-    // small-mesh table writes (verts, normals, vertex colours, light, camera)
-    const Tensor table = sv("table");
-    Tensor acc[6];
-    for (int i = 1; i < 6; ++i) {
-      if (!needs(2 + i)) continue;
-      const bool written = table.defined() && (i != 3 || mode == PR_TEX_VERTEX);
-      acc[i] = written ? at::empty_like(t[i]) : at::zeros_like(t[i]);
-    }
+    // 1. the blend backward on the sparse colours: d dists, d zbuf, d colours, the scalars
+    p.flags = (p.flags & ~PR_BLEND_PHONG) | PR_BLEND_COLOR_SPARSE;
+    auto gd = at::empty_like(d), gz = at::empty_like(z), gc = at::empty_like(colors);
     auto gsc = at::empty({3}, d.options());
-    PRShadeArgs sh{};
-    shade_common(sh, p2f, sv("counts"), sv("f"), sv("face_uvs"), t, rows, mode,
-                 ctx->saved_data["directional"].toBool());
-    sh.grad_verts = ptr<float>(acc[1]);
-    sh.grad_normals = ptr<float>(acc[2]);
-    if (mode == PR_TEX_VERTEX) sh.grad_vert_colors = ptr<float>(acc[3]);
-    else sh.grad_maps = ptr<float>(acc[3]);
-    sh.grad_light = ptr<float>(acc[4]);
-    sh.grad_camera = ptr<float>(acc[5]);
     PRBlendBwdArgs a{};
     a.p = p;
     a.pix_to_face = ptr<int64_t>(p2f);
     a.dists = ptr<float>(d);
     a.zbuf = ptr<float>(z);
-    a.bary = ptr<float>(t[0]);
-    a.grad_bary = ptr<float>(gb);
+    a.colors = ptr<float>(colors);
+    a.grad_colors = ptr<float>(gc);
     a.winners = ptr<uint8_t>(sv("winners"));
     a.grad_image = ptr<float>(g);
     a.rast_cache = ptr<float>(sv("cache"));
@@ -1037,18 +1033,48 @@ struct BlendPhongFn : public torch::autograd::Function<BlendPhongFn> {
     a.grad_scalars = ptr<float>(gsc);
     a.pix_count = ptr<int32_t>(sv("counts"));
     a.sync = ptr<int32_t>(sv("sync"));
-    a.shade = &sh;
-    a.phong_table = ptr<float>(table);
     at::DeviceGuard dg(d.device());
     auto ws = workspace(api().blend_bwd_workspace_size(&a), d);
     a.workspace = ws.data_ptr();
     a.workspace_bytes = static_cast<size_t>(ws.numel());
     void* st = stream_of(g);
     check(api().blend_bwd(&a, st), "pr_blend_bwd (phong)");
+    // 2. the shading backward: d bary and the mesh / texture / light / camera gradients
+    PRShadeArgs sh{};
+    shade_common(sh, p2f, sv("counts"), sv("f"), sv("face_uvs"), t, rows, mode,
+                 ctx->saved_data["directional"].toBool());
+    sh.grad_colors = ptr<float>(gc);
+    const char* kAcc[6] = {"", "acc1", "acc2", "acc3", "acc4", "acc5"};
+    bool pre = ctx->saved_data["prezeroed"].toBool();
+    ctx->saved_data["prezeroed"] = false;
+    Tensor sg[6];
+    for (int i = 0; i < 6; ++i) {
+      if (!needs(2 + i)) continue;
+      const Tensor zt = i > 0 && pre ? sv(kAcc[i]) : Tensor();
+      sg[i] = zt.defined() ? zt : at::empty_like(t[i]);
+      if (i > 0 && prezeroable(i, mode) && !zt.defined()) pre = false;
+    }
+    sh.grad_bary = ptr<float>(sg[0]);
+    sh.grad_verts = ptr<float>(sg[1]);
+    sh.grad_normals = ptr<float>(sg[2]);
+    if (mode == PR_TEX_VERTEX) sh.grad_vert_colors = ptr<float>(sg[3]);
+    else sh.grad_maps = ptr<float>(sg[3]);
+    sh.grad_light = ptr<float>(sg[4]);
+    sh.grad_camera = ptr<float>(sg[5]);
+    Tensor sws;
+    if (at::globalContext().deterministicAlgorithms()) {  // in-order sums, no float atomics
+      sh.flags = PR_DETERMINISTIC;
+      sws = workspace(api().shade_bwd_workspace_size(&sh), g);
+      sh.workspace = sws.data_ptr();
+      sh.workspace_bytes = static_cast<size_t>(sws.numel());
+    }
+    if (pre && !(sh.flags & PR_DETERMINISTIC)) sh.flags |= PR_GRAD_PREZEROED;
+    if ((p.flags & PR_BLEND_LIVE_ONLY) && sh.pix_count) sh.flags |= PR_SHADE_LIVE_ONLY;
+    if (needs(2) || needs(3) || needs(4) || needs(5) || needs(6) || needs(7))
+      check(api().shade_bwd(&sh, st), "pr_shade_bwd (phong)");
     if (needs(0)) out[0] = gd;
     if (needs(1)) out[1] = gz;
-    if (needs(2)) out[2] = gb;
-    for (int i = 1; i < 6; ++i) out[2 + i] = acc[i];
+    for (int i = 0; i < 6; ++i) out[2 + i] = sg[i];
     Tensor host;
     for (int i = 0; i < 3; ++i) {
       auto ref = sv(i == 0 ? "s0" : i == 1 ? "s1" : "s2");

@@ -197,12 +197,10 @@ class RandomPhongShader(_RandomShaderBase):
                 and fragments.pix_to_face.is_cuda))
         znear, zfar = _planes_from(cameras, kwargs)
         sr, sa = self.smoothrast, self.smoothagg
-        if (FUSE_PHONG and _is_fusable(sr, sa, fragments) and _multidevice.sample_devices() is None
-                and not torch.are_deterministic_algorithms_enabled()):
-            # the shading fused into the blend (PR_BLEND_PHONG): a slot is shaded only where it wins
-            # a sample, no (N,H,W,K,3) colour tensor, no shading kernels.  (Its mesh / texture / light
-            # gradients are float-atomic sums: deterministic mode shades first, pr_shade_bwd's
-            # ordered sums.)
+        if FUSE_PHONG and _is_fusable(sr, sa, fragments) and _multidevice.sample_devices() is None:
+            # the shading fused into the blend's forward (PR_BLEND_PHONG): a slot is shaded only where
+            # it wins a sample (no shading pass over every slot); the backward's shading chain rule
+            # runs for those slots only (pr_shade_bwd skips zero d colours)
             sh = phong_inputs(meshes, fragments, lights, cameras, materials)
             if sh is not None:
                 return _blend.perturbed_blend_phong(

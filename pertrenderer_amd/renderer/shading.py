@@ -127,6 +127,22 @@ class _ShadeFn(torch.autograd.Function):
         return gb, gv, gn, gt, gl, gc, None
 
 
+def _shade_bwd_args(a, mode, gcol, out):
+    """Point the PRShadeArgs `a` at d colours `gcol` and the outputs out = [d bary, d verts,
+    d normals, d texels / vertex colours / maps, d light, d camera] (None: not wanted)."""
+    gb, gv, gn, gt, gl, gc = out
+    a.grad_colors = nat.ptr(gcol)
+    a.grad_bary, a.grad_verts, a.grad_normals = nat.ptr(gb), nat.ptr(gv), nat.ptr(gn)
+    if mode == nat.PR_TEX_GIVEN:
+        a.grad_texels = nat.ptr(gt)
+    elif mode == nat.PR_TEX_VERTEX:
+        a.grad_vert_colors = nat.ptr(gt)
+    else:
+        a.grad_maps = nat.ptr(gt)
+    a.grad_light, a.grad_camera = nat.ptr(gl), nat.ptr(gc)
+    return a
+
+
 def _args(cfg, t):
     a = nat.PRShadeArgs()
     N, H, W, K = cfg["p2f"].shape

@@ -142,7 +142,7 @@ def test_layer_is_used_in_eager_step(device):
 @pytest.mark.parametrize("deterministic", [False, True])
 def test_eval_scene_uses_cpp_shading_and_normals(device, deterministic):
     """eval.py's renderer in the C++ layer: the fused Phong blend node (BlendPhongFn) and the vertex
-    normals; in deterministic mode the shading node (ShadeFn, ordered sums) then the texel blend."""
+    normals, in deterministic mode too (its shading backward then sums in order)."""
     import bench
     wl = bench.Workload(device, image_size=64, K=20, samples=8, eval_scene=True, rast_samples=16)
     torch.use_deterministic_algorithms(deterministic, warn_only=True)
@@ -159,6 +159,6 @@ def test_eval_scene_uses_cpp_shading_and_normals(device, deterministic):
         seen.add(id(fn))
         names.append(fn.name())
         stack.extend(f for f, _ in fn.next_functions)
-    shading = "ShadeFn" if deterministic else "BlendPhongFn"
+    shading = "BlendPhongFn"
     assert any(shading in n for n in names) and any("VertNormalsFn" in n for n in names), names
     assert not any(n.startswith("_") and n.endswith("Backward") for n in names), names

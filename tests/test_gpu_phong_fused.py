@@ -1,6 +1,7 @@
-"""RandomPhongShader with its shading fused into the blend (PR_BLEND_PHONG) against the unfused
-composition it replaces (random_rasterizer.py:99-116: sample_textures -> phong_shading -> smooth_rgb_blend,
-here pr_shade_fwd/bwd -> the texel blend pr_blend_* with colour mode 1).
+"""RandomPhongShader with its shading fused into the blend's forward (PR_BLEND_PHONG; backward:
+PR_BLEND_COLOR_SPARSE then pr_shade_bwd) against the unfused composition it replaces
+(random_rasterizer.py:99-116: sample_textures -> phong_shading -> smooth_rgb_blend, here pr_shade_fwd/bwd
+-> the texel blend pr_blend_* with colour mode 1).
 
 Same Monte-Carlo draws (injected reference noise, or the same Philox keys): the image, d dists,
 d zbuf and d bary are bit-identical (every slot colour and d colour is computed with the same
@@ -104,9 +105,9 @@ def test_fused_phong_host_layers_agree(device):
             assert_close(a, b, rtol=1e-5, atol_rel=1e-6, name=str(i))
 
 
-def test_fused_phong_runs_no_shading_kernel(device, tmp_path):
-    """The fused path launches no pr_shade_* kernel (and so builds no (N,H,W,K,3) colour tensor):
-    the profiler's kernel trace holds the blend kernels and no shading kernel."""
+def test_fused_phong_runs_no_shading_pass(device, tmp_path):
+    """The fused forward shades inside the blend kernel: no shading pass over every slot
+    (shade_fwd_*) runs; the backward is the blend kernel then the shading backward."""
     import json
     from torch.profiler import ProfilerActivity, profile
     _render("uv", "point", True, "philox", device)  # warm
@@ -118,4 +119,5 @@ def test_fused_phong_runs_no_shading_kernel(device, tmp_path):
     names = [e.get("name", "") for e in json.load(open(tr))["traceEvents"]
              if e.get("ph") == "X" and e.get("cat") == "kernel"]
     assert any("blend_fwd_kernel" in n for n in names) and any("blend_bwd_kernel" in n for n in names), names
-    assert not any("shade_" in n for n in names), [n for n in names if "shade_" in n]
+    assert not any("shade_fwd" in n for n in names), [n for n in names if "shade_" in n]
+    assert any("shade_bwd" in n for n in names), names
