@@ -145,8 +145,9 @@ CONFIGS = {
 
 class Workload:
     def __init__(self, device, image_size=256, K=50, samples=8, sigma=1e-3, gamma=1e-2, dist_cam=2.7, seed=0,
-                 batch=1, azim=120.0, rast_samples=None, eval_scene=False):
+                 batch=1, azim=120.0, rast_samples=None, eval_scene=False, loss="native"):
         self.device = device
+        self.loss_kind = loss
         g = torch.Generator().manual_seed(seed)
         Sr = samples if rast_samples is None else rast_samples
         blend = pa.random_rasterizer.BlendParams(sigma, gamma, (0.0, 0.0, 0.0))
@@ -199,6 +200,13 @@ class Workload:
         mesh = self.base.update_padded(Rotate(R).transform_points(self.base.verts_padded()))
         kw = {"lights": self.lights} if self.lights is not None else {}
         images = self.renderer(mesh, cameras=self.cameras, **kw)
+        if self.loss_kind == "native":
+            # eval.py:352-353's ((images[..., :3] - target) ** 2).mean() on the package's fused loss
+            # kernels (pose_opt._RgbMse, pr_rgb_mse_*: 2 forward + 1 backward launches, fp32 summation
+            # order only) -- cfg 5's captured step uses the same; --loss torch: the 11-kernel torch
+            # composition
+            from pertrenderer_amd.pose_opt import rgb_mse
+            return rgb_mse(images, self.target)
         return ((images[..., :3] - self.target) ** 2).mean()
 
     def zero_grad(self):
@@ -500,6 +508,8 @@ def main():
     ap.add_argument("--faces-per-pixel", type=int, default=None)
     ap.add_argument("--samples", type=int, default=None, help="Monte-Carlo samples (global in --shard samples)")
     ap.add_argument("--batch", type=int, default=None, help="meshes per rank")
+    ap.add_argument("--loss", choices=["native", "torch"], default="native",
+                    help="the step's L2 loss: the package's fused kernels (default) or torch ops")
     ap.add_argument("--cpu-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
@@ -562,7 +572,7 @@ def main():
         S_local, Sr_local = S, Sr
 
     mk_wl = lambda: Workload(device, cfg["image_size"], cfg["K"], S_local, seed=0, batch=cfg["batch"], azim=azim,
-                             rast_samples=Sr_local, eval_scene=args.config == "eval")
+                             rast_samples=Sr_local, eval_scene=args.config == "eval", loss=args.loss)
     wl = mk_wl()
     P = cfg["batch"] * cfg["image_size"] * cfg["image_size"]
     mode, note = args.mode, None
@@ -700,9 +710,11 @@ def main():
         "data": "synthetic (meshes from the reference data, random vertex colours, random target)",
         "config": {"workload": f"{args.config} pose-opt step: {meshes}, {Hs}x{Hs}, faces_per_pixel={K}, "
                                f"{samples_txt} Gaussian, sigma=1e-3 gamma=1e-2, blur=ln(1e4-1)*sigma, "
-                               "fwd + L2 loss + bwd + Adam step on the pose (lr 5e-2)",
+                               f"fwd + L2 loss ({args.loss}) + bwd + Adam step on the pose (lr 5e-2)",
                    "image_size": Hs, "faces_per_pixel": K, "nb_samples": S, "rast_samples": Sr, "batch": B,
                    "distinct_frames_per_step": distinct, "execution": mode, "parallelism": par,
+                   "loss": ("eval.py:352-353's ((images[..., :3] - target) ** 2).mean() on the fused native "
+                            "kernels pr_rgb_mse_fwd/_bwd" if args.loss == "native" else "torch ops"),
                    # where the eager autograd nodes run (host_layer.py): "c++" torch::autograd
                    # Functions over the C ABI, or the Python Functions
                    "host_layer": pa.host_layer.layer(),

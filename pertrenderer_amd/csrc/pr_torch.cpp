@@ -58,6 +58,9 @@ struct Api {
   decltype(&pr_shade_bwd) shade_bwd = nullptr;
   decltype(&pr_vert_normals_fwd) vert_normals_fwd = nullptr;
   decltype(&pr_vert_normals_bwd) vert_normals_bwd = nullptr;
+  decltype(&pr_rgb_mse_workspace) rgb_mse_workspace = nullptr;
+  decltype(&pr_rgb_mse_fwd) rgb_mse_fwd = nullptr;
+  decltype(&pr_rgb_mse_bwd) rgb_mse_bwd = nullptr;
 };
 Api g_api;
 bool g_bound = false;
@@ -91,6 +94,9 @@ void bind(const std::unordered_map<std::string, int64_t>& addrs) {
   bind_one(addrs, "pr_shade_bwd", a.shade_bwd);
   bind_one(addrs, "pr_vert_normals_fwd", a.vert_normals_fwd);
   bind_one(addrs, "pr_vert_normals_bwd", a.vert_normals_bwd);
+  bind_one(addrs, "pr_rgb_mse_workspace", a.rgb_mse_workspace);
+  bind_one(addrs, "pr_rgb_mse_fwd", a.rgb_mse_fwd);
+  bind_one(addrs, "pr_rgb_mse_bwd", a.rgb_mse_bwd);
   if (a.abi_version() != PR_ABI_VERSION)
     throw std::runtime_error("pr_torch: built for ABI " + std::to_string(PR_ABI_VERSION) + ", library has " +
                              std::to_string(a.abi_version()));
@@ -1162,6 +1168,63 @@ Tensor vert_normals(const Tensor& verts, const Tensor& faces, Opt csr_start, Opt
   return VertNormalsFn::apply(verts, faces, csr_start, csr_corners);
 }
 
+// ------------------------------------------------------------------ RGB loss
+// pose_opt._RgbMse: eval.py:352-353's ((images[..., :3] - target) ** 2).mean() on pr_rgb_mse_fwd /
+// _bwd (fixed-order sums), the caller's loss of the bench / pose step
+PRRgbMseArgs rgb_mse_args(const Tensor& img, const Tensor& t) {
+  if (img.dim() != 4 || img.scalar_type() != at::kFloat || t.scalar_type() != at::kFloat || img.size(3) < 3 ||
+      t.size(-1) != 3)
+    throw std::invalid_argument("rgb_mse: float32 (N,H,W,C>=3) images and (..,H,W,3) target expected");
+  const int64_t N = img.size(0), H = img.size(1), W = img.size(2);
+  if (t.numel() != H * W * 3 && t.numel() != N * H * W * 3)
+    throw std::invalid_argument("rgb_mse: target does not broadcast to the images");
+  PRRgbMseArgs a{};
+  a.P = N * H * W;
+  a.C = static_cast<int32_t>(img.size(3));
+  a.HW = static_cast<int32_t>(H * W);
+  a.target_batched = (t.numel() == N * H * W * 3 && N > 1) ? 1 : 0;
+  a.image = ptr<float>(img);
+  a.target = ptr<float>(t);
+  return a;
+}
+
+struct RgbMseFn : public torch::autograd::Function<RgbMseFn> {
+  static Tensor forward(AutogradContext* ctx, Tensor images, Tensor target) {
+    on_device({&images, &target});
+    auto img = images.contiguous(), t = target.contiguous();
+    PRRgbMseArgs a = rgb_mse_args(img, t);
+    auto loss = at::empty({}, img.options());
+    auto part = at::empty({static_cast<int64_t>(api().rgb_mse_workspace(a.P))}, img.options());
+    a.loss = ptr<float>(loss);
+    a.partials = ptr<float>(part);
+    at::DeviceGuard dg(img.device());
+    check(api().rgb_mse_fwd(&a, stream_of(img)), "pr_rgb_mse_fwd");
+    Keep k(ctx);
+    k("img", img);
+    k("t", t);
+    k.commit();
+    return loss;
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    variable_list out(2);
+    if (!grads[0].defined()) return out;
+    const Saved sv(ctx);
+    auto img = sv("img"), t = sv("t");
+    PRRgbMseArgs a = rgb_mse_args(img, t);
+    auto gl = dense(grads[0], at::kFloat);
+    auto gi = at::empty_like(img);
+    a.grad_loss = ptr<float>(gl);
+    a.grad_image = ptr<float>(gi);
+    at::DeviceGuard dg(img.device());
+    check(api().rgb_mse_bwd(&a, stream_of(gi)), "pr_rgb_mse_bwd");
+    out[0] = gi;
+    return once(grads, out);
+  }
+};
+
+Tensor rgb_mse(const Tensor& images, const Tensor& target) { return RgbMseFn::apply(images, target); }
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -1176,5 +1239,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scalar_link", &scalar_link);
   m.def("shade", &shade);
   m.def("blend_phong", &blend_phong);
+  m.def("rgb_mse", &rgb_mse);
   m.def("vert_normals", &vert_normals);
 }

@@ -28,7 +28,7 @@ _ENTRIES = ("pr_abi_version", "pr_last_error", "pr_so3_exp_fwd", "pr_so3_exp_bwd
             "pr_rotate_bwd", "pr_project_rast_fwd", "pr_project_bwd", "pr_rast_fwd_workspace_size",
             "pr_rast_bwd_workspace_size", "pr_rast_bwd", "pr_blend_fwd", "pr_blend_plan_size",
             "pr_blend_bwd_workspace_size", "pr_blend_bwd", "pr_shade_fwd", "pr_shade_bwd_workspace_size", "pr_shade_bwd",
-            "pr_vert_normals_fwd", "pr_vert_normals_bwd")
+            "pr_vert_normals_fwd", "pr_vert_normals_bwd", "pr_rgb_mse_workspace", "pr_rgb_mse_fwd", "pr_rgb_mse_bwd")
 
 
 def _path():

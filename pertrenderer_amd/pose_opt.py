@@ -42,6 +42,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from . import host_layer
 from . import random_rasterizer as rr
 from .renderer import (BlendParams, HardPhongShader, Meshes, MeshRasterizer, MeshRenderer, OpenGLPerspectiveCameras,
                        PointLights, RasterizationSettings, Textures, load_obj, look_at_view_transform)
@@ -229,6 +230,15 @@ def _renew_adam(opt, log_rot, lr):
         opt.param_groups[0]["lr"].fill_(float(lr))
 
 
+def rgb_mse(images, target):
+    """eval.py:352-353's loss on the native kernels: the C++ autograd node (host_layer.py) when it
+    is in use, else the Python Function (_RgbMse); the same launches either way."""
+    ext = host_layer.get()
+    if ext is not None and images.is_cuda and target.is_cuda:
+        return ext.rgb_mse(images, target)
+    return _RgbMse.apply(images, target)
+
+
 class _RgbMse(torch.autograd.Function):
     """((images[..., :3] - target) ** 2).mean() (experiments/eval.py:352-353) on the native kernels
     pr_rgb_mse_fwd / pr_rgb_mse_bwd: images (N,H,W,C>=3) float32, target (H,W,3) broadcast over
@@ -308,7 +318,7 @@ class _CapturedIteration:
         # call (init_renderers' bmm, angle_deg) between the replays of a kept graph leaves wrong:
         # GraphSession's reused graphs recorded stale losses with it and tracked the wrong best
         # pose (tools/scratch/graph_mean_repro.py, profiles/r5/cfg5_graph_reuse.md).
-        return _RgbMse.apply(images, self.target)
+        return rgb_mse(images, self.target)
 
     def _body(self):
         st, log_rot = self.st, self.log_rot
