@@ -31,9 +31,15 @@ struct U4 {
   uint32_t x, y, z, w;
 };
 
+// PR_PHILOX_ROUNDS: 10 (Random123's default, pinned by its known-answer vectors) in the product;
+// builds with 7 (the fewest rounds Salmon et al. found Crush-resistant) measure the generator's share
+// of the blend kernels -- a different stream, so never the product's
+#ifndef PR_PHILOX_ROUNDS
+#define PR_PHILOX_ROUNDS 10
+#endif
 PR_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < PR_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
