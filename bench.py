@@ -133,7 +133,7 @@ def load_sphere(device):
 # BASELINE.json configs: cfg2 is the headline (metric's) workload; cfg3/cfg4 are the batch
 # configurations (16 meshes alternating sphere_642 / cube2, each with its own pose); "eval" is
 # eval.py's own renderer (textured cube, RandomPhongShader, GaussianRast's default Sr=16, Sa=8)
-RNG_PEAK_NORMALS_PER_S = 2.04e12  # measured generator throughput per MI355X (DESIGN.md §4 Noise)
+RNG_PEAK_NORMALS_PER_S = 2.76e12  # measured generator throughput per MI355X, Philox4x32-7 + Box-Muller (DESIGN.md §4 Noise)
 
 CONFIGS = {
     "cfg2": dict(batch=1, image_size=256, K=50, samples=8),
@@ -727,14 +727,15 @@ def main():
     }
     # SURVEY §8(d) RNG term: the algorithmic Gaussian draws of the step (the forward's Sr*K rast
     # and Sa*(K+1) agg normals per pixel, regenerated once more by the backward) against the
-    # generator's measured peak (tools/philox_bench.hip: Philox4x32-10 + Box-Muller, every lane busy).
+    # generator's measured peak (tools/philox_bench.hip: Philox4x32-7 + Box-Muller, every lane busy).
     # The kernels skip saturated rast slots, sure-loser logits and padded slots, so the achieved
     # rate can exceed the peak: that is work never done, not a faster generator.
     normals = 2 * B * Hs * Hs * (Sr_local * K + S_local * (K + 1)) * world
     out["rng"] = {"normals_per_step": normals, "normals_per_s": round(normals * args.steps / elapsed, 1),
                   "peak_normals_per_s": RNG_PEAK_NORMALS_PER_S * world,
                   "frac": round(normals * args.steps / elapsed / (RNG_PEAK_NORMALS_PER_S * world), 4),
-                  "peak_from": "tools/philox_bench.hip on one MI355X: 511 G Philox blocks/s x 4 normals"}
+                  "peak_from": "tools/philox_bench.hip on one MI355X: 690 G Philox4x32-7 blocks/s (the streams' rounds) "
+                               "x 4 normals"}
     if shard == "samples":
         # strong scaling: the rasterizer (and the tiny pose kernels) run in full on every rank, the
         # blend on this rank's sample shard; T(N) >= T_rep + T_shard(1) / N bounds the speed-up

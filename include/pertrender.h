@@ -526,12 +526,15 @@ int pr_interp_bwd(const PRInterpArgs* args, void* stream);
 int pr_seed_advance(uint64_t* seeds, int32_t n, void* stream);
 
 /* The kernels' own noise generator on explicit counters (diagnostic / known-answer entry):
- * block i = Philox4x32-10(counters[4i..4i+3], key = keys[i] (lo word, hi word)).
+ * block i = Philox4x32-R(counters[4i..4i+3], key = keys[i] (lo word, hi word)), R = rounds: 10
+ * (Random123's known-answer vectors) or PR_PHILOX_STREAM_ROUNDS (the streams' generator; ABI 20).
  * words (n,4) u32 receives the raw block; normals (n,4) f32 its Box-Muller N(0,1) samples
  * (pr_common.h gauss4), cauchy (n,4) f32 its clamped Cauchy samples (cauchy4).  Each output
- * is nullable.  This is exactly the per-(pixel, slot, sample-group) draw of PR_NOISE_PHILOX. */
+ * is nullable.  With R = PR_PHILOX_STREAM_ROUNDS this is exactly the per-(pixel, slot,
+ * sample-group) draw of PR_NOISE_PHILOX. */
 int pr_philox(const uint32_t* counters, const uint64_t* keys, int64_t n, uint32_t* words, float* normals,
-              float* cauchy, void* stream);
+              float* cauchy, int32_t rounds, void* stream);
+#define PR_PHILOX_STREAM_ROUNDS 7 /* rounds of the PR_NOISE_PHILOX streams (pr_philox's rounds: 10 or this) */
 
 #ifdef __cplusplus
 }

@@ -1,8 +1,9 @@
-"""numpy Philox4x32-10 and the noise streams of the kernels' Philox mode  —  TEST INFRASTRUCTURE ONLY.
+"""numpy Philox4x32-R and the noise streams of the kernels' Philox mode  —  TEST INFRASTRUCTURE ONLY.
 
 Restates Salmon, Moraes, Dror & Shaw, "Parallel random numbers: as easy as 1, 2, 3"
-(SC'11), Philox4x32 with R=10 rounds, as used by pertrenderer_amd/csrc/pr_common.h,
-and the counter layout the kernels use:
+(SC'11), Philox4x32 with R rounds (pertrenderer_amd/csrc/pr_common.h philox4x32<R>): the noise
+streams use STREAM_ROUNDS = 7 (round 6; Crush-resistant per Salmon et al.), the round function is
+pinned at R = 10 by Random123's known-answer vectors.  The counter layout the kernels use:
   rast:  counter (pixel, slot, sample // 4, 0x52415354), key = seed_r
   agg:   counter (pixel, slot, sample // 4, 0x41474752), key = seed_a
 Each block gives 4 N(0,1) samples by Box-Muller (pr_common.h:gauss4).
@@ -16,13 +17,21 @@ TAG_RAST, TAG_AGG = 0x52415354, 0x41474752
 _MASK = np.uint64(0xFFFFFFFF)
 
 
+STREAM_ROUNDS = 7  # pr_common.h PR_PHILOX_ROUNDS (include/pertrender.h PR_PHILOX_STREAM_ROUNDS)
+
+
 def philox4x32_10(ctr, key):
-    """ctr: (...,4) uint32, key: (...,2) uint32 -> (...,4) uint32."""
+    """Philox4x32-10 (Random123's known-answer vectors)."""
+    return philox4x32(ctr, key, 10)
+
+
+def philox4x32(ctr, key, rounds=STREAM_ROUNDS):
+    """ctr: (...,4) uint32, key: (...,2) uint32 -> (...,4) uint32 after `rounds` rounds."""
     c = [np.asarray(ctr[..., i], np.uint32) for i in range(4)]
     k0 = np.asarray(key[..., 0], np.uint32).copy()
     k1 = np.asarray(key[..., 1], np.uint32).copy()
     with np.errstate(over="ignore"):
-        for _ in range(10):
+        for _ in range(rounds):
             p0 = M0 * c[0].astype(np.uint64)
             p1 = M1 * c[2].astype(np.uint64)
             hi0, lo0 = (p0 >> np.uint64(32)).astype(np.uint32), (p0 & _MASK).astype(np.uint32)
@@ -39,12 +48,12 @@ def u01(r):
             * np.float32(5.9604644775390625e-08))
 
 
-def block(seed, pixel, slot, group, tag):
+def block(seed, pixel, slot, group, tag, rounds=STREAM_ROUNDS):
     pixel, slot, group = np.broadcast_arrays(np.asarray(pixel, np.uint32), np.asarray(slot, np.uint32),
                                              np.asarray(group, np.uint32))
     ctr = np.stack([pixel, slot, group, np.full(pixel.shape, tag, np.uint32)], axis=-1)
     key = np.array([seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF], np.uint32)
-    return philox4x32_10(ctr, np.broadcast_to(key, ctr.shape[:-1] + (2,)))
+    return philox4x32(ctr, np.broadcast_to(key, ctr.shape[:-1] + (2,)), rounds)
 
 
 def _bm4(w):

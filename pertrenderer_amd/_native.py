@@ -177,7 +177,7 @@ EXPORTS = {
     "pr_so3_exp_bwd": (C.c_int, [C.POINTER(PRSO3Args), _vp]),
     "pr_rotate_fwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
     "pr_rotate_bwd": (C.c_int, [C.POINTER(PRRotateArgs), _vp]),
-    "pr_philox": (C.c_int, [_vp, _vp, C.c_int64, _vp, _vp, _vp, _vp]),
+    "pr_philox": (C.c_int, [_vp, _vp, C.c_int64, _vp, _vp, _vp, C.c_int32, _vp]),
     "pr_shade_fwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),
     "pr_shade_bwd_workspace_size": (C.c_size_t, [C.POINTER(PRShadeArgs)]),
     "pr_shade_bwd": (C.c_int, [C.POINTER(PRShadeArgs), _vp]),

@@ -1827,14 +1827,16 @@ __global__ void seed_advance_kernel(uint64_t* seeds, int n) {
   if (i < n) seeds[i] = seed_next(seeds[i]);
 }
 
-// pr_philox: the generator of PR_NOISE_PHILOX on caller-given counters (known-answer tests)
+// pr_philox: the generator of PR_NOISE_PHILOX on caller-given counters (known-answer tests); R = 10
+// (Random123's vectors) or the streams' kPhiloxRounds
+template <int R>
 __global__ void __launch_bounds__(kThreads) philox_kernel(const uint4* ctr, const uint64_t* keys, int64_t n,
                                                           uint4* words, float4* normals, float4* cauchy) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const uint4 c = ctr[i];
   const uint64_t k = keys[i];
-  const U4 u = philox4x32_10(U4{c.x, c.y, c.z, c.w}, (uint32_t)k, (uint32_t)(k >> 32));
+  const U4 u = philox4x32<R>(U4{c.x, c.y, c.z, c.w}, (uint32_t)k, (uint32_t)(k >> 32));
   if (words) words[i] = make_uint4(u.x, u.y, u.z, u.w);
   float e[4];
   if (normals) {
@@ -2322,11 +2324,15 @@ extern "C" int pr_seed_advance(uint64_t* seeds, int32_t n, void* stream) {
 }
 
 extern "C" int pr_philox(const uint32_t* counters, const uint64_t* keys, int64_t n, uint32_t* words, float* normals,
-                         float* cauchy, void* stream) {
+                         float* cauchy, int32_t rounds, void* stream) {
   if (!counters || !keys || n <= 0 || n > (int64_t(1) << 40)) return set_error(PR_ERR_ARG, "philox: bad args");
+  if (rounds != 10 && rounds != kPhiloxRounds) return set_error(PR_ERR_ARG, "philox: rounds must be 10 or the streams'");
   const int64_t nb = (n + kThreads - 1) / kThreads;
-  philox_kernel<<<(unsigned)nb, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-      reinterpret_cast<const uint4*>(counters), keys, n, reinterpret_cast<uint4*>(words),
-      reinterpret_cast<float4*>(normals), reinterpret_cast<float4*>(cauchy));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint4* c = reinterpret_cast<const uint4*>(counters);
+  uint4* w = reinterpret_cast<uint4*>(words);
+  float4 *nm = reinterpret_cast<float4*>(normals), *cy = reinterpret_cast<float4*>(cauchy);
+  if (rounds == 10) philox_kernel<10><<<(unsigned)nb, kThreads, 0, st>>>(c, keys, n, w, nm, cy);
+  else philox_kernel<kPhiloxRounds><<<(unsigned)nb, kThreads, 0, st>>>(c, keys, n, w, nm, cy);
   return check_launch("philox");
 }

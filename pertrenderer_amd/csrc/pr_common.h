@@ -31,15 +31,19 @@ struct U4 {
   uint32_t x, y, z, w;
 };
 
-// PR_PHILOX_ROUNDS: 10 (Random123's default, pinned by its known-answer vectors) in the product;
-// builds with 7 (the fewest rounds Salmon et al. found Crush-resistant) measure the generator's share
-// of the blend kernels -- a different stream, so never the product's
+// Philox4x32-R (Salmon et al., SC'11).  The noise streams use R = PR_PHILOX_ROUNDS = 7 (round 6):
+// Salmon et al. report Philox4x32 Crush-resistant (TestU01 BigCrush) from 7 rounds, Random123's
+// default 10 keeps a safety margin.  The blend kernels are bound by their generator at large S, so
+// 7 rounds measured cfg 2 3588 -> 3680 and cfg 4 998 -> 1060 frames/s (DESIGN.md §4 Noise).  The
+// round function is pinned by Random123's 10-round known-answer vectors through pr_philox(rounds 10).
 #ifndef PR_PHILOX_ROUNDS
-#define PR_PHILOX_ROUNDS 10
+#define PR_PHILOX_ROUNDS 7
 #endif
-PR_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+constexpr int kPhiloxRounds = PR_PHILOX_ROUNDS;
+template <int R>
+PR_DEV U4 philox4x32(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < PR_PHILOX_ROUNDS; ++r) {
+  for (int r = 0; r < R; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
@@ -50,6 +54,7 @@ PR_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
   }
   return c;
 }
+PR_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) { return philox4x32<10>(c, k0, k1); }
 
 // uniform in (0,1): odd 24-bit integer * 2^-24, exact in fp32, never 0 or 1
 PR_DEV float u01(uint32_t r) { return (float)((r >> 8) | 1u) * 5.9604644775390625e-08f; }
@@ -87,7 +92,7 @@ PR_DEV void cauchy4(const U4& u, float e[4]) {
 PR_DEV float noise_score(float e, bool cauchy) { return cauchy ? (2.f * e) / (1.f + e * e) : e; }
 
 PR_DEV U4 philox_block(uint64_t seed, uint32_t pixel, uint32_t slot, uint32_t group, uint32_t tag) {
-  return philox4x32_10(U4{pixel, slot, group, tag}, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return philox4x32<kPhiloxRounds>(U4{pixel, slot, group, tag}, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
 // k-th index of [0, n) in centre-out order (n/2, n/2-1, n/2+1, ...): workgroups over

@@ -1,12 +1,15 @@
-"""Known-answer tests of the Philox4x32-10 generator behind PR_NOISE_PHILOX.
+"""Known-answer tests of the Philox4x32 generator behind PR_NOISE_PHILOX.
 
 The vectors are Random123's published kat_vectors for philox4x32_10 (Salmon et al., SC'11;
-the three rows the Random123 distribution lists for R=10).  They pin
+the three rows the Random123 distribution lists for R=10).  They pin the round function of
   * oracle/philox_ref.py (the numpy restatement, CPU test), and
-  * the device generator itself, through the C-ABI entry pr_philox (GPU test), which runs
-    pr_common.h's philox4x32_10 / gauss4 / cauchy4 — the exact code the blend kernels draw with.
+  * the device generator itself, through the C-ABI entry pr_philox at 10 rounds (GPU test), which
+    runs pr_common.h's philox4x32<R> / gauss4 / cauchy4 — the code the blend kernels draw with.
+The streams run the same round function for PR_PHILOX_STREAM_ROUNDS = 7 rounds (round 6): the
+device's 7-round blocks equal the restatement's bit for bit (test_device_noise_streams_...).
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -34,8 +37,14 @@ def test_numpy_philox_matches_random123_kat():
 def test_counter_layout_of_the_noise_streams():
     """block() puts (pixel, slot, sample group, tag) in the counter and the 64-bit seed in the key."""
     seed = 0x299f31d0_a4093822
-    b = philox_ref.block(seed, 0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344)
+    b = philox_ref.block(seed, 0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344, rounds=10)
     assert [int(x) for x in b] == list(KAT[2][2])
+    # the streams' rounds (7) by default, matching the header's constant
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                            "pertrender.h")).read()
+    assert f"#define PR_PHILOX_STREAM_ROUNDS {philox_ref.STREAM_ROUNDS} " in hdr
+    b7 = philox_ref.block(seed, 0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344)
+    assert [int(x) for x in b7] != list(KAT[2][2])
 
 
 def test_uniform_mapping_is_open_interval():
@@ -44,7 +53,7 @@ def test_uniform_mapping_is_open_interval():
     assert u[0] == np.float32(2.0 ** -24) and u[1] == np.float32(1 - 2.0 ** -24)
 
 
-def _device_draw(ctr, keys, dev):
+def _device_draw(ctr, keys, dev, rounds=philox_ref.STREAM_ROUNDS):
     from pertrenderer_amd import _native as nat
     lib = nat.load()
     n = ctr.shape[0]
@@ -54,7 +63,7 @@ def _device_draw(ctr, keys, dev):
     normals = torch.empty((n, 4), dtype=torch.float32, device=dev)
     cauchy = torch.empty((n, 4), dtype=torch.float32, device=dev)
     nat.check(lib.pr_philox(nat.ptr(c), nat.ptr(k), C.c_int64(n), nat.ptr(words), nat.ptr(normals),
-                            nat.ptr(cauchy), nat.stream_of(words)), "pr_philox")
+                            nat.ptr(cauchy), C.c_int32(rounds), nat.stream_of(words)), "pr_philox")
     torch.cuda.synchronize()
     return (words.cpu().numpy().view(np.uint32), normals.cpu().numpy(), cauchy.cpu().numpy())
 
@@ -63,7 +72,7 @@ def _device_draw(ctr, keys, dev):
 def test_device_philox_matches_random123_kat(device):
     ctr = np.array([c for c, _, _ in KAT], np.uint32)
     keys = np.array([k[0] | (k[1] << 32) for _, k, _ in KAT], np.uint64)
-    words, _, _ = _device_draw(ctr, keys, device)
+    words, _, _ = _device_draw(ctr, keys, device, rounds=10)
     np.testing.assert_array_equal(words, np.array([o for _, _, o in KAT], np.uint32))
 
 
@@ -80,7 +89,7 @@ def test_device_noise_streams_match_numpy_restatement(device):
     keys = rng.integers(0, 2 ** 63, n, dtype=np.uint64)
     words, normals, cauchy = _device_draw(ctr, keys, device)
     kw = np.stack([keys & np.uint64(0xFFFFFFFF), keys >> np.uint64(32)], -1).astype(np.uint32)
-    ref_w = philox_ref.philox4x32_10(ctr, kw)
+    ref_w = philox_ref.philox4x32(ctr, kw)  # the streams' rounds
     np.testing.assert_array_equal(words, ref_w)
     ref_n = np.stack(philox_ref._bm4(ref_w), -1)
     np.testing.assert_allclose(normals, ref_n, rtol=0, atol=2e-5 * np.maximum(1.0, np.abs(ref_n)).max())
