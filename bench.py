@@ -184,6 +184,8 @@ class Workload:
                                      shader=shader)
         self.log_rot = (0.3 * torch.randn((batch, 3), generator=g)).to(device).requires_grad_(True)
         self.target = torch.rand((batch, image_size, image_size, 3), generator=g).to(device)
+        # loss.backward()'s seed gradient, made once (a captured step then holds no fill kernel for it)
+        self.one = torch.ones((), device=device)
         self.K, self.S, self.Sr, self.H, self.batch = K, samples, Sr, image_size, batch
         self.F = faces.shape[0]
 
@@ -370,7 +372,7 @@ def build_step(wl, world, mode, device, grad_weight, dist_on=None):
         wl.opt = torch.optim.Adam([wl.log_rot], lr=5e-2, fused=True)
 
         def step():
-            wl.forward().backward()
+            wl.forward().backward(wl.one)
             if dist_on:
                 average_gradients(wl.params(), weight=grad_weight)
             wl.opt.step()
@@ -387,7 +389,7 @@ def build_step(wl, world, mode, device, grad_weight, dist_on=None):
     with torch.cuda.stream(side):
         for _ in range(3):
             ds.advance()
-            wl.forward().backward()
+            wl.forward().backward(wl.one)
             wl.opt.step()
             wl.zero_grad()
     torch.cuda.current_stream().wait_stream(side)
@@ -396,7 +398,7 @@ def build_step(wl, world, mode, device, grad_weight, dist_on=None):
     # thread_local: CUDA calls of other threads (the RCCL watchdog at N>1) must not void the capture
     with torch.cuda.graph(graph, capture_error_mode="thread_local"):
         ds.advance()
-        wl.forward().backward()
+        wl.forward().backward(wl.one)
         if not dist_on:
             wl.opt.step()
     wl.graph = graph
@@ -423,7 +425,7 @@ def split_fwd_bwd(wl, steps, world, dist_on=None):
         wl.seed.advance()
         loss = wl.forward()
     with torch.cuda.graph(gb, pool=pool, capture_error_mode="thread_local"):
-        loss.backward(retain_graph=True)
+        loss.backward(wl.one, retain_graph=True)
         if not (world > 1 if dist_on is None else dist_on):
             wl.opt.step()
     for _ in range(3):
@@ -461,7 +463,7 @@ def instrumented_pass(wl, steps):
         for _ in range(steps):
             if seed is not None:
                 seed.advance()
-            wl.forward().backward()
+            wl.forward().backward(wl.one)
             for p in wl.params():
                 p.grad = None
         torch.cuda.synchronize()
@@ -486,7 +488,7 @@ def eager_split(wl, steps):
         fb[i][0].record()
         loss = wl.forward()
         fb[i][1].record()
-        loss.backward()
+        loss.backward(wl.one)
         fb[i][2].record()
         wl.zero_grad()
     torch.cuda.synchronize()
