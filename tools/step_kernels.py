@@ -36,9 +36,13 @@ def step(wl, ds):
     with record_function("## renderer (rasterizer + shader)"):
         images = wl.renderer(mesh, cameras=wl.cameras, **kw)
     with record_function("## loss (caller)"):
-        loss = ((images[..., :3] - wl.target) ** 2).mean()
+        if wl.loss_kind == "native":  # bench's default: eval.py's loss on pose_opt.rgb_mse
+            from pertrenderer_amd.pose_opt import rgb_mse
+            loss = rgb_mse(images, wl.target)
+        else:
+            loss = ((images[..., :3] - wl.target) ** 2).mean()
     with record_function("## backward"):
-        loss.backward()
+        loss.backward(wl.one)
     with record_function("## adam (caller)"):
         wl.opt.step()
     wl.zero_grad()
@@ -54,6 +58,7 @@ def main():
     ap.add_argument("--config", default="cfg2", choices=sorted(bench.CONFIGS))
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--loss", choices=["native", "torch"], default="native", help="bench.py --loss")
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph",
                     help="graph: the captured step's configuration (device seed and smoothing scalars, "
                          "capturable Adam), run eagerly; eager: bench --mode eager / eval.py's (CPU smoothing "
@@ -63,7 +68,7 @@ def main():
     pa.native_library()
     c = bench.CONFIGS[args.config]
     wl = bench.Workload(dev, c["image_size"], c["K"], c["samples"], batch=c["batch"],
-                        rast_samples=c.get("rast_samples"), eval_scene=args.config == "eval")
+                        rast_samples=c.get("rast_samples"), eval_scene=args.config == "eval", loss=args.loss)
     if args.mode == "graph":
         ds = pa.noise.DeviceSeed(dev)
         pa.noise.use_device_seed(ds)

@@ -1,12 +1,14 @@
-"""One graph step's kernel timeline from a rocprofv3 kernel trace (between two seed_advance launches).
+"""One graph step's kernel timeline from a rocprofv3 kernel trace (between two launches of the
+step's first kernel: so3_exp_fwd since the seed advance moved into project_prep).
 
-    python tools/step_timeline.py gpurun_out/prof_TAG/prof_kernel_trace.csv [step_index]
+    python tools/step_timeline.py gpurun_out/prof_TAG/prof_kernel_trace.csv [step_index] [first_kernel]
 """
 import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda x: int(x["Start_Timestamp"]))
-idx = [i for i, x in enumerate(rows) if "seed_advance" in x["Kernel_Name"]]
+first = sys.argv[3] if len(sys.argv) > 3 else "so3_exp_fwd"
+idx = [i for i, x in enumerate(rows) if first in x["Kernel_Name"]]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(idx) // 2
 i0, i1 = idx[k], idx[k + 1]
 t0 = int(rows[i0]["Start_Timestamp"])
