@@ -342,8 +342,9 @@ def _timed(name, fn):
 # ============================================================== fused blend
 # Keep the per-slot (prob, rast score) of the forward for the backward (8 B/slot of
 # HBM) instead of regenerating the rast noise there.  Either way the results are
-# bit-identical (tests/test_gpu_blend.py::test_rast_cache_is_bit_identical).
-RAST_CACHE = True
+# bit-identical (tests/test_gpu_blend.py::test_rast_cache_is_bit_identical).  PR_RAST_CACHE=0
+# regenerates (measurement knob).
+RAST_CACHE = os.environ.get("PR_RAST_CACHE", "1") != "0"
 
 
 def _no_uniform_grad(vflags):
