@@ -15,8 +15,10 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from pertrenderer_amd import _native as nat  # noqa: E402
 
-cfg = bench.CONFIGS[os.environ.get("PR_PROF_CONFIG", "cfg2")]
-wl = bench.Workload(torch.device("cuda:0"), cfg["image_size"], cfg["K"], cfg["samples"], batch=cfg["batch"])
+name = os.environ.get("PR_PROF_CONFIG", "cfg2")
+cfg = bench.CONFIGS[name]
+wl = bench.Workload(torch.device("cuda:0"), cfg["image_size"], cfg["K"], cfg["samples"], batch=cfg["batch"],
+                    rast_samples=cfg.get("rast_samples"), eval_scene=name == "eval")
 for _ in range(3):  # warm: the last forward's records are kept
     wl.forward().backward()
     torch.cuda.synchronize()
