@@ -232,7 +232,11 @@ def _renew_adam(opt, log_rot, lr):
 
 def rgb_mse(images, target):
     """eval.py:352-353's loss on the native kernels: the C++ autograd node (host_layer.py) when it
-    is in use, else the Python Function (_RgbMse); the same launches either way."""
+    is in use, else the Python Function (_RgbMse); the same launches either way.  The native
+    nodes differentiate the images only: a target that requires grad takes eval.py's torch
+    expression, so its gradient is not dropped."""
+    if torch.is_tensor(target) and target.requires_grad and torch.is_grad_enabled():
+        return ((images[..., :3] - target) ** 2).mean()
     ext = host_layer.get()
     if ext is not None and images.is_cuda and target.is_cuda:
         return ext.rgb_mse(images, target)

@@ -218,6 +218,19 @@ def test_native_rgb_loss_matches_torch(device, shape, tshape):
         assert float(g[..., 3:].abs().max()) == 0.0
 
 
+def test_rgb_mse_target_gradient_not_dropped(device):
+    """pose_opt.rgb_mse with a target that requires grad: both gradients match eval.py's torch
+    expression (the native nodes differentiate the images only, so such a call takes torch's)."""
+    torch.manual_seed(6)
+    img = torch.rand((2, 9, 7, 4), device=device, requires_grad=True)
+    t = torch.rand((9, 7, 3), device=device, requires_grad=True)
+    gi, gt = torch.autograd.grad(pose_opt.rgb_mse(img, t), (img, t))
+    ri, rt = torch.autograd.grad(((img[..., :3] - t) ** 2).mean(), (img, t))
+    torch.testing.assert_close(gi, ri)
+    torch.testing.assert_close(gt, rt)
+    assert float(gt.abs().max()) > 0
+
+
 def test_pose_step_kernel_bookkeeping(device):
     """pr_pose_step (the captured step's bookkeeping) against eval.py:356-358, 372-385 restated in
     torch: records, best-loss pose, the grad-norm guard, the smoothing gradients' running sum and
