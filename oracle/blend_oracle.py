@@ -116,6 +116,7 @@ def logits_bwd(dz, prob, mask, zfar, znear, gamma, alpha, eps, aux):
     dzmax = dzmax * (aux["zmax_raw"][..., None] >= eps)          # clamp(min=eps) (:199)
     dz_inv = dzk + torch.zeros_like(dzk).scatter_(-1, aux["kmax"][..., None], dzmax)  # max (:199)
     dzbuf = -(dz_inv * mask / (zfar - znear))                     # :198
+    aux["dz_inv"] = dz_inv
     # prod_corrected backward (:329-336): x = gamma/alpha, y = log prob
     L = aux["L"]
     dL = aux["gal"] * dzk
@@ -128,6 +129,16 @@ def logits_bwd(dz, prob, mask, zfar, znear, gamma, alpha, eps, aux):
     dgamma = dgal / alpha
     dalpha = -dgal * ((gamma / alpha) / alpha)
     return dzbuf, dprob, dgamma, dalpha
+
+
+def plane_grads(zbuf, zfar, znear, mask, dz_inv):
+    """d znear, d zfar (each (N,1,1,1)) of smoothagg.py:198's z_inv = (zfar - zbuf) / (zfar - znear)
+    * mask given dL/dz_inv: torch autograd of that expression, i.e. what the reference's graph
+    gives camera planes that require grad (random_rasterizer.py:172-173)."""
+    zn = znear.detach().clone().requires_grad_(True)
+    zf = zfar.detach().clone().requires_grad_(True)
+    z_inv = (zf - zbuf) / (zf - zn) * mask
+    return torch.autograd.grad(z_inv, (zn, zf), dz_inv)
 
 
 def _prod_backward(x, g):
@@ -163,7 +174,7 @@ def blend_forward(p2f, dists, zbuf, colors, noise_r, noise_a, sigma, gamma, alph
     img = torch.ones((N, H, W, 4), dtype=F32)
     img[..., :3] = (wz[..., None] * colors).sum(dim=-2) + wb * bg      # :50-53
     img[..., 3] = 1.0 - alpha_chan                                     # :54
-    saved = dict(mask=mask, maps=maps, vr=vr, prob=prob, one_minus=one_minus, aux=aux, w=w,
+    saved = dict(mask=mask, maps=maps, vr=vr, prob=prob, one_minus=one_minus, aux=aux, w=w, zbuf=zbuf,
                  vra=vra, W=Wt, colors=colors, bg=bg, zfar=zfar, znear=znear, noise_r=noise_r,
                  noise_a=noise_a, sigma=sigma, gamma=gamma, alpha=alpha, eps=eps, P=P,
                  kinds=(rast_kind, rast_vr, agg_kind, agg_vr))
@@ -188,8 +199,9 @@ def blend_backward(gimg, s):
     dprob = dprob_a + dprob_l
     dP = dprob * s["mask"]                                             # :47
     dD, dsigma = heaviside_bwd(s["maps"], s["vr"], s["noise_r"], s["sigma"], dP, rk, rvr)
+    dzn, dzf = plane_grads(s["zbuf"], s["zfar"], s["znear"], s["mask"], s["aux"]["dz_inv"])
     return dict(dists=-dD, zbuf=dzbuf, colors=dcolors, sigma=dsigma, gamma=dg1 + dg2,
-                alpha=dalpha)
+                alpha=dalpha, znear=dzn, zfar=dzf)
 
 
 # --------------------------------------------------------------- standalone methods
@@ -202,13 +214,15 @@ def rasterize_forward_backward(dists, noise_r, sigma, gP, kind="gaussian", use_v
 
 
 def aggregate_forward_backward(zbuf, zfar, znear, prob, mask, noise_a, gamma, alpha, eps, gW,
-                               kind="gaussian", use_vr=True):
+                               kind="gaussian", use_vr=True, planes=False):
     """GaussianAgg / CauchyAgg / GaussianAgg_wovr .aggregate (smoothagg.py:196-250) and the
-    backward."""
+    backward (planes=True: also d znear, d zfar)."""
     z, aux = logits(zbuf, zfar, znear, prob, mask, gamma, alpha, eps)
     Wt, w, vra = argmax_fwd(z, noise_a, gamma)
     dz, dg1 = argmax_bwd(w, vra, noise_a, gamma, gW, kind, use_vr)
     dzbuf, dprob, dg2, dalpha = logits_bwd(dz, prob, mask, zfar, znear, gamma, alpha, eps, aux)
+    if planes:
+        return (Wt, dzbuf, dprob, dg1 + dg2, dalpha) + tuple(plane_grads(zbuf, zfar, znear, mask, aux["dz_inv"]))
     return Wt, dzbuf, dprob, dg1 + dg2, dalpha
 
 
@@ -279,5 +293,8 @@ def soft_blend_forward_backward(p2f, dists, zbuf, colors, sigma, gamma, alpha, e
     img[..., :3] = (Wt[..., :-1, None] * col).sum(-2) + Wt[..., -1:] * bg
     img[..., 3] = 1.0 - alpha_chan
     (img * gimg).sum().backward()
-    return img.detach(), dict(dists=d.grad, zbuf=zb.grad, colors=col.grad, sigma=sig.grad,
-                              gamma=gam.grad, alpha=alp.grad)
+    out = dict(dists=d.grad, zbuf=zb.grad, colors=col.grad, sigma=sig.grad, gamma=gam.grad, alpha=alp.grad)
+    for name, z in (("znear", znear), ("zfar", zfar)):  # planes that require grad (leaves)
+        if torch.is_tensor(z) and z.requires_grad:
+            out[name] = z.grad
+    return img.detach(), out

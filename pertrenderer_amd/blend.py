@@ -295,6 +295,61 @@ def _link_grad(gsc, need):
 _valid_counts = None
 
 
+class _ZPlaneGrad(torch.autograd.Function):
+    """Identity on zbuf whose backward also gives znear / zfar their gradients.  zbuf enters the
+    blend only through z_inv = (zfar - zbuf) / (zfar - znear) * mask (smoothagg.py:198), so the
+    kernels' d zbuf = -dL/dz_inv / (zfar - znear) at valid slots fixes dL/dz_inv, and then
+    d znear = sum -d zbuf (zfar - zbuf) / (zfar - znear), d zfar = sum -d zbuf (zbuf - znear) /
+    (zfar - znear) over each image's valid slots.  Used only when a plane requires grad."""
+
+    @staticmethod
+    def forward(ctx, zbuf, znear, zfar, valid):
+        ctx.save_for_backward(zbuf, valid)
+        ctx.planes = (znear, zfar)
+        return zbuf.clone()
+
+    @staticmethod
+    def backward(ctx, gz):
+        if gz is None:
+            return None, None, None, None
+        zb, valid = ctx.saved_tensors
+        N = zb.shape[0]
+        zn_in, zf_in = ctx.planes
+        zn = _planes(zn_in, N, zb.device).reshape(N, 1, 1, 1)
+        zf = _planes(zf_in, N, zb.device).reshape(N, 1, 1, 1)
+        d = zf - zn
+        g = torch.where(valid, gz, torch.zeros((), dtype=gz.dtype, device=gz.device))
+        z = torch.where(valid, zb, zn)  # (masked slots contribute 0 either way; no inf / nan)
+        out = []
+        for plane, term in ((zn_in, zf - z), (zf_in, z - zn)):
+            if torch.is_tensor(plane) and plane.requires_grad:
+                per = (-(g * term) / d).sum(dim=(1, 2, 3))  # (N,)
+                gp = per.sum() if plane.numel() == 1 else per
+                out.append(gp.reshape(plane.shape).to(device=plane.device, dtype=plane.dtype))
+            else:
+                out.append(None)
+        return gz, out[0], out[1], None
+
+
+def _planes_need_grad(znear, zfar):
+    return torch.is_grad_enabled() and any(torch.is_tensor(z) and z.requires_grad for z in (znear, zfar))
+
+
+def plane_link(zbuf, znear, zfar, pix_to_face=None, mask=None):
+    """zbuf, linked to znear / zfar when either requires grad (the native kernels take the planes
+    as constants): returns (zbuf, linked).  Valid slots from the rasterizer's counts when attached,
+    else pix_to_face >= 0, else `mask`."""
+    if not _planes_need_grad(znear, zfar):
+        return zbuf, False
+    if mask is None:
+        counts = _counts_for(pix_to_face)
+        K = pix_to_face.shape[-1]
+        mask = (torch.arange(K, device=pix_to_face.device) < counts[..., None].long()) if counts is not None \
+            else pix_to_face >= 0
+    valid = mask.expand(zbuf.shape).to(torch.bool)
+    return _ZPlaneGrad.apply(zbuf, znear, zfar, valid), True
+
+
 def _counts_for(pix_to_face):
     """The native rasterizer's valid-prefix counts of these fragments (int32 (N,H,W) on the same
     device), or None: the kernels then read pix_to_face at every slot."""
@@ -632,6 +687,8 @@ def perturbed_blend_phong(sh, pix_to_face, bary, dists, zbuf, sigma, gamma, alph
                     noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind))
         noise = _merge(*pair)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
+    zbuf, linked = plane_link(zbuf, znear, zfar, pix_to_face)
+    live_only = live_only and not linked  # the plane link reads d zbuf at every slot
     counts = _counts_for(pix_to_face)
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=counts)
@@ -743,6 +800,8 @@ def perturbed_blend_vertex(vert_colors, faces, pix_to_face, bary, dists, zbuf, s
                     noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind))
         noise = _merge(*pair)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
+    zbuf, linked = plane_link(zbuf, znear, zfar, pix_to_face)
+    live_only = live_only and not linked  # the plane link reads d zbuf at every slot
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
     if live_only and cfg["counts"] is not None:  # the caller reads the valid prefix only (backward: no zero rows)
@@ -775,6 +834,8 @@ def perturbed_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, nb_sa
                     noise_mod.draw_agg((N, H, W, K + 1), nb_samples_agg, pix_to_face.device, fixed_noise, agg_kind))
         noise = _merge(*pair)
     _check_injected(noise, nb_samples_rast, nb_samples_agg, shape, True, True)
+    zbuf, linked = plane_link(zbuf, znear, zfar, pix_to_face)
+    live_only = live_only and not linked  # the plane link reads d zbuf at every slot
     cfg = dict(Sr=int(nb_samples_rast), Sa=int(nb_samples_agg), eps=float(eps),
                bg=_background(background), noise=noise, vflags=vflags, counts=_counts_for(pix_to_face))
     if live_only and cfg["counts"] is not None:  # the caller reads the valid prefix only (backward: no zero rows)
@@ -795,6 +856,7 @@ def soft_blend(colors, pix_to_face, dists, zbuf, sigma, gamma, alpha, eps=1e-10,
         raise ValueError(f"colors must be (N,H,W,K,3) = {shape + (3,)}, got {tuple(colors.shape)}")
     if tuple(dists.shape) != shape or tuple(zbuf.shape) != shape:
         raise ValueError("dists / zbuf must match pix_to_face's shape")
+    zbuf, _ = plane_link(zbuf, znear, zfar, pix_to_face)
     cfg = dict(Sr=1, Sa=1, eps=float(eps), bg=_background(background), noise=Noise.philox(),
                vflags=nat.PR_BLEND_SOFT, counts=_counts_for(pix_to_face))
     (sigma, gamma, alpha), link = _link_scalars((sigma, gamma, alpha), pix_to_face.device)
@@ -927,4 +989,5 @@ def perturbed_aggregate(zbuf, zfar, znear, prob_map, mask, gamma, alpha, nb_samp
     mask = mask.expand(N, H, W, K) if mask.shape != zbuf.shape else mask
     prob_map = prob_map.expand(N, H, W, K) if prob_map.shape != zbuf.shape else prob_map
     cfg = dict(Sa=int(nb_samples), eps=float(eps), noise=noise, vflags=vflags)
+    zbuf, _ = plane_link(zbuf, znear, zfar, mask=mask)
     return _AggregateFn.apply(zbuf, prob_map, gamma, alpha, mask, znear, zfar, cfg)

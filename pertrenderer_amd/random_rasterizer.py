@@ -65,8 +65,9 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
     if _is_fusable(smoothrast, smoothagg, fragments):
         if _multidevice.sample_devices() is not None and _noise.get_noise_source() == "philox":
             # samples split over the devices of set_sample_devices (in-process RCCL collectives)
+            zbuf, _ = _blend.plane_link(fragments.zbuf, znear, zfar, fragments.pix_to_face)
             return _multidevice.sharded_blend(
-                colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
+                colors, fragments.pix_to_face, fragments.dists, zbuf, smoothrast.sigma,
                 smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
                 eps=smoothagg.eps, background=background, znear=znear, zfar=zfar,
                 fixed_noise=smoothagg.fixed_noise, **_variant_kw(smoothrast, smoothagg))
@@ -258,8 +259,9 @@ class RandomSimpleShader(_RandomShaderBase):
             sr, sa = self.smoothrast, self.smoothagg
             if _multidevice.sample_devices() is not None and _noise.get_noise_source() == "philox":
                 # samples split over the devices of set_sample_devices (in-process RCCL collectives)
+                zbuf, _ = _blend.plane_link(fragments.zbuf, znear, zfar, fragments.pix_to_face)
                 return _multidevice.sharded_blend(
-                    fragments.bary_coords, fragments.pix_to_face, fragments.dists, fragments.zbuf, sr.sigma,
+                    fragments.bary_coords, fragments.pix_to_face, fragments.dists, zbuf, sr.sigma,
                     sa.gamma, sa.alpha, sr.nb_samples, sa.nb_samples, eps=sa.eps,
                     background=blend_params.background_color, znear=znear, zfar=zfar, fixed_noise=sa.fixed_noise,
                     vert_colors=vc, faces=meshes.faces_packed(), **_variant_kw(sr, sa))
