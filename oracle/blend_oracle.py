@@ -135,10 +135,11 @@ def plane_grads(zbuf, zfar, znear, mask, dz_inv):
     """d znear, d zfar (each (N,1,1,1)) of smoothagg.py:198's z_inv = (zfar - zbuf) / (zfar - znear)
     * mask given dL/dz_inv: torch autograd of that expression, i.e. what the reference's graph
     gives camera planes that require grad (random_rasterizer.py:172-173)."""
-    zn = znear.detach().clone().requires_grad_(True)
-    zf = zfar.detach().clone().requires_grad_(True)
-    z_inv = (zf - zbuf) / (zf - zn) * mask
-    return torch.autograd.grad(z_inv, (zn, zf), dz_inv)
+    with torch.enable_grad():  # (also when called from an autograd Function's backward)
+        zn = znear.detach().clone().requires_grad_(True)
+        zf = zfar.detach().clone().requires_grad_(True)
+        z_inv = (zf - zbuf.detach()) / (zf - zn) * mask
+        return torch.autograd.grad(z_inv, (zn, zf), dz_inv.detach())
 
 
 def _prod_backward(x, g):

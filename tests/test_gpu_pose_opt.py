@@ -160,7 +160,9 @@ def test_kept_graphs_record_each_problems_losses(device, noise_type):
     assert kept["nb"] == fresh["nb"]
     if noise_type == "softras":
         np.testing.assert_allclose(kept["loss"][:20], fresh["loss"][:20], rtol=1e-4)
-        np.testing.assert_allclose(kept["gnorm"][:20], fresh["gnorm"][:20], rtol=1e-4)
+        # gradient norms: the backward's float-atomic sums differ run to run (~1e-4 relative on the
+        # small norms); a stale replay would differ by O(1)
+        np.testing.assert_allclose(kept["gnorm"][:20], fresh["gnorm"][:20], rtol=1e-3)
         assert abs(kept["loss"][:100].mean() - fresh["loss"][:100].mean()) < 1e-3 * fresh["loss"][:100].mean()
         assert abs(kept["angle"] - fresh["angle"]) < 0.5, (kept["angle"], fresh["angle"])
         np.testing.assert_allclose(kept["v"], fresh["v"], rtol=2e-2, atol=1e-9)
