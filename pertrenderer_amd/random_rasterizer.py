@@ -55,6 +55,13 @@ def _background_tensor(bg, device):
     return t
 
 
+def _bg_needs_grad(bg):
+    """A background colour tensor that requires grad: the reference's colour mix differentiates it
+    (random_rasterizer.py:39-43, 52); the native kernels take it as constants, so such calls take
+    the composition below (native rasterize / aggregate, torch colour mix)."""
+    return torch.is_tensor(bg) and bg.requires_grad and torch.is_grad_enabled()
+
+
 def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, znear=1.0, zfar=100, live_only=False):
     """(N,H,W,K,3) colours + Fragments -> (N,H,W,4) RGBA (random_rasterizer.py:34-56).  live_only (an
     extension, RandomPhongShader's): every consumer of the colours' and fragments' gradients reads the
@@ -62,7 +69,8 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
     N, H, W, K = fragments.pix_to_face.shape
     device = fragments.pix_to_face.device
     background = blend_params.background_color
-    if _is_fusable(smoothrast, smoothagg, fragments):
+    bg_grad = _bg_needs_grad(background)
+    if _is_fusable(smoothrast, smoothagg, fragments) and not bg_grad:
         if _multidevice.sample_devices() is not None and _noise.get_noise_source() == "philox":
             # samples split over the devices of set_sample_devices (in-process RCCL collectives)
             zbuf, _ = _blend.plane_link(fragments.zbuf, znear, zfar, fragments.pix_to_face)
@@ -76,7 +84,7 @@ def smooth_rgb_blend(colors, fragments, smoothrast, smoothagg, blend_params, zne
             smoothagg.gamma, smoothagg.alpha, smoothrast.nb_samples, smoothagg.nb_samples,
             eps=smoothagg.eps, background=background, znear=znear, zfar=zfar,
             fixed_noise=smoothagg.fixed_noise, live_only=live_only, **_variant_kw(smoothrast, smoothagg))
-    if type(smoothrast) is SoftRast and type(smoothagg) is SoftAgg and fragments.pix_to_face.is_cuda:
+    if type(smoothrast) is SoftRast and type(smoothagg) is SoftAgg and fragments.pix_to_face.is_cuda and not bg_grad:
         # eval.py's "softras" pair as one native kernel pair (PR_BLEND_SOFT)
         return _blend.soft_blend(colors, fragments.pix_to_face, fragments.dists, fragments.zbuf, smoothrast.sigma,
                                  smoothagg.gamma, smoothagg.alpha, eps=smoothagg.eps, background=background,
@@ -164,6 +172,8 @@ class RandomPhongShader(_RandomShaderBase):
                         or (type(self.smoothrast) is SoftRast and type(self.smoothagg) is SoftAgg))
         if not native_blend or kwargs.get("cameras", self.cameras) is None:
             return False
+        if _bg_needs_grad(kwargs.get("blend_params", self.blend_params).background_color):
+            return False  # the composition path reads every slot
         if not _native_ok_params(kwargs.get("lights", self.lights), kwargs.get("materials", self.materials)):
             return False
         tex = getattr(meshes, "textures", None)
@@ -192,13 +202,14 @@ class RandomPhongShader(_RandomShaderBase):
         # MeshRenderer says the fragments' sole consumer is its own rasterizer backward
         # (_pr_valid_only, takes_valid_only).  A direct shader(fragments, mesh) call gets the
         # reference's zero rows in d dists / d zbuf / d bary (random_rasterizer.py:46-47).
-        live_only = bool(kwargs.get("_pr_valid_only", False)) and (
+        live_only = bool(kwargs.get("_pr_valid_only", False)) and not _bg_needs_grad(blend_params.background_color) and (
             (_is_fusable(self.smoothrast, self.smoothagg, fragments) and _multidevice.sample_devices() is None)
             or (type(self.smoothrast) is SoftRast and type(self.smoothagg) is SoftAgg
                 and fragments.pix_to_face.is_cuda))
         znear, zfar = _planes_from(cameras, kwargs)
         sr, sa = self.smoothrast, self.smoothagg
-        if FUSE_PHONG and _is_fusable(sr, sa, fragments) and _multidevice.sample_devices() is None:
+        if (FUSE_PHONG and _is_fusable(sr, sa, fragments) and _multidevice.sample_devices() is None
+                and not _bg_needs_grad(blend_params.background_color)):
             # the shading fused into the blend's forward (PR_BLEND_PHONG): a slot is shaded only where
             # it wins a sample (no shading pass over every slot); the backward's shading chain rule
             # runs for those slots only (pr_shade_bwd skips zero d colours)
@@ -244,7 +255,8 @@ class RandomSimpleShader(_RandomShaderBase):
         fused into the native blend on one device (its gradients go to the rasterizer backward)."""
         return (_vertex_colors(meshes) is not None and isinstance(self.smoothrast, _PerturbedRast)
                 and isinstance(self.smoothagg, _PerturbedAgg) and _multidevice.sample_devices() is None
-                and kwargs.get("cameras", self.cameras) is not None)
+                and kwargs.get("cameras", self.cameras) is not None
+                and not _bg_needs_grad(kwargs.get("blend_params", self.blend_params).background_color))
 
     def forward(self, fragments, meshes, **kwargs):
         cameras = kwargs.get("cameras", self.cameras)
@@ -254,7 +266,8 @@ class RandomSimpleShader(_RandomShaderBase):
         blend_params = kwargs.get("blend_params", self.blend_params)
         znear, zfar = _planes_from(cameras, kwargs)
         vc = _vertex_colors(meshes)
-        if vc is not None and _is_fusable(self.smoothrast, self.smoothagg, fragments):
+        if (vc is not None and _is_fusable(self.smoothrast, self.smoothagg, fragments)
+                and not _bg_needs_grad(blend_params.background_color)):
             # TexturesVertex sampling fused into the blend (no (N,H,W,K,3) texel tensor)
             sr, sa = self.smoothrast, self.smoothagg
             if _multidevice.sample_devices() is not None and _noise.get_noise_source() == "philox":

@@ -1,4 +1,5 @@
-"""Gradients w.r.t. the camera planes znear / zfar when they are tensors that require grad.
+"""Gradients w.r.t. the camera planes znear / zfar, and the background colour, when they are
+tensors that require grad.
 
 The reference computes z_inv = (zfar - zbuf) / (zfar - znear) * mask in torch (smoothagg.py:198,
 planes from the cameras: random_rasterizer.py:172-173), so such planes get gradients there.  The
@@ -110,3 +111,48 @@ def test_constant_planes_add_no_node(device):
         zn = torch.ones((), device=device, requires_grad=True)
         out, linked = blend.plane_link(z, zn, 100.0, p2f)
         assert out is z and not linked
+
+
+@pytest.mark.parametrize("shader_kind", ["simple", "phong"])
+def test_background_gradient_matches_finite_difference(shader_kind, device):
+    """A background colour tensor that requires grad (the reference's colour mix differentiates it:
+    random_rasterizer.py:39-43, 52) takes the composition path, through MeshRenderer too.  The image
+    is linear in the background for fixed draws, so d L / d bg equals the difference quotient of
+    two renders with the same torch draws (one unit step per channel)."""
+    import math
+    import pertrenderer_amd as pa
+    from pertrenderer_amd import noise
+    from pertrenderer_amd.renderer import (FoVPerspectiveCameras, MeshRasterizer, PointLights,
+                                           RasterizationSettings, look_at_view_transform)
+    from pertrenderer_amd.renderer.renderer import MeshRenderer
+    from test_gpu_shading import _scene
+    mesh, _, _, _, mats, _, _, _ = _scene(device, "vertex")
+    R, T = look_at_view_transform(2.2, 25.0, 40.0, device=device)
+    cams = FoVPerspectiveCameras(R=R, T=T, device=device)
+    rs = RasterizationSettings(image_size=32, blur_radius=math.log(1e4 - 1) * 1e-3, faces_per_pixel=8)
+    sr, sa = pa.GaussianRast(nb_samples=4, sigma=1e-3), pa.GaussianAgg(nb_samples=4, gamma=1e-2)
+    if shader_kind == "simple":
+        shader = pa.RandomSimpleShader(device=device, cameras=cams, smoothrast=sr, smoothagg=sa)
+    else:
+        shader = pa.RandomPhongShader(device=device, cameras=cams, lights=PointLights(device=device),
+                                      materials=mats, smoothrast=sr, smoothagg=sa)
+    renderer = MeshRenderer(MeshRasterizer(cameras=cams, raster_settings=rs), shader)
+    G = torch.rand((1, 32, 32, 4), device=device, generator=torch.Generator(device).manual_seed(8))
+    old = noise.get_noise_source()
+    noise.set_noise_source("torch")
+    try:
+        def render(bg):
+            torch.manual_seed(13)
+            return renderer(mesh, blend_params=pa.random_rasterizer.BlendParams(1e-4, 1e-4, bg))
+        bg = torch.tensor([0.2, 0.3, 0.4], device=device, requires_grad=True)
+        img = render(bg)
+        (gbg,) = torch.autograd.grad((img * G).sum(), bg)
+        with torch.no_grad():
+            base = render(bg.detach())
+            assert_close(img.detach(), base, name="image (composition vs fused)")
+            fd = torch.stack([((render(bg.detach() + torch.eye(3, device=device)[c]) - base) * G).sum()
+                              for c in range(3)])
+    finally:
+        noise.set_noise_source(old)
+    assert float(fd.abs().max()) > 0
+    assert_close(gbg, fd, rtol=1e-4, atol_rel=1e-5, name="d background")
